@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: S3D-G + word2vec text tower, MIL-NCE, synthetic 16f x 200 x 200 clips,
+num_candidates=4, bf16, 256 clips per GPU (BASELINE.json configs 2 and 3).
+
+    python bench.py --gpus N --steps K --warmup W
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Each timed step is the full training step: on-device synthetic batch generation, forward of
+both towers, cross-GPU all-gather of embeddings, MIL-NCE on the global batch, backward with
+bucketed RCCL gradient all-reduce, fused Adam, LR schedule. Rank 0 prints ONE JSON line; the
+value is the whole-job aggregate video-text pairs/s (max step time over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch_per_gpu", type=int, default=256)
+    ap.add_argument("--num_frames", type=int, default=16)
+    ap.add_argument("--size", type=int, default=200)
+    ap.add_argument("--num_candidates", type=int, default=4)
+    ap.add_argument("--device", type=str, default="auto")
+    ap.add_argument("--blocks", type=str, default="")
+    ap.add_argument("--profile_steps", type=int, default=0, help="extra steps under torch profiler")
+    opts = ap.parse_args()
+
+    import torch
+    from mil_nce_howto100m_amd.config import get_args
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != opts.gpus and world == 1 and opts.gpus > 1:
+        print(f"warning: --gpus {opts.gpus} but WORLD_SIZE=1; launch with torch.distributed.run",
+              file=sys.stderr)
+    ctx = pdist.init_distributed("nccl", opts.device)
+    b = opts.batch_per_gpu
+    args = get_args(argv=["--batch_size", str(b * ctx.world_size), "--num_frames", str(opts.num_frames),
+                          "--video_size", str(opts.size), "--num_candidates", str(opts.num_candidates),
+                          "--warmup_steps", "10000", "--lr", "0.001", "--epochs", "150",
+                          "--word2vec_path", "", "--blocks", opts.blocks])
+    seed_everything(args.seed, ctx.rank)
+    data = SyntheticClips(b, opts.num_frames, opts.size, opts.num_candidates, args.max_words, args.vocab_size,
+                          seed=args.seed, device=ctx.device, rank=ctx.rank, world_size=ctx.world_size)
+    model = build_model(args, ctx.device)
+    trainer = Trainer(args, model, ctx, len(data))
+    cuda = ctx.device.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    step = 0
+    for _ in range(opts.warmup):
+        loss = trainer.train_step(data.batch(step))
+        step += 1
+    sync()
+    pdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    losses = []
+    for _ in range(opts.steps):
+        losses.append(trainer.train_step(data.batch(step)))
+        step += 1
+    sync()
+    pdist.barrier()
+    sync()
+    dt = time.perf_counter() - t0
+    dt = pdist.all_reduce_max(dt)
+    final_loss = float(losses[-1].item()) if losses else float("nan")
+    if opts.profile_steps and cuda:
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+            for _ in range(opts.profile_steps):
+                trainer.train_step(data.batch(step))
+                step += 1
+            sync()
+        if ctx.is_main:
+            os.makedirs("gpurun_out", exist_ok=True)
+            with open("gpurun_out/torch_profile.txt", "w") as f:
+                f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=80))
+    ms = 1000.0 * dt / max(1, opts.steps)
+    pairs = b * ctx.world_size * opts.steps / dt
+    if ctx.is_main:
+        peak = torch.cuda.max_memory_allocated() / 2 ** 30 if cuda else 0.0
+        out = {
+            "metric": "video-text pairs/sec/node (S3D-G MIL-NCE train step)",
+            "value": round(pairs, 2),
+            "unit": "pairs/s",
+            "n_gpus": ctx.world_size,
+            "steps": opts.steps,
+            "warmup": opts.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if cuda else "fp32",
+            "data": "synthetic (on-device generator, random-init weights)",
+            "config": {"model": "S3D-G + word2vec text tower, MIL-NCE",
+                       "global_batch": b * ctx.world_size, "seq_len": opts.num_frames,
+                       "frames": opts.num_frames, "resolution": opts.size,
+                       "num_candidates": opts.num_candidates,
+                       "parallelism": f"dp{ctx.world_size}"},
+            "final_loss": round(final_loss, 4),
+            "peak_mem_gib": round(peak, 2),
+        }
+        print(json.dumps(out), flush=True)
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,248 @@
+// Train-mode BatchNorm3d + ReLU around the implicit-GEMM conv (channels-last, bf16 data).
+//
+// forward : conv epilogue partial sums --(bn_finalize)--> mean/invstd/scale/shift + running
+//           stats update (momentum 0.1, unbiased running_var, num_batches_tracked += 1)
+//           --(bn_relu_apply)--> z = relu(y*scale + shift), optionally also accumulating the
+//           per-(clip, channel) sum of z that the following SelfGating needs (its global mean),
+//           so the gate never re-reads z for the mean.
+// backward: bn_bwd_reduce (sum dz*mask, sum dz*mask*xhat per channel, mask = z > 0 recomputed
+//           from y) -> bn_bwd_finalize (dgamma, dbeta, coefficients) -> bn_bwd_apply
+//           dy = gamma*invstd*(dz*mask - dbeta/n - xhat*dgamma/n).
+// All elementwise passes move 16 B per lane (8 bf16).
+#include "common.h"
+
+// ---------------------------------------------------------------------------------------
+__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, int Npad, int C, double count,
+                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                   float* __restrict__ rmean, float* __restrict__ rvar,
+                                   long long* __restrict__ nbt, float momentum, float eps, int training,
+                                   float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (training && c == 0 && nbt != nullptr) nbt[0] += 1;
+  if (c >= C) return;
+  float mean, var;
+  if (training) {
+    double s = 0.0, q = 0.0;
+    for (int i = 0; i < nparts; ++i) {
+      s += (double)part[(long long)i * 2 * Npad + c];
+      q += (double)part[(long long)i * 2 * Npad + Npad + c];
+    }
+    const double m = s / count;
+    double v = q / count - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+    const double unbiased = count > 1.0 ? v * count / (count - 1.0) : v;
+    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  const float invstd = rsqrtf(var + eps);
+  const float sc = gamma[c] * invstd;
+  out[c] = mean;
+  out[C + c] = invstd;
+  out[2 * C + c] = sc;
+  out[3 * C + c] = beta[c] - mean * sc;
+}
+
+// ---------------------------------------------------------------------------------------
+// z = relu(y*scale + shift). Grid (splits, B): block handles rows of one clip so the gating
+// channel sums can be reduced in LDS and committed with one atomic per channel per block.
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(
+    const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
+    int C, int rows_per_b, int rows_per_block, float* __restrict__ gsum) {
+  __shared__ float red[256 * 8];
+  const int cpr = C >> 3;
+  const int rpi = 256 / cpr;  // rows per iteration
+  const int tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < rpi;
+  const int b = blockIdx.y;
+  const int r_begin = blockIdx.x * rows_per_block;
+  const int r_end = min(rows_per_b, r_begin + rows_per_block);
+  const int c0 = cc * 8;
+  float sc[8], sh[8], acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = active ? ss[2 * C + c0 + k] : 0.f;
+    sh[k] = active ? ss[3 * C + c0 + k] : 0.f;
+    acc[k] = 0.f;
+  }
+  if (active) {
+    const long long base = (long long)b * rows_per_b;
+    for (int r = r_begin + rr; r < r_end; r += rpi) {
+      const long long row = base + r;
+      uint4 v = *(const uint4*)(y + row * ldy + c0);
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
+        acc[k] += f[k];
+      }
+      *(uint4*)(z + row * ldz + c0) = pack8(f);
+    }
+  }
+  if (gsum == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
+  __syncthreads();
+  // first row-group sums the others for its channel chunk
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s = acc[k];
+      for (int j = 1; j < rpi; ++j) s += red[k * 256 + j * cpr + cc];
+      atomicAdd(gsum + (long long)b * C + c0 + k, s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-channel partials of sum(dz*mask) and sum(dz*mask*xhat) -> part[blk][2][C]
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dz, int ldz, const bf16_t* __restrict__ y, int ldy,
+    const float* __restrict__ ss, int C, long long M, int rows_per_block, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int cpr = C >> 3;
+  const int rpi = 256 / cpr;
+  const int tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < rpi;
+  const int c0 = cc * 8;
+  const long long r_begin = (long long)blockIdx.x * rows_per_block;
+  const long long r_end = min(M, r_begin + rows_per_block);
+  float mean[8], istd[8], sc[8], sh[8], a1[8], a2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = active ? ss[c0 + k] : 0.f;
+    istd[k] = active ? ss[C + c0 + k] : 0.f;
+    sc[k] = active ? ss[2 * C + c0 + k] : 0.f;
+    sh[k] = active ? ss[3 * C + c0 + k] : 0.f;
+    a1[k] = 0.f;
+    a2[k] = 0.f;
+  }
+  if (active) {
+    for (long long r = r_begin + rr; r < r_end; r += rpi) {
+      float g[8], v[8];
+      unpack8(*(const uint4*)(dz + r * ldz + c0), g);
+      unpack8(*(const uint4*)(y + r * ldy + c0), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? g[k] : 0.f;
+        a1[k] += gm;
+        a2[k] += gm * (v[k] - mean[k]) * istd[k];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = a1[k];
+  __syncthreads();
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s = a1[k];
+      for (int j = 1; j < rpi; ++j) s += red[k * 256 + j * cpr + cc];
+      part[(long long)blockIdx.x * 2 * C + c0 + k] = s;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = a2[k];
+  __syncthreads();
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s = a2[k];
+      for (int j = 1; j < rpi; ++j) s += red[k * 256 + j * cpr + cc];
+      part[(long long)blockIdx.x * 2 * C + C + c0 + k] = s;
+    }
+  }
+}
+
+// coef[4][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n, unused}; dgamma/dbeta accumulated into grads.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C, double count,
+                                       const float* __restrict__ gamma, const float* __restrict__ ss,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = 0; i < nparts; ++i) {
+    s1 += part[(long long)i * 2 * C + c];
+    s2 += part[(long long)i * 2 * C + C + c];
+  }
+  dbeta[c] = (float)s1;
+  dgamma[c] = (float)s2;
+  coef[c] = gamma[c] * ss[C + c];
+  coef[C + c] = (float)(s1 / count);
+  coef[2 * C + c] = (float)(s2 / count);
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
+    const bf16_t* __restrict__ dz, int ldz, const bf16_t* __restrict__ y, int ldy,
+    const float* __restrict__ ss, const float* __restrict__ coef, int C, long long nchunks,
+    bf16_t* __restrict__ dy) {
+  const int cpr = C >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nchunks;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cpr;
+    const int c0 = (int)(i - r * cpr) * 8;
+    float g[8], v[8], o[8];
+    unpack8(*(const uint4*)(dz + r * ldz + c0), g);
+    unpack8(*(const uint4*)(y + r * ldy + c0), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      const float sc = ss[2 * C + c], sh = ss[3 * C + c];
+      const float gm = (v[k] * sc + sh > 0.f) ? g[k] : 0.f;
+      const float xh = (v[k] - ss[c]) * ss[C + c];
+      o[k] = coef[c] * (gm - coef[C + c] - xh * coef[2 * C + c]);
+    }
+    *(uint4*)(dy + r * C + c0) = pack8(o);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+MILNCE_API int milnce_bn_finalize(const float* part, int nparts, int Npad, int C, double count, const float* gamma,
+                                  const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
+                                  float eps, int training, float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nparts, Npad, C,
+                     count, gamma, beta, rmean, rvar, nbt, momentum, eps, training, out);
+  return (int)hipGetLastError();
+}
+
+static int pick_splits(long long rows, int target_rows) {
+  long long s = (rows + target_rows - 1) / target_rows;
+  return (int)(s < 1 ? 1 : s);
+}
+
+MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, const float* ss, int C, int B,
+                                    int rows_per_b, float* gsum, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int splits = pick_splits(rows_per_b, 512);
+  const int rpb = (rows_per_b + splits - 1) / splits;
+  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy,
+                     (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, gsum);
+  return (int)hipGetLastError();
+}
+
+// part must hold nblocks*2*C floats; nblocks = ceil(M / rows_per_block) (queried with part == null).
+MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
+                             const float* gamma, float* part, int nparts, float* dgamma, float* dbeta,
+                             float* coef, void* dy, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int rows_per_block = (int)((M + nparts - 1) / nparts);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
+                     (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nparts, C,
+                     (double)M, gamma, ss, dgamma, dbeta, coef);
+  const long long nchunks = M * (C / 8);
+  long long grid = (nchunks + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((int)grid), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
+                     (const bf16_t*)y, ldy, ss, coef, C, nchunks, (bf16_t*)dy);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,91 @@
+// Shared helpers for the MI355X (gfx950 / CDNA4) kernels of libmilnce_hip.so.
+// All kernels are written for wave64 and the gfx950 MFMA / LDS model; nothing here is
+// portable to other targets on purpose.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MILNCE_API extern "C" __attribute__((visibility("default")))
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;  // lowers to v_cvt_pk_bf16_f32 (RNE, NaN-preserving) on gfx950
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+// Unpack 8 bf16 held in a uint4 to floats.
+__device__ __forceinline__ void unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 v;
+  v.x = pack2bf(f[0], f[1]); v.y = pack2bf(f[2], f[3]);
+  v.z = pack2bf(f[4], f[5]); v.w = pack2bf(f[6], f[7]);
+  return v;
+}
+
+// Fast unsigned division by a runtime-invariant divisor (dividend < 2^31).
+struct FastDiv {
+  uint32_t d, mul, shr;
+};
+
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  if (d == 1) { f.mul = 0; f.shr = 0; return f; }
+  uint32_t l = 0;
+  while ((1u << l) < d) ++l;  // ceil(log2 d)
+  uint32_t p = 31 + l;
+  uint64_t m = ((1ull << p) + d - 1) / d;
+  f.mul = (uint32_t)m;
+  f.shr = p - 32;
+  return f;
+}
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return f.d == 1 ? n : (__umulhi(n, f.mul) >> f.shr);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// XCD-aware bijective remap of a 1-D block id (cdna_hip_programming.md §5, T1): blocks that
+// the dispatcher deals to the same XCD (id % 8 equal) get a contiguous range of logical ids.
+__device__ __forceinline__ int xcd_remap(int id, int nblocks) {
+  const int q = nblocks / 8, r = nblocks % 8;
+  const int xcd = id % 8, slot = id / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
+}
+
+#define HIP_RET(expr)                           \
+  do {                                          \
+    hipError_t _e = (expr);                     \
+    if (_e != hipSuccess) return (int)_e;       \
+  } while (0)

@@ -1,0 +1,309 @@
+// SelfGating (s3dg.py:47-59) fused with the Inception channel concat (s3dg.py:45), plus the
+// global average pool (s3dg.py:323).
+//
+// forward : the per-(clip, channel) sums of every branch come for free from the BN-apply
+//           epilogue (bn.hip); gate_fc turns them into g = sigmoid(W * mean + b) (one block
+//           per clip and branch), gate_scale writes z_i * g_i straight into its channel slice of
+//           the concatenated block output (no separate th.cat pass).
+// backward: gate_bwd_reduce  dg[b, c] = sum_thw dout * z      (all branches, one launch)
+//           gate_bwd_small   dpre = dg*g*(1-g); dmean = dpre W; dW = dpre^T mean; db = sum_b dpre
+//           gate_bwd_apply   dz_i = dout_i * g_i + dmean_i / THW   (all branches, one launch)
+#include "common.h"
+
+#define MAXSEG 4
+
+struct SegTable {
+  int nseg;
+  int off[MAXSEG + 1];      // channel offsets in the concat row (off[nseg] = Ctot)
+  const bf16_t* z[MAXSEG];  // branch activations [B*THW, C_i]
+  bf16_t* dz[MAXSEG];       // branch grads (backward)
+  const float* w[MAXSEG];   // fc weight [C_i, C_i]
+  const float* bias[MAXSEG];
+  float* dw[MAXSEG];
+  float* db[MAXSEG];
+};
+
+__device__ __forceinline__ int seg_of(const SegTable& t, int c) {
+  int s = 0;
+#pragma unroll
+  for (int k = 1; k < MAXSEG; ++k) s += (k < t.nseg && c >= t.off[k]) ? 1 : 0;
+  return s;
+}
+
+// gsum/g/mean are [B, Ctot] fp32 (branch i at columns off[i]..off[i+1]).
+__global__ void gate_fc_kernel(SegTable t, const float* __restrict__ gsum, float inv_thw, int Ctot,
+                               float* __restrict__ mean, float* __restrict__ g) {
+  const int b = blockIdx.x, s = blockIdx.y;
+  if (s >= t.nseg) return;
+  const int c0 = t.off[s], C = t.off[s + 1] - c0;
+  extern __shared__ float m[];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float v = gsum[(long long)b * Ctot + c0 + c] * inv_thw;
+    m[c] = v;
+    mean[(long long)b * Ctot + c0 + c] = v;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float* wr = t.w[s] + (long long)c * C;
+    float a = t.bias[s][c];
+    for (int k = 0; k < C; ++k) a += wr[k] * m[k];
+    g[(long long)b * Ctot + c0 + c] = 1.f / (1.f + __expf(-a));
+  }
+}
+
+// out[row, c] = z_seg[row, c - off] * g[b, c]
+__global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float* __restrict__ g, int Ctot,
+                                                         long long rows, int thw, bf16_t* __restrict__ out) {
+  const int cpr = Ctot >> 3;
+  const long long n = rows * cpr;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cpr;
+    const int c = (int)(i - r * cpr) * 8;
+    const int s = seg_of(t, c);
+    const int C = t.off[s + 1] - t.off[s];
+    const int b = (int)(r / thw);
+    float f[8];
+    unpack8(*(const uint4*)(t.z[s] + r * C + (c - t.off[s])), f);
+    const float* gg = g + (long long)b * Ctot + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] *= gg[k];
+    *(uint4*)(out + r * Ctot + c) = pack8(f);
+  }
+}
+
+// dg[b, c] += sum over this block's rows of dout[r, c] * z[r, c]   (grid: splits x B)
+__global__ __launch_bounds__(256) void gate_bwd_reduce_kernel(SegTable t, const bf16_t* __restrict__ dout,
+                                                              int Ctot, int thw, int rows_per_block,
+                                                              float* __restrict__ dg) {
+  __shared__ float red[256 * 8];
+  const int cpr = Ctot >> 3;
+  const int tid = threadIdx.x;
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  const int b = blockIdx.y;
+  const int r_begin = blockIdx.x * rows_per_block;
+  const int r_end = min(thw, r_begin + rows_per_block);
+  // threads sweep (row, chunk) pairs; each thread owns a fixed chunk when cpr divides 256,
+  // otherwise chunks rotate -- accumulate per (chunk) through LDS at the end.
+  const int groups = 256 / cpr;  // >= 1 since Ctot <= 2048
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < groups;
+  const int c = cc * 8;
+  int s = 0, C = 0;
+  if (active) { s = seg_of(t, c); C = t.off[s + 1] - t.off[s]; }
+  if (active) {
+    for (int r = r_begin + rr; r < r_end; r += groups) {
+      const long long row = (long long)b * thw + r;
+      float d[8], z[8];
+      unpack8(*(const uint4*)(dout + row * Ctot + c), d);
+      unpack8(*(const uint4*)(t.z[s] + row * C + (c - t.off[s])), z);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += d[k] * z[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
+  __syncthreads();
+  if (active && rr == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[k];
+      for (int j = 1; j < groups; ++j) v += red[k * 256 + j * cpr + cc];
+      atomicAdd(dg + (long long)b * Ctot + c + k, v);
+    }
+  }
+}
+
+// per segment: dpre[b,c] = dg*g*(1-g) (in place in dg), dmean[b,c] = sum_k dpre[b,k] W[k,c]
+__global__ void gate_bwd_dmean_kernel(SegTable t, float* __restrict__ dg, const float* __restrict__ g,
+                                      int Ctot, float* __restrict__ dmean) {
+  const int b = blockIdx.x, s = blockIdx.y;
+  if (s >= t.nseg) return;
+  const int c0 = t.off[s], C = t.off[s + 1] - c0;
+  extern __shared__ float dp[];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const long long i = (long long)b * Ctot + c0 + c;
+    const float gg = g[i];
+    const float v = dg[i] * gg * (1.f - gg);
+    dp[c] = v;
+    dg[i] = v;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    float a = 0.f;
+    for (int k = 0; k < C; ++k) a += dp[k] * t.w[s][(long long)k * C + c];
+    dmean[(long long)b * Ctot + c0 + c] = a;
+  }
+}
+
+// dW[c, k] += sum_b dpre[b, c] * mean[b, k];  db[c] += sum_b dpre[b, c]
+__global__ void gate_bwd_dw_kernel(SegTable t, const float* __restrict__ dpre, const float* __restrict__ mean,
+                                   int Ctot, int B) {
+  const int s = blockIdx.z;
+  if (s >= t.nseg) return;
+  const int c0 = t.off[s], C = t.off[s + 1] - c0;
+  const int c = blockIdx.y;
+  if (c >= C) return;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < C; k += gridDim.x * blockDim.x) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dpre[(long long)b * Ctot + c0 + c] * mean[(long long)b * Ctot + c0 + k];
+    t.dw[s][(long long)c * C + k] += a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += dpre[(long long)b * Ctot + c0 + c];
+    t.db[s][c] += a;
+  }
+}
+
+// dz_seg[r, c] = dout[r, c] * g[b, c] + dmean[b, c] * inv_thw
+__global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ g,
+                                                             const float* __restrict__ dmean, int Ctot,
+                                                             long long rows, int thw, float inv_thw) {
+  const int cpr = Ctot >> 3;
+  const long long n = rows * cpr;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cpr;
+    const int c = (int)(i - r * cpr) * 8;
+    const int s = seg_of(t, c);
+    const int C = t.off[s + 1] - t.off[s];
+    const int b = (int)(r / thw);
+    float d[8];
+    unpack8(*(const uint4*)(dout + r * Ctot + c), d);
+    const long long gi = (long long)b * Ctot + c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = d[k] * g[gi + k] + dmean[gi + k] * inv_thw;
+    *(uint4*)(t.dz[s] + r * C + (c - t.off[s])) = pack8(d);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// global average pool over THW: x [B*THW, C] bf16 -> out [B, C] fp32 (atomics into zeroed out)
+__global__ __launch_bounds__(256) void avgpool_kernel(const bf16_t* __restrict__ x, int C, int thw,
+                                                      int rows_per_block, float inv, float* __restrict__ out) {
+  __shared__ float red[256 * 8];
+  const int cpr = C >> 3, groups = 256 / cpr, tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < groups;
+  const int b = blockIdx.y;
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
+  float acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+  if (active) {
+    for (int r = r_begin + rr; r < r_end; r += groups) {
+      float f[8];
+      unpack8(*(const uint4*)(x + ((long long)b * thw + r) * C + cc * 8), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[k] += f[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
+  __syncthreads();
+  if (active && rr == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[k];
+      for (int j = 1; j < groups; ++j) v += red[k * 256 + j * cpr + cc];
+      atomicAdd(out + (long long)b * C + cc * 8 + k, v * inv);
+    }
+  }
+}
+
+__global__ void avgpool_bwd_kernel(const float* __restrict__ dout, int C, int thw, long long rows, float inv,
+                                   bf16_t* __restrict__ dx) {
+  const int cpr = C >> 3;
+  const long long n = rows * cpr;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / cpr;
+    const int c = (int)(i - r * cpr) * 8;
+    const int b = (int)(r / thw);
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f[k] = dout[(long long)b * C + c + k] * inv;
+    *(uint4*)(dx + r * C + c) = pack8(f);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+static SegTable make_table(int nseg, const int* widths, const void* const* z, void* const* dz,
+                           const float* const* w, const float* const* bias, float* const* dw, float* const* db) {
+  SegTable t;
+  t.nseg = nseg;
+  t.off[0] = 0;
+  for (int i = 0; i < MAXSEG; ++i) {
+    const bool v = i < nseg;
+    t.off[i + 1] = t.off[i] + (v ? widths[i] : 0);
+    t.z[i] = v && z ? (const bf16_t*)z[i] : nullptr;
+    t.dz[i] = v && dz ? (bf16_t*)dz[i] : nullptr;
+    t.w[i] = v && w ? w[i] : nullptr;
+    t.bias[i] = v && bias ? bias[i] : nullptr;
+    t.dw[i] = v && dw ? dw[i] : nullptr;
+    t.db[i] = v && db ? db[i] : nullptr;
+  }
+  return t;
+}
+
+static int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z, const float* const* w,
+                               const float* const* bias, const float* gsum, int B, int thw, float* mean, float* g,
+                               void* out, hipStream_t stream) {
+  SegTable t = make_table(nseg, widths, z, nullptr, w, bias, nullptr, nullptr);
+  const int Ctot = t.off[nseg];
+  int cmax = 0;
+  for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
+  hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum,
+                     1.f / thw, Ctot, mean, g);
+  const long long rows = (long long)B * thw;
+  hipLaunchKernelGGL(gate_scale_kernel, dim3(grid_for(rows * (Ctot / 8))), dim3(256), 0, stream, t, g, Ctot, rows,
+                     thw, (bf16_t*)out);
+  return (int)hipGetLastError();
+}
+
+// dg and dmean are [B, Ctot] fp32 scratch (dg zeroed by the caller)
+MILNCE_API int milnce_gate_bwd(int nseg, const int* widths, const void* const* z, void* const* dz,
+                               const float* const* w, float* const* dw, float* const* db, const void* dout,
+                               const float* g, const float* mean, int B, int thw, float* dg, float* dmean,
+                               hipStream_t stream) {
+  SegTable t = make_table(nseg, widths, z, dz, w, nullptr, dw, db);
+  const int Ctot = t.off[nseg];
+  int cmax = 0;
+  for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
+  const int splits = (thw + 511) / 512;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, Ctot,
+                     thw, rpb, dg);
+  hipLaunchKernelGGL(gate_bwd_dmean_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, dg, g, Ctot,
+                     dmean);
+  hipLaunchKernelGGL(gate_bwd_dw_kernel, dim3((cmax + 255) / 256, cmax, nseg), dim3(256), 0, stream, t, dg, mean,
+                     Ctot, B);
+  const long long rows = (long long)B * thw;
+  hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(grid_for(rows * (Ctot / 8))), dim3(256), 0, stream, t,
+                     (const bf16_t*)dout, g, dmean, Ctot, rows, thw, 1.f / thw);
+  return (int)hipGetLastError();
+}
+
+MILNCE_API int milnce_avgpool(const void* x, int B, int thw, int C, float* out, hipStream_t stream) {
+  const int splits = (thw + 255) / 256;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(avgpool_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)x, C, thw, rpb,
+                     1.f / thw, out);
+  return (int)hipGetLastError();
+}
+
+MILNCE_API int milnce_avgpool_bwd(const float* dout, int B, int thw, int C, void* dx, hipStream_t stream) {
+  const long long rows = (long long)B * thw;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(grid_for(rows * (C / 8))), dim3(256), 0, stream, dout, C, thw, rows,
+                     1.f / thw, (bf16_t*)dx);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,201 @@
+// Small fused kernels around the model:
+//   * fused Adam over the flat fp32 parameter / moment buffers (one launch for all params,
+//     all-reduce scale folded in), torch.optim.Adam arithmetic;
+//   * on-device synthetic clip generator (uint8 NDHWC4), bit-compatible with data/synthetic.py;
+//   * stem input conversion from the reference clip layout [B,3,T,H,W] (uint8 or float in
+//     [0,1]) to the stem's [B,T,H,W,4] operand layout;
+//   * text tower ReLU + max-over-words (s3dg.py:201-202) with arg-max for the backward.
+#include "common.h"
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long long n,
+                                                   float lr, float b1, float b2, float eps, float wd, float bc1,
+                                                   float sqrt_bc2, float gscale) {
+  const long long n4 = n >> 2;
+  const float step = lr / bc1;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
+       i += (long long)gridDim.x * blockDim.x) {
+    float4 pp = ((float4*)p)[i], gg = ((const float4*)g)[i], mm = ((float4*)m)[i], vv = ((float4*)v)[i];
+    float* pa = (float*)&pp; float* ga = (float*)&gg; float* ma = (float*)&mm; float* va = (float*)&vv;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float gk = ga[k] * gscale;
+      if (wd != 0.f) gk += wd * pa[k];
+      ma[k] = b1 * ma[k] + (1.f - b1) * gk;
+      va[k] = b2 * va[k] + (1.f - b2) * gk * gk;
+      const float denom = sqrtf(va[k]) / sqrt_bc2 + eps;
+      pa[k] -= step * ma[k] / denom;
+    }
+    ((float4*)p)[i] = pp; ((float4*)m)[i] = mm; ((float4*)v)[i] = vv;
+  }
+  // tail
+  const long long t = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && t < n && threadIdx.x < 4) {
+    float gk = g[t] * gscale;
+    if (wd != 0.f) gk += wd * p[t];
+    m[t] = b1 * m[t] + (1.f - b1) * gk;
+    v[t] = b2 * v[t] + (1.f - b2) * gk * gk;
+    p[t] -= step * m[t] / (sqrtf(v[t]) / sqrt_bc2 + eps);
+  }
+}
+
+MILNCE_API int milnce_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float b1, float b2,
+                           float eps, float wd, float bc1, float bc2, float gscale, hipStream_t stream) {
+  long long grid = ((n >> 2) + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(adam_kernel, dim3((int)grid), dim3(256), 0, stream, p, g, m, v, n, lr, b1, b2, eps, wd, bc1,
+                     sqrtf(bc2), gscale);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x = ((x >> 16) ^ x) * 0x45d9f3bu;
+  x = ((x >> 16) ^ x) * 0x45d9f3bu;
+  return ((x >> 16) ^ x) & 0x7fffffffu;
+}
+
+__global__ __launch_bounds__(256) void synth_video_kernel(const int* __restrict__ labels, const int* __restrict__ ids,
+                                                          int T, int S, uint32_t* __restrict__ out, long long npix) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix;
+       i += (long long)gridDim.x * blockDim.x) {
+    long long r = i;
+    const int x = r % S; r /= S;
+    const int y = r % S; r /= S;
+    const int t = r % T;
+    const int b = (int)(r / T);
+    const float lab = (float)labels[b];
+    const float freq = 0.05f + 0.01f * fmodf(lab, 7.f);
+    const float drift = 0.5f + 0.25f * fmodf(lab, 5.f);
+    const uint32_t h = mix32((uint32_t)ids[b] * 65537u + ((uint32_t)t * S + y) * S + x);
+    const float noise = (float)(h % 64u) - 32.f;
+    uint32_t px = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const float color = 64.f + 48.f * fmodf(lab * 3.f + ch * 5.f, 4.f);
+      const float wave = sinf(freq * ((float)x + (float)y * (1.f + 0.1f * ch)) + drift * (float)t);
+      float v = color + 60.f * wave + noise;
+      v = fminf(fmaxf(v, 0.f), 255.f);
+      px |= ((uint32_t)v & 0xffu) << (8 * ch);
+    }
+    out[i] = px;
+  }
+}
+
+MILNCE_API int milnce_synth_video(const int* labels, const int* ids, int B, int T, int S, void* out,
+                                  hipStream_t stream) {
+  const long long npix = (long long)B * T * S * S;
+  long long grid = (npix + 255) / 256;
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(synth_video_kernel, dim3((int)grid), dim3(256), 0, stream, labels, ids, T, S,
+                     (uint32_t*)out, npix);
+  return (int)hipGetLastError();
+}
+
+// [B,3,T,H,W] -> [B,T,H,W,4] uint8 (src_kind 0) or [B,T,H,W,8] bf16 (1: float32 in [0,1], 2: bf16;
+// 8 channels so the bf16 operand load stays 16-B wide; channels 3..7 are zero).
+__global__ void stem_prep_kernel(const void* __restrict__ src, int kind, int T, int H, int W, void* __restrict__ dst,
+                                 long long npix) {
+  const long long plane = (long long)T * H * W;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / plane, s = i - b * plane;
+    if (kind == 0) {
+      const uint8_t* u = (const uint8_t*)src;
+      const uint32_t v = (uint32_t)u[(b * 3 + 0) * plane + s] | ((uint32_t)u[(b * 3 + 1) * plane + s] << 8) |
+                         ((uint32_t)u[(b * 3 + 2) * plane + s] << 16);
+      ((uint32_t*)dst)[i] = v;
+    } else {
+      float f[3];
+      for (int c = 0; c < 3; ++c)
+        f[c] = kind == 1 ? ((const float*)src)[(b * 3 + c) * plane + s]
+                         : bf2f(((const bf16_t*)src)[(b * 3 + c) * plane + s]);
+      uint4 o;
+      o.x = pack2bf(f[0], f[1]);
+      o.y = pack2bf(f[2], 0.f);
+      o.z = 0u;
+      o.w = 0u;
+      ((uint4*)dst)[i] = o;
+    }
+  }
+}
+
+MILNCE_API int milnce_stem_prep(const void* src, int kind, int B, int T, int H, int W, void* dst, hipStream_t stream) {
+  const long long npix = (long long)B * T * H * W;
+  long long grid = (npix + 255) / 256;
+  if (grid > 16384) grid = 16384;
+  hipLaunchKernelGGL(stem_prep_kernel, dim3((int)grid), dim3(256), 0, stream, src, kind, T, H, W, dst, npix);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// h [N, Wd, F] bf16 -> out [N, F] fp32 = max_w relu(h); arg [N, F] uint8 (first max)
+__global__ void text_relu_max_kernel(const bf16_t* __restrict__ h, int Wd, int F, float* __restrict__ out,
+                                     uint8_t* __restrict__ arg, long long nchunks) {
+  const int cpr = F >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nchunks;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long n = i / cpr;
+    const int f0 = (int)(i - n * cpr) * 8;
+    float best[8];
+    uint32_t bi[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int w = 0; w < Wd; ++w) {
+      float v[8];
+      unpack8(*(const uint4*)(h + ((n * Wd + w) * F + f0)), v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float r = fmaxf(v[k], 0.f);
+        if (r > best[k]) { best[k] = r; bi[k] = w; }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      out[n * F + f0 + k] = best[k];
+      arg[n * F + f0 + k] = (uint8_t)bi[k];
+    }
+  }
+}
+
+// dh [N, Wd, F] bf16: dout at the arg-max word where the max was positive (ReLU active), else 0
+__global__ void text_relu_max_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ out,
+                                         const uint8_t* __restrict__ arg, int Wd, int F, bf16_t* __restrict__ dh,
+                                         long long nchunks) {
+  const int cpr = F >> 3;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nchunks;
+       i += (long long)gridDim.x * blockDim.x) {
+    // i indexes (n, w, chunk)
+    const long long nw = i / cpr;
+    const int f0 = (int)(i - nw * cpr) * 8;
+    const long long n = nw / Wd;
+    const int w = (int)(nw - n * Wd);
+    float g[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const long long o = n * F + f0 + k;
+      g[k] = (arg[o] == w && out[o] > 0.f) ? dout[o] : 0.f;
+    }
+    *(uint4*)(dh + i * 8) = pack8(g);
+  }
+}
+
+MILNCE_API int milnce_text_relu_max(const void* h, int N, int Wd, int F, float* out, void* arg, hipStream_t stream) {
+  const long long n = (long long)N * (F / 8);
+  long long grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(text_relu_max_kernel, dim3((int)grid), dim3(256), 0, stream, (const bf16_t*)h, Wd, F, out,
+                     (uint8_t*)arg, n);
+  return (int)hipGetLastError();
+}
+
+MILNCE_API int milnce_text_relu_max_bwd(const float* dout, const float* out, const void* arg, int N, int Wd, int F,
+                                        void* dh, hipStream_t stream) {
+  const long long n = (long long)N * Wd * (F / 8);
+  long long grid = (n + 255) / 256;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(text_relu_max_bwd_kernel, dim3((int)grid), dim3(256), 0, stream, dout, out,
+                     (const uint8_t*)arg, Wd, F, (bf16_t*)dh, n);
+  return (int)hipGetLastError();
+}

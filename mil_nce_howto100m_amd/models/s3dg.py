@@ -1,0 +1,236 @@
+"""S3D-G video tower + word2vec text tower (the reference model, ``s3dg.py:11-328``).
+
+Parameter/buffer names, shapes, default init and ``state_dict`` keys are identical to the
+reference (``nn.Conv3d``/``nn.BatchNorm3d``/``nn.Linear`` are used as parameter containers),
+so checkpoints load in both directions. The *execution* is different:
+
+  * activations are channels-last ``[B, T, H, W, C]`` (bf16 on GPU) end to end;
+  * every ``STConv3D`` unit (conv -> BN(train stats) -> ReLU, ``s3dg.py:107-111``) is one fused
+    op; on GPU it is an MFMA implicit-GEMM conv whose epilogue emits BN partial statistics;
+  * the four ``SelfGating`` modules of an Inception block and its ``th.cat`` (``s3dg.py:38-45``)
+    are one op that writes each gated branch into its channel slice of the block output;
+  * the stem consumes uint8 clips directly (``/255`` is folded into the conv's operand load).
+
+"Separable" is the reference's full-channel (2+1)D factorisation — a ``1 x k x k`` conv
+followed by a ``k x 1 x 1`` conv, both Cin->Cout dense (``s3dg.py:74-99``), not depthwise.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .text import SentenceEmbedding
+
+
+def _triple(v) -> Tuple[int, int, int]:
+    if isinstance(v, (list, tuple)):
+        assert len(v) == 3
+        return tuple(int(a) for a in v)
+    return (int(v),) * 3
+
+
+class STConv3D(nn.Module):
+    """conv -> BN -> ReLU [-> temporal conv -> BN -> ReLU] (``s3dg.py:61-111``)."""
+
+    def __init__(self, input_dim, output_dim, kernel_size, stride=1, padding=0, separable=False):
+        super().__init__()
+        assert len(kernel_size) == 3
+        self.separable = separable
+        k = _triple(kernel_size)
+        s = _triple(stride)
+        p = _triple(padding)
+        if separable:
+            # s3dg.py:74-99 ; the k[0]==1 separable case NameErrors in the reference and is unused.
+            assert k[0] != 1
+            self.k1, self.s1, self.p1 = (1, k[1], k[2]), (1, s[1], s[2]), (0, p[1], p[2])
+            self.k2, self.s2, self.p2 = (k[0], 1, 1), (s[0], 1, 1), (p[0], 0, 0)
+            self.conv1 = nn.Conv3d(input_dim, output_dim, self.k1, self.s1, self.p1, bias=False)
+            self.bn1 = nn.BatchNorm3d(output_dim)
+            self.conv2 = nn.Conv3d(output_dim, output_dim, self.k2, self.s2, self.p2, bias=False)
+            self.bn2 = nn.BatchNorm3d(output_dim)
+        else:
+            self.k1, self.s1, self.p1 = k, s, p
+            self.conv1 = nn.Conv3d(input_dim, output_dim, k, s, p, bias=False)
+            self.bn1 = nn.BatchNorm3d(output_dim)
+
+    def forward(self, x, want_gsum: bool = False):
+        """Returns z, or (z, per-(clip, channel) sum of z) when ``want_gsum`` (GPU path; the
+        sum feeds the following SelfGating's global mean for free)."""
+        if self.separable:
+            z = ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training)
+            return ops.conv_bn_relu(z, self.conv2.weight, self.bn2, self.s2, self.p2, self.training, want_gsum)
+        return ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training, want_gsum)
+
+
+class SelfGating(nn.Module):
+    """Parameter container for ``x * sigmoid(fc(mean_THW(x)))`` (``s3dg.py:47-59``)."""
+
+    def __init__(self, input_dim):
+        super().__init__()
+        self.fc = nn.Linear(input_dim, input_dim)
+
+    def forward(self, x, gsum=None):
+        return ops.gate_concat([x], [self.fc.weight], [self.fc.bias], None if gsum is None else [gsum])
+
+
+class InceptionBlock(nn.Module):
+    """Four-branch gated Inception block (``s3dg.py:11-45``)."""
+
+    def __init__(self, input_dim, num_outputs_0_0a, num_outputs_1_0a, num_outputs_1_0b,
+                 num_outputs_2_0a, num_outputs_2_0b, num_outputs_3_0b, gating=True):
+        super().__init__()
+        self.conv_b0 = STConv3D(input_dim, num_outputs_0_0a, [1, 1, 1])
+        self.conv_b1_a = STConv3D(input_dim, num_outputs_1_0a, [1, 1, 1])
+        self.conv_b1_b = STConv3D(num_outputs_1_0a, num_outputs_1_0b, [3, 3, 3], padding=1, separable=True)
+        self.conv_b2_a = STConv3D(input_dim, num_outputs_2_0a, [1, 1, 1])
+        self.conv_b2_b = STConv3D(num_outputs_2_0a, num_outputs_2_0b, [3, 3, 3], padding=1, separable=True)
+        self.conv_b3_b = STConv3D(input_dim, num_outputs_3_0b, [1, 1, 1])
+        self.gating = gating
+        self.output_dim = num_outputs_0_0a + num_outputs_1_0b + num_outputs_2_0b + num_outputs_3_0b
+        if gating:
+            self.gating_b0 = SelfGating(num_outputs_0_0a)
+            self.gating_b1 = SelfGating(num_outputs_1_0b)
+            self.gating_b2 = SelfGating(num_outputs_2_0b)
+            self.gating_b3 = SelfGating(num_outputs_3_0b)
+
+    def forward(self, x):
+        g = self.gating
+        b0 = self.conv_b0(x, want_gsum=g)
+        b1 = self.conv_b1_b(self.conv_b1_a(x), want_gsum=g)
+        b2 = self.conv_b2_b(self.conv_b2_a(x), want_gsum=g)
+        b3 = self.conv_b3_b(ops.maxpool_s1(x), want_gsum=g)
+        if not g:
+            return torch.cat((b0, b1, b2, b3), dim=-1)
+        gates = (self.gating_b0, self.gating_b1, self.gating_b2, self.gating_b3)
+        zs, sums = zip(b0, b1, b2, b3)
+        return ops.gate_concat(list(zs), [m.fc.weight for m in gates], [m.fc.bias for m in gates], list(sums))
+
+
+# Inception configs (s3dg.py:223-233): (cin-from-previous, 6 widths)
+INCEPTION_CFG = [
+    ("mixed_3b", (64, 96, 128, 16, 32, 32)),
+    ("mixed_3c", (128, 128, 192, 32, 96, 64)),
+    ("maxpool_4a", None),
+    ("mixed_4b", (192, 96, 208, 16, 48, 64)),
+    ("mixed_4c", (160, 112, 224, 24, 64, 64)),
+    ("mixed_4d", (128, 128, 256, 24, 64, 64)),
+    ("mixed_4e", (112, 144, 288, 32, 64, 64)),
+    ("mixed_4f", (256, 160, 320, 32, 128, 128)),
+    ("maxpool_5a", None),
+    ("mixed_5b", (256, 160, 320, 32, 128, 128)),
+    ("mixed_5c", (384, 192, 384, 48, 128, 128)),
+]
+ALL_BLOCKS = [n for n, c in INCEPTION_CFG if c is not None]
+
+
+class S3D(nn.Module):
+    """S3D-G + text module (``s3dg.py:207-328``).
+
+    ``blocks`` keeps a prefix/subset of the Inception blocks (the "2-block S3D" plumbing
+    config of BASELINE.json); the default keeps all nine. Dropped blocks are not created, so a
+    reduced model's state_dict is a strict subset of the full one.
+    """
+
+    def __init__(self, num_classes=512, gating=True, space_to_depth=False, word2vec_path="",
+                 init="uniform", token_to_word_path="", vocab_size=66250,
+                 blocks: Optional[Sequence[str]] = None):
+        super().__init__()
+        self.num_classes = num_classes
+        self.space_to_depth = space_to_depth
+        if space_to_depth:
+            self.conv1 = STConv3D(24, 64, [2, 4, 4], stride=1, padding=(1, 2, 2), separable=False)
+        else:
+            self.conv1 = STConv3D(3, 64, [3, 7, 7], stride=2, padding=(1, 3, 3), separable=False)
+        self.conv_2b = STConv3D(64, 64, [1, 1, 1], separable=False)
+        self.conv_2c = STConv3D(64, 192, [3, 3, 3], padding=1, separable=True)
+        # The top-level ``gating`` flag is overwritten by this module in the reference
+        # (s3dg.py:212 vs :220) so the stem gate is always applied; reproduced.
+        self.gating = SelfGating(192)
+        self.maxpool_2a = ((1, 3, 3), (1, 2, 2))
+        self.maxpool_3a = ((1, 3, 3), (1, 2, 2))
+        self.maxpool_4a = ((3, 3, 3), (2, 2, 2))
+        self.maxpool_5a = ((2, 2, 2), (2, 2, 2))
+        keep = set(ALL_BLOCKS if blocks is None or len(blocks) == 0 else blocks)
+        self._plan: List[str] = []
+        dim = 192
+        for name, cfg in INCEPTION_CFG:
+            if cfg is None:
+                self._plan.append(name)
+                continue
+            if name not in keep:
+                continue
+            blk = InceptionBlock(dim, *cfg)
+            setattr(self, name, blk)
+            self._plan.append(name)
+            dim = blk.output_dim
+        self.feature_dim = dim
+        self.fc = nn.Linear(dim, num_classes)
+        self.text_module = SentenceEmbedding(num_classes, token_to_word_path=token_to_word_path,
+                                             word2vec_path=word2vec_path, num_embeddings=vocab_size)
+        if init == "kaiming_normal":  # s3dg.py:240-246
+            for m in self.modules():
+                if isinstance(m, nn.Conv3d):
+                    nn.init.kaiming_normal_(m.weight, mode="fan_in", nonlinearity="relu")
+                elif isinstance(m, nn.BatchNorm3d):
+                    nn.init.constant_(m.weight, 1)
+                    nn.init.constant_(m.bias, 0)
+
+    # -------------------------------------------------------------------------------------
+    def forward(self, video, text, mode="all", mixed5c=False):
+        if mode == "all":
+            return self.forward_video(video), self.text_module(text)
+        if mode == "video":
+            return self.forward_video(video, mixed5c=mixed5c)
+        if mode == "text":
+            return self.text_module(text)
+        raise NotImplementedError(mode)
+
+    def prepare_video(self, video: torch.Tensor) -> torch.Tensor:
+        """Bring any accepted clip format to the stem's input layout.
+
+        Accepted: reference float ``[B,3,T,H,W]`` in [0,1]; uint8 ``[B,3,T,H,W]`` (raw loader
+        output); native uint8 ``[B,T,H,W,4]`` (RGB + zero pad channel, from the synthetic
+        generator). GPU stem input: uint8/bf16 ``[B,T,H,W,4]``; CPU: float ``[B,T,H,W,3]``.
+        """
+        native = video.dim() == 5 and video.shape[-1] == 4 and video.shape[1] != 3
+        if video.is_cuda and ops.use_hip(video) and not self.space_to_depth:
+            from ..ops import hip_ops
+            return hip_ops.prepare_stem_input(video, native)
+        if native:
+            v = video[..., :3]
+        else:
+            v = video.permute(0, 2, 3, 4, 1)
+        if v.dtype == torch.uint8:
+            v = v.float() / 255.0
+        v = v.contiguous()
+        if video.is_cuda:
+            v = v.to(torch.bfloat16)
+        else:
+            v = v.float()
+        return v
+
+    def forward_video(self, inputs, mixed5c=False):
+        net = self.prepare_video(inputs)
+        if self.space_to_depth:
+            net = ops.space_to_depth(net)
+        net = self.conv1(net)
+        if self.space_to_depth:
+            net = net[:, 1:, 1:, 1:, :].contiguous()
+        net = ops.maxpool_tf_same(net, *self.maxpool_2a)
+        net = self.conv_2b(net)
+        net, gsum = self.conv_2c(net, want_gsum=True)
+        net = self.gating(net, gsum)
+        net = ops.maxpool_tf_same(net, *self.maxpool_3a)
+        for name in self._plan:
+            if name.startswith("maxpool"):
+                net = ops.maxpool_tf_same(net, *getattr(self, name))
+            else:
+                net = getattr(self, name)(net)
+        net = ops.global_avgpool(net)
+        if mixed5c:
+            return net
+        return self.fc(net.to(self.fc.weight.dtype))

@@ -1,0 +1,78 @@
+"""Fused operators of the S3D-G / MIL-NCE hot path.
+
+Dispatch rule (one rule, no per-op fallbacks):
+  * tensors on a GPU  -> hand-written HIP kernels in ``libmilnce_hip.so`` (``ops/hip_ops.py``).
+    If the library is missing on a GPU box this raises: there is no silent fallback.
+  * tensors on CPU    -> the ATen reference implementation (``ops/aten.py``), used for the
+    gloo plumbing configuration and as the numerical oracle in tests.
+
+``MILNCE_OPS=aten`` forces the ATen implementation on GPU too; it exists only to A/B the HIP
+kernels against MIOpen/hipBLASLt in ``tools/ab_bench.py`` and is never used by bench/smoke.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from . import aten
+
+_FORCE_ATEN = os.environ.get("MILNCE_OPS", "") == "aten"
+
+
+def use_hip(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _FORCE_ATEN
+
+
+def _hip():
+    from . import hip_ops  # imported lazily: loads (and checks) the native library
+    return hip_ops
+
+
+def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
+    """conv -> BN -> ReLU. With ``want_gsum`` also returns the per-(clip, channel) sum of the
+    output (fp32 [B, C]) that a following SelfGating needs (None on the ATen path)."""
+    if use_hip(x):
+        return _hip().conv_bn_relu(x, weight, bn, stride, padding, training, want_gsum)
+    z = aten.conv_bn_relu(x, weight, bn, stride, padding, training)
+    return (z, None) if want_gsum else z
+
+
+def gate_concat(branches, fc_weights, fc_biases, gsums=None):
+    if use_hip(branches[0]):
+        return _hip().gate_concat(branches, fc_weights, fc_biases, gsums)
+    return aten.gate_concat(branches, fc_weights, fc_biases)
+
+
+def maxpool_tf_same(x, kernel, stride):
+    if use_hip(x):
+        return _hip().maxpool3d(x, kernel, stride, tf_same=True)
+    return aten.maxpool_tf_same(x, kernel, stride)
+
+
+def maxpool_s1(x):
+    if use_hip(x):
+        return _hip().maxpool3d(x, (3, 3, 3), (1, 1, 1), tf_same=False)
+    return aten.maxpool_s1(x)
+
+
+def global_avgpool(x):
+    if use_hip(x):
+        return _hip().global_avgpool(x)
+    return aten.global_avgpool(x)
+
+
+def text_relu_max(h):
+    if use_hip(h):
+        return _hip().text_relu_max(h)
+    return aten.text_relu_max(h)
+
+
+def milnce_loss(video_embd, text_embd):
+    if use_hip(video_embd):
+        return _hip().milnce_loss(video_embd, text_embd)
+    return aten.milnce_loss(video_embd, text_embd)
+
+
+def space_to_depth(x):
+    return aten.space_to_depth(x)

@@ -1,0 +1,85 @@
+"""ctypes binding of ``libmilnce_hip.so`` (built from ``csrc/*.hip`` by ``csrc/build.py``).
+
+The library exposes a plain C ABI (raw device pointers + ``hipStream_t``), so it needs no torch
+headers and builds in seconds. ``torch`` must be imported first so the already-loaded HIP
+runtime (soname ``libamdhip64.so.7``) is shared with PyTorch's allocator and streams.
+Every call checks the returned ``hipError_t`` and raises on failure — there is no fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_double, c_float, c_int, c_longlong, c_void_p
+from typing import Dict
+
+import torch  # noqa: F401  (must precede the library load)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libmilnce_hip.so")
+
+P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
+
+SIGNATURES: Dict[str, list] = {
+    "milnce_conv_fwd": [P, I, P, P, P] + [I] * 6 + [I] * 9 + [I] * 6 + [P],
+    "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 6 + [P],
+    "milnce_pack_weight": [P, P] + [I] * 9 + [P],
+    "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
+    "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
+    "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, P, P, P, P, P],
+    "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P],
+    "milnce_gate_bwd": [I, P, P, P, P, P, P, P, P, P, I, I, P, P, P],
+    "milnce_avgpool": [P, I, I, I, P, P],
+    "milnce_avgpool_bwd": [P, I, I, I, P, P],
+    "milnce_maxpool_fwd": [P, P, P] + [I] * 21 + [P],
+    "milnce_maxpool_bwd": [P, P, P] + [I] * 21 + [P],
+    "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
+    "milnce_synth_video": [P, P, I, I, I, P, P],
+    "milnce_stem_prep": [P, I, I, I, I, I, P, P],
+    "milnce_text_relu_max": [P, I, I, I, P, P, P],
+    "milnce_text_relu_max_bwd": [P, P, P, I, I, I, P, P],
+    "milnce_loss_fwd": [P, I, I, P, P, P, P],
+    "milnce_loss_bwd": [P, P, P, P, I, I, P, P],
+    "milnce_softdtw_fwd": [P, I, I, I, I, I, I, F, F, P, P],
+    "milnce_softdtw_bwd": [P, P, I, I, I, I, I, I, F, F, P, P, P],
+    "milnce_dtw_path": [P, I, I, I, P, P, P],
+}
+
+_lib = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.isfile(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python csrc/build.py` (or __graft_entry__.build()). "
+            "GPU tensors require the HIP kernels; there is no ATen fallback.")
+    l = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(l, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    _lib = l
+    return l
+
+
+def call(name: str, *args) -> None:
+    fn = getattr(lib(), name)
+    rc = fn(*args)
+    if rc != 0:
+        raise NativeLibraryError(f"{name} failed with hipError {rc}")
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream

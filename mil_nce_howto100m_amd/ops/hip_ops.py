@@ -1,0 +1,463 @@
+"""Autograd Functions over the HIP kernels (GPU path). Activations are bf16 NDHWC.
+
+Every forward and backward here is a call into ``libmilnce_hip.so``; the only library GEMMs
+are the tiny, plain ones (text tower fc1/fc2, video fc, the MIL-NCE logits, the gating fc of
+the stem) which go to hipBLASLt through ``torch.mm``. Shapes are planned once per
+(layer geometry, input shape) and cached.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import aten
+from ._lib import call, lib, ptr, stream
+
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _ceil(a: int, b: int) -> int:
+    return (a + b - 1) // b
+
+
+# =========================================================================================
+# Conv + BN + ReLU
+# =========================================================================================
+@dataclass(frozen=True)
+class ConvPlan:
+    B: int
+    T: int
+    H: int
+    W: int
+    Cin: int       # channels as stored in x (4 for the stem)
+    Cin_p: int     # channels of the weight parameter (3 for the stem)
+    Cout: int
+    k: Tuple[int, int, int]
+    s: Tuple[int, int, int]
+    p: Tuple[int, int, int]
+    To: int
+    Ho: int
+    Wo: int
+    M: int
+    Ktot: int
+    bn: int
+    bk: int
+    Npad: int
+    Kpad: int
+    grid_m: int
+    # dgrad (stride 1 only)
+    d_bn: int
+    d_bk: int
+    d_Npad: int
+    d_Kpad: int
+    d_grid_m: int
+    # wgrad
+    w_tn: int
+    w_tk: int
+    w_Npad: int
+    w_Kpad: int
+    w_splits: int
+
+
+_PLANS: Dict[tuple, ConvPlan] = {}
+_NUM_CU = 256
+
+
+def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
+    bn = 128 if N > 64 else 64
+    bk = 64 if K >= 128 else 32
+    npad = _ceil(N, bn) * bn
+    kpad = _ceil(K, bk) * bk
+    m_tiles = _ceil(M, 128)
+    n_tiles = npad // bn
+    grid_m = max(1, min(m_tiles, _ceil(4 * _NUM_CU, n_tiles)))
+    return bn, bk, npad, kpad, grid_m
+
+
+def conv_plan(x_shape, w_shape, stride, padding) -> ConvPlan:
+    key = (tuple(x_shape), tuple(w_shape), tuple(stride), tuple(padding))
+    plan = _PLANS.get(key)
+    if plan is not None:
+        return plan
+    B, T, H, W, Cin = x_shape
+    Cout, Cin_p, kt, kh, kw = w_shape
+    st, sh, sw = stride
+    pt, ph, pw = padding
+    To = (T + 2 * pt - kt) // st + 1
+    Ho = (H + 2 * ph - kh) // sh + 1
+    Wo = (W + 2 * pw - kw) // sw + 1
+    M = B * To * Ho * Wo
+    taps = kt * kh * kw
+    Ktot = taps * Cin
+    bn, bk, npad, kpad, grid_m = _fwd_tiles(M, Cout, Ktot)
+    # dgrad: a stride-1 conv over dY (channels Cout) producing Cin_p channels
+    d_bn, d_bk, d_npad, d_kpad, d_grid_m = _fwd_tiles(B * T * H * W, Cin_p, taps * Cout)
+    # wgrad: output [Cout, Ktot], reduction over M
+    w_tn = 128 if Cout > 64 else 64
+    w_tk = 128 if Ktot > 64 else 64
+    if Cin % 8 != 0:  # uint8 stem
+        w_tn = 64
+    w_npad = _ceil(Cout, w_tn) * w_tn
+    w_kpad = _ceil(Ktot, w_tk) * w_tk
+    tiles = (w_npad // w_tn) * (w_kpad // w_tk)
+    splits = max(1, min(_ceil(4 * _NUM_CU, tiles), _ceil(M, 32 * 8)))
+    plan = ConvPlan(B, T, H, W, Cin, Cin_p, Cout, (kt, kh, kw), (st, sh, sw), (pt, ph, pw), To, Ho, Wo, M, Ktot,
+                    bn, bk, npad, kpad, grid_m, d_bn, d_bk, d_npad, d_kpad, d_grid_m, w_tn, w_tk, w_npad, w_kpad,
+                    splits)
+    _PLANS[key] = plan
+    return plan
+
+
+def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
+    kt, kh, kw = plan.k
+    if mode == 0:
+        out = torch.empty((plan.Npad, plan.Kpad), dtype=BF16, device=weight.device)
+        call("milnce_pack_weight", ptr(weight), ptr(out), plan.Cout, plan.Cin, plan.Cin_p, kt, kh, kw,
+             plan.Npad, plan.Kpad, 0, stream())
+    else:
+        out = torch.empty((plan.d_Npad, plan.d_Kpad), dtype=BF16, device=weight.device)
+        call("milnce_pack_weight", ptr(weight), ptr(out), plan.Cout, plan.Cin, plan.Cin_p, kt, kh, kw,
+             plan.d_Npad, plan.d_Kpad, 1, stream())
+    return out
+
+
+def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: Optional[torch.Tensor]):
+    y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=x.device)
+    kt, kh, kw = plan.k
+    st, sh, sw = plan.s
+    pt, ph, pw = plan.p
+    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats),
+         plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
+         plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, stream())
+    return y
+
+
+def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan) -> torch.Tensor:
+    kt, kh, kw = plan.k
+    assert plan.s == (1, 1, 1), "dgrad is only needed for stride-1 convs"
+    dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dy.device)
+    pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
+    call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), None,
+         plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
+         plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, stream())
+    return dx
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tensor:
+    kt, kh, kw = plan.k
+    st, sh, sw = plan.s
+    pt, ph, pw = plan.p
+    slab = torch.empty((plan.w_splits, plan.w_Npad, plan.w_Kpad), dtype=F32, device=dy.device)
+    dw = torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
+    call("milnce_conv_wgrad", ptr(dy), plan.Cout, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
+         plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
+         plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, stream())
+    return dw
+
+
+def _bn_nparts(M: int) -> int:
+    return int(max(1, min(2048, _ceil(M, 2048))))
+
+
+class _ConvBNReLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
+                want_gsum):
+        plan = conv_plan(x.shape, weight.shape, stride, padding)
+        dev = x.device
+        wp = _pack(weight, plan, 0)
+        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+        y = conv_forward_raw(x, wp, plan, stats)
+        C = plan.Cout
+        ss = torch.empty((4 * C,), dtype=F32, device=dev)
+        call("milnce_bn_finalize", ptr(stats), plan.grid_m, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
+             ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(momentum), float(eps), int(training),
+             ptr(ss), stream())
+        z = torch.empty_like(y)
+        gsum = torch.zeros((plan.B, C), dtype=F32, device=dev) if want_gsum else None
+        call("milnce_bn_relu_apply", ptr(y), C, ptr(z), C, ptr(ss), C, plan.B, plan.To * plan.Ho * plan.Wo,
+             ptr(gsum), stream())
+        ctx.save_for_backward(x, weight, y, ss, gamma)
+        ctx.plan = plan
+        if gsum is None:
+            return z
+        ctx.mark_non_differentiable(gsum)
+        return z, gsum
+
+    @staticmethod
+    def backward(ctx, dz, *unused):
+        x, weight, y, ss, gamma = ctx.saved_tensors
+        plan: ConvPlan = ctx.plan
+        dz = dz.contiguous()
+        C = plan.Cout
+        dev = dz.device
+        nparts = _bn_nparts(plan.M)
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
+        coef = torch.empty((3 * C,), dtype=F32, device=dev)
+        dgamma = torch.empty((C,), dtype=F32, device=dev)
+        dbeta = torch.empty((C,), dtype=F32, device=dev)
+        dy = torch.empty_like(y)
+        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts,
+             ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), stream())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wd = _pack(weight, plan, 1)
+            dx = conv_dgrad(dy, wd, plan)
+        dw = conv_wgrad(dy, x, plan) if ctx.needs_input_grad[1] else None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+
+
+def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
+    if x.dtype not in (torch.uint8, BF16):
+        x = x.to(BF16)
+    x = x.contiguous()
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    out = _ConvBNReLU.apply(x, weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                            tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum))
+    return out
+
+
+# =========================================================================================
+# SelfGating + concat
+# =========================================================================================
+def _arr(ctype, vals):
+    return (ctype * len(vals))(*vals)
+
+
+class _GateConcat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, nseg, gsum, *args):
+        zs = args[:nseg]
+        ws = args[nseg:2 * nseg]
+        bs = args[2 * nseg:3 * nseg]
+        B, T, H, W = zs[0].shape[:4]
+        thw = T * H * W
+        widths = [int(z.shape[-1]) for z in zs]
+        ctot = sum(widths)
+        dev = zs[0].device
+        mean = torch.empty((B, ctot), dtype=F32, device=dev)
+        g = torch.empty((B, ctot), dtype=F32, device=dev)
+        out = torch.empty((B, T, H, W, ctot), dtype=BF16, device=dev)
+        call("milnce_gate_fwd", nseg, _arr(ctypes.c_int, widths), _arr(ctypes.c_void_p, [ptr(z) for z in zs]),
+             _arr(ctypes.c_void_p, [ptr(w) for w in ws]), _arr(ctypes.c_void_p, [ptr(b) for b in bs]),
+             ptr(gsum), B, thw, ptr(mean), ptr(g), ptr(out), stream())
+        ctx.save_for_backward(*zs, *ws, g, mean)
+        ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        nseg = ctx.nseg
+        saved = ctx.saved_tensors
+        zs = saved[:nseg]
+        ws = saved[nseg:2 * nseg]
+        g, mean = saved[2 * nseg], saved[2 * nseg + 1]
+        dout = dout.contiguous()
+        B = g.shape[0]
+        ctot = g.shape[1]
+        dev = dout.device
+        dzs = [torch.empty_like(z) for z in zs]
+        dws = [torch.zeros_like(w) for w in ws]
+        dbs = [torch.zeros((w.shape[0],), dtype=F32, device=dev) for w in ws]
+        dg = torch.zeros((B, ctot), dtype=F32, device=dev)
+        dmean = torch.empty((B, ctot), dtype=F32, device=dev)
+        call("milnce_gate_bwd", nseg, _arr(ctypes.c_int, ctx.widths), _arr(ctypes.c_void_p, [ptr(z) for z in zs]),
+             _arr(ctypes.c_void_p, [ptr(d) for d in dzs]), _arr(ctypes.c_void_p, [ptr(w) for w in ws]),
+             _arr(ctypes.c_void_p, [ptr(d) for d in dws]), _arr(ctypes.c_void_p, [ptr(d) for d in dbs]),
+             ptr(dout), ptr(g), ptr(mean), B, ctx.thw, ptr(dg), ptr(dmean), stream())
+        return (None, None, *dzs, *dws, *dbs)
+
+
+def gate_concat(branches, fc_weights, fc_biases, gsums=None):
+    branches = [b.contiguous() if b.dtype == BF16 else b.to(BF16).contiguous() for b in branches]
+    if gsums is None or any(s is None for s in gsums):
+        gsums = [b.float().sum(dim=(1, 2, 3)) for b in branches]
+    gsum = gsums[0] if len(gsums) == 1 else torch.cat(gsums, dim=1)
+    return _GateConcat.apply(len(branches), gsum.contiguous(), *branches, *fc_weights, *fc_biases)
+
+
+# =========================================================================================
+# Pools
+# =========================================================================================
+def _pool_out(n: int, k: int, s: int, p0: int, p1: int) -> int:
+    np_ = n + p0 + p1
+    o = -(-(np_ - k) // s) + 1
+    if (o - 1) * s >= np_:
+        o -= 1
+    return o
+
+
+class _MaxPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, kernel, stride, tf_same):
+        B, T, H, W, C = x.shape
+        if tf_same:
+            pads = aten.tf_same_pad(kernel, stride)
+            zero_pad = 1
+        else:
+            pads = [(1, 1)] * 3
+            zero_pad = 0
+        To = _pool_out(T, kernel[0], stride[0], *pads[0])
+        Ho = _pool_out(H, kernel[1], stride[1], *pads[1])
+        Wo = _pool_out(W, kernel[2], stride[2], *pads[2])
+        y = torch.empty((B, To, Ho, Wo, C), dtype=BF16, device=x.device)
+        arg = torch.empty((B, To, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        geo = [B, T, H, W, C, To, Ho, Wo, *kernel, *stride, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
+               pads[2][0], pads[2][1], zero_pad]
+        call("milnce_maxpool_fwd", ptr(x), ptr(y), ptr(arg), *geo, stream())
+        ctx.save_for_backward(arg)
+        ctx.geo = geo
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        geo = ctx.geo
+        B, T, H, W, C = geo[:5]
+        dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dy.device)
+        call("milnce_maxpool_bwd", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo, stream())
+        return dx, None, None, None
+
+
+def maxpool3d(x, kernel, stride, tf_same: bool):
+    return _MaxPool.apply(x.contiguous(), tuple(kernel), tuple(stride), bool(tf_same))
+
+
+class _AvgPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        B, T, H, W, C = x.shape
+        out = torch.zeros((B, C), dtype=F32, device=x.device)
+        call("milnce_avgpool", ptr(x), B, T * H * W, C, ptr(out), stream())
+        ctx.shape = (B, T, H, W, C)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, T, H, W, C = ctx.shape
+        dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
+        call("milnce_avgpool_bwd", ptr(dout.contiguous().float()), B, T * H * W, C, ptr(dx), stream())
+        return dx
+
+
+def global_avgpool(x):
+    return _AvgPool.apply(x.contiguous())
+
+
+# =========================================================================================
+# Text tower
+# =========================================================================================
+class _TextTower(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tokens, table, w1, b1, w2, b2):
+        N, Wd = tokens.shape
+        e = table.index_select(0, tokens.reshape(-1))                     # [N*Wd, 300] bf16
+        h = torch.addmm(b1.to(BF16), e, w1.to(BF16).t())                   # [N*Wd, 2048] bf16 (hipBLASLt)
+        F_ = h.shape[1]
+        hm = torch.empty((N, F_), dtype=F32, device=h.device)
+        arg = torch.empty((N, F_), dtype=torch.uint8, device=h.device)
+        call("milnce_text_relu_max", ptr(h), N, Wd, F_, ptr(hm), ptr(arg), stream())
+        out = torch.addmm(b2, hm, w2.t())
+        ctx.save_for_backward(e, hm, arg, w2)
+        ctx.dims = (N, Wd, F_)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        e, hm, arg, w2 = ctx.saved_tensors
+        N, Wd, F_ = ctx.dims
+        dout = dout.contiguous().float()
+        dw2 = dout.t().mm(hm)
+        db2 = dout.sum(0)
+        dhm = dout.mm(w2).contiguous()
+        dh = torch.empty((N * Wd, F_), dtype=BF16, device=dout.device)
+        call("milnce_text_relu_max_bwd", ptr(dhm), ptr(hm), ptr(arg), N, Wd, F_, ptr(dh), stream())
+        dhf = dh.float()
+        dw1 = dhf.t().mm(e.float())
+        db1 = dhf.sum(0)
+        return None, None, dw1, db1, dw2, db2
+
+
+def text_tower(tokens, table_bf16, w1, b1, w2, b2):
+    return _TextTower.apply(tokens.contiguous(), table_bf16, w1, b1, w2, b2)
+
+
+def text_relu_max(h):
+    N, Wd, F_ = h.shape
+    hb = h.to(BF16).contiguous()
+    hm = torch.empty((N, F_), dtype=F32, device=h.device)
+    arg = torch.empty((N, F_), dtype=torch.uint8, device=h.device)
+    call("milnce_text_relu_max", ptr(hb), N, Wd, F_, ptr(hm), ptr(arg), stream())
+    return hm
+
+
+# =========================================================================================
+# MIL-NCE
+# =========================================================================================
+class _MILNCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, v, t):
+        B = v.shape[0]
+        K = t.shape[0] // B
+        x = v.mm(t.t()).contiguous()
+        den = torch.empty((B,), dtype=F32, device=v.device)
+        nom = torch.empty((B,), dtype=F32, device=v.device)
+        loss = torch.empty((1,), dtype=F32, device=v.device)
+        call("milnce_loss_fwd", ptr(x), B, K, ptr(den), ptr(nom), ptr(loss), stream())
+        ctx.save_for_backward(v, t, x, den, nom)
+        ctx.K = K
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        v, t, x, den, nom = ctx.saved_tensors
+        B, K = v.shape[0], ctx.K
+        dx = torch.empty_like(x)
+        gg = g.reshape(1).float().contiguous()
+        call("milnce_loss_bwd", ptr(x), ptr(den), ptr(nom), ptr(gg), B, K, ptr(dx), stream())
+        return dx.mm(t), dx.t().mm(v)
+
+
+def milnce_loss(video_embd, text_embd):
+    return _MILNCE.apply(video_embd.float().contiguous(), text_embd.float().contiguous())
+
+
+# =========================================================================================
+# Optimizer, data, stem input
+# =========================================================================================
+def adam_step(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, grad_scale):
+    call("milnce_adam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(b1), float(b2), float(eps),
+         float(wd), float(bc1), float(bc2), float(grad_scale), stream())
+
+
+def synth_video(labels_i32, ids_i32, T, S, seed):
+    B = labels_i32.shape[0]
+    out = torch.empty((B, T, S, S, 4), dtype=torch.uint8, device=labels_i32.device)
+    call("milnce_synth_video", ptr(labels_i32.contiguous()), ptr(ids_i32.contiguous()), B, T, S, ptr(out), stream())
+    return out
+
+
+def prepare_stem_input(video, native: bool):
+    if native:
+        v = video.contiguous()
+        if v.dtype not in (torch.uint8, BF16):
+            v = v.to(BF16)
+        return v
+    B, C, T, H, W = video.shape
+    assert C == 3
+    video = video.contiguous()
+    if video.dtype == torch.uint8:
+        out = torch.empty((B, T, H, W, 4), dtype=torch.uint8, device=video.device)
+        kind = 0
+    else:
+        if video.dtype not in (F32, BF16):
+            video = video.float()
+        kind = 1 if video.dtype == F32 else 2
+        out = torch.empty((B, T, H, W, 8), dtype=BF16, device=video.device)
+    call("milnce_stem_prep", ptr(video), kind, B, T, H, W, ptr(out), stream())
+    return out

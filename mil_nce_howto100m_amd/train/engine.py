@@ -1,0 +1,169 @@
+"""Training engine: one process per GPU, the MIL-NCE step, epochs, checkpoint/resume.
+
+The step (``main_distributed.py:226-241`` ``TrainOneBatch``) is:
+
+    zero flat grads -> [broadcast BN buffers from rank 0] -> forward (S3D-G + text tower)
+    -> all-gather video+text embeddings (one collective, local-slice backward)
+    -> MIL-NCE over the global batch (computed redundantly on every rank, like the reference)
+    -> backward (bucketed RCCL all-reduce issued as buckets fill) -> wait buckets
+    -> fused Adam (HIP, grad scale folded in) -> cosine LR step
+
+Differences from the reference, all deliberate: the loss is returned as a device tensor and
+only synchronised every ``n_display`` steps (the reference's per-step ``loss.item()``,
+``main_distributed.py:241``, is a host sync); the seed reaches every rank.
+"""
+from __future__ import annotations
+
+import os
+import random
+import time
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..losses import build_loss
+from ..models import S3D
+from ..parallel import dist as pdist
+from ..parallel.ddp import BufferBroadcaster, GradBucketer, broadcast_parameters
+from . import checkpoint as ckpt
+from .logging import MetricsLogger, log, train_line
+from .optim import FlatAdam, FlatSGD, cosine_schedule_with_warmup
+
+
+def seed_everything(seed: int, rank: int = 0) -> None:
+    random.seed(seed + rank)
+    np.random.seed((seed + rank) % (2 ** 32))
+    torch.manual_seed(seed)  # same weights on every rank before the rank-0 broadcast
+
+
+def build_model(args, device: torch.device) -> S3D:
+    blocks = [b for b in (getattr(args, "blocks", "") or "").split(",") if b]
+    model = S3D(args.num_class, space_to_depth=False,
+                word2vec_path=args.word2vec_path if os.path.isfile(args.word2vec_path or "") else "",
+                init=args.weight_init, token_to_word_path=getattr(args, "token_to_word_path", ""),
+                vocab_size=getattr(args, "vocab_size", 66250), blocks=blocks)
+    if args.pretrain_cnn_path:
+        sd = ckpt.load_checkpoint(args.pretrain_cnn_path)
+        if "state_dict" in sd:
+            sd = sd["state_dict"]
+        ckpt.load_model_weights(model, sd, strict=True)
+    return model.to(device)
+
+
+class Trainer:
+    def __init__(self, args, model: S3D, ctx: pdist.DistContext, steps_per_epoch: int):
+        self.args, self.model, self.ctx = args, model, ctx
+        self.device = ctx.device
+        broadcast_parameters(model, ctx.world_size)
+        params = list(model.parameters())
+        scale = 1.0 / ctx.world_size if getattr(args, "grad_scale", "reference") == "reference" else 1.0
+        if args.optimizer == "adam":
+            self.optimizer = FlatAdam(params, lr=args.lr, grad_scale=scale)
+        elif args.optimizer == "sgd":
+            self.optimizer = FlatSGD(params, lr=args.lr, momentum=args.momemtum, grad_scale=scale)
+        else:
+            raise ValueError(args.optimizer)
+        self.bucketer = GradBucketer(params, ctx.world_size, int(getattr(args, "bucket_mb", 8.0) * (1 << 20)))
+        self.optimizer.bind_flat_grad(self.bucketer.flat, self.bucketer.offsets)
+        self.buffers = BufferBroadcaster(model, ctx.world_size) if getattr(args, "broadcast_buffers", 1) else None
+        self.scheduler = cosine_schedule_with_warmup(self.optimizer, args.warmup_steps,
+                                                     steps_per_epoch * args.epochs)
+        self.criterion = build_loss(args)
+        self.global_step = 0
+
+    # ---------------------------------------------------------------------------------
+    def forward_loss(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        video = batch["video"]
+        text = batch["text"]
+        text = text.reshape(-1, text.shape[-1])
+        video_embd, text_embd = self.model(video, text)
+        video_embd, text_embd = pdist.all_gather_embeddings(video_embd, text_embd, self.ctx)
+        return self.criterion(video_embd, text_embd)
+
+    def train_step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        self.model.train()
+        self.bucketer.zero()
+        if self.buffers is not None:
+            self.buffers()
+        loss = self.forward_loss(batch)
+        loss.backward()
+        self.bucketer.finish()
+        self.optimizer.step()
+        self.scheduler.step()
+        self.global_step += 1
+        return loss.detach()
+
+    # ---------------------------------------------------------------------------------
+    def state(self, epoch: int) -> dict:
+        return {"epoch": epoch, "state_dict": ckpt.model_state_dict(self.model),
+                "optimizer": self.optimizer.state_dict(), "scheduler": self.scheduler.state_dict()}
+
+    def load_state(self, state: dict) -> int:
+        ckpt.load_model_weights(self.model, state["state_dict"], strict=True)
+        self.optimizer.load_state_dict(state["optimizer"])
+        self.scheduler.load_state_dict(state["scheduler"])
+        self.global_step = int(self.scheduler.last_epoch)
+        return int(state["epoch"])
+
+
+def checkpoint_dir_of(args) -> str:
+    return os.path.join(getattr(args, "checkpoint_root", "checkpoint") or "checkpoint", args.checkpoint_dir)
+
+
+def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, float]:
+    """Epoch loop of main_distributed.py:185-200 on synthetic on-device data."""
+    from ..data.synthetic import SyntheticClips
+
+    ctx = ctx or pdist.context()
+    seed_everything(args.seed, ctx.rank)
+    # batch_size is global per node; divided across the ranks like main_distributed.py:88.
+    local_bs = max(1, args.batch_size // max(1, ctx.world_size))
+    data = SyntheticClips(local_bs, args.num_frames, args.video_size, args.num_candidates,
+                          args.max_words, args.vocab_size, seed=args.seed, device=ctx.device,
+                          rank=ctx.rank, world_size=ctx.world_size, epoch_len=args.synthetic_len)
+    steps_per_epoch = len(data) if not args.steps_per_epoch else min(len(data), args.steps_per_epoch)
+    model = build_model(args, ctx.device)
+    trainer = Trainer(args, model, ctx, steps_per_epoch)
+    metrics = MetricsLogger(getattr(args, "log_jsonl", ""), ctx.rank)
+    cdir = checkpoint_dir_of(args)
+    if ctx.is_main and args.checkpoint_dir:
+        os.makedirs(cdir, exist_ok=True)
+    pdist.barrier()
+    start_epoch = args.start_epoch
+    if args.resume:
+        path = ckpt.get_last_checkpoint(cdir)
+        if path:
+            log("=> loading checkpoint '{}'".format(path), args, ctx.rank)
+            start_epoch = trainer.load_state(ckpt.load_checkpoint(path, map_location=ctx.device))
+            log("=> loaded checkpoint '{}' (epoch {})".format(path, start_epoch), args, ctx.rank)
+        else:
+            log("=> no checkpoint found at '{}'".format(cdir), args, ctx.rank)
+    total_bs = local_bs * ctx.world_size
+    log("Starting training loop for rank: {}, total batch size: {}".format(ctx.rank, total_bs), args, ctx.rank)
+    last = {}
+    for epoch in range(start_epoch, args.epochs):
+        running = torch.zeros((), device=ctx.device)
+        t0 = time.time()
+        for i in range(steps_per_epoch):
+            batch = data.batch(epoch * steps_per_epoch + i)
+            running += trainer.train_step(batch)
+            if (i + 1) % args.n_display == 0:
+                avg = float(running.item()) / args.n_display  # the only host sync
+                d = time.time() - t0
+                lr = trainer.optimizer.param_groups[0]["lr"]
+                if args.verbose:
+                    log(train_line(epoch + 1, d, total_bs * float(i) / max(1, data.epoch_len), avg, lr), args, ctx.rank)
+                metrics.write(epoch=epoch + 1, step=trainer.global_step, loss=avg, lr=lr,
+                              pairs_per_s=total_bs * args.n_display / max(d, 1e-9))
+                last = {"loss": avg, "lr": lr}
+                running.zero_()
+                t0 = time.time()
+            if args.ckpt_every_steps and trainer.global_step % args.ckpt_every_steps == 0 and ctx.is_main:
+                ckpt.save_checkpoint(trainer.state(epoch), cdir, epoch)
+        if ctx.is_main:
+            ckpt.save_checkpoint(trainer.state(epoch + 1), cdir, epoch + 1)
+        pdist.barrier()
+    return last

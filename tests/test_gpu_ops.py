@@ -1,0 +1,263 @@
+"""Numerics of every HIP kernel against a plain-PyTorch fp32 reference of the same op.
+
+Inputs are generated in bf16 (the kernels' storage type) and the reference runs in fp32 on the
+same (upcast) values, so the tolerance covers accumulation order and the bf16 rounding of the
+outputs only. Run on an MI355X: ``pytest -m gpu``.
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from mil_nce_howto100m_amd.ops import aten
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def hip():
+    from mil_nce_howto100m_amd.ops import hip_ops
+    return hip_ops
+
+
+def rel_err(a, b):
+    a = a.float()
+    b = b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def ref_conv(x_bf, w, stride, padding):
+    """fp32 conv on the bf16-rounded operands; x is NDHWC."""
+    xr = x_bf.float().permute(0, 4, 1, 2, 3)
+    y = F.conv3d(xr, w.to(torch.bfloat16).float(), None, stride, padding)
+    return y.permute(0, 2, 3, 4, 1)
+
+
+CONV_CASES = [
+    # B, T, H, W, Cin, Cout, k, s, p
+    (2, 4, 9, 9, 64, 192, (1, 3, 3), (1, 1, 1), (0, 1, 1)),
+    (2, 4, 9, 9, 192, 192, (3, 1, 1), (1, 1, 1), (1, 0, 0)),
+    (2, 4, 7, 7, 16, 32, (1, 3, 3), (1, 1, 1), (0, 1, 1)),
+    (2, 4, 7, 7, 24, 64, (3, 1, 1), (1, 1, 1), (1, 0, 0)),
+    (2, 3, 5, 5, 832, 48, (1, 1, 1), (1, 1, 1), (0, 0, 0)),
+    (3, 2, 7, 7, 112, 144, (1, 3, 3), (1, 1, 1), (0, 1, 1)),
+    (2, 2, 5, 6, 528, 256, (1, 1, 1), (1, 1, 1), (0, 0, 0)),
+]
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(case):
+    torch.manual_seed(0)
+    B, T, H, W, Cin, Cout, k, s, p = case
+    h = hip()
+    x = torch.randn(B, T, H, W, Cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(Cout, Cin, *k, device=DEV) * (2.0 / (Cin * k[0] * k[1] * k[2])) ** 0.5
+    plan = h.conv_plan(x.shape, w.shape, s, p)
+    wp = h._pack(w, plan, 0)
+    stats = torch.empty(plan.grid_m * 2 * plan.Npad, device=DEV)
+    y = h.conv_forward_raw(x, wp, plan, stats)
+    yr = ref_conv(x, w, s, p)
+    assert rel_err(y, yr) < 1e-2
+    st = stats.view(plan.grid_m, 2, plan.Npad).sum(0)[:, :Cout]
+    yf = yr.reshape(-1, Cout)
+    assert rel_err(st[0], yf.sum(0)) < 2e-2
+    assert rel_err(st[1], (yf * yf).sum(0)) < 2e-2
+    # dgrad / wgrad against autograd of the fp32 reference
+    dy = torch.randn_like(y)
+    xr = x.float().requires_grad_(True)
+    wr = w.to(torch.bfloat16).float().requires_grad_(True)
+    out = F.conv3d(xr.permute(0, 4, 1, 2, 3), wr, None, s, p).permute(0, 2, 3, 4, 1)
+    out.backward(dy.float())
+    dx = h.conv_dgrad(dy, h._pack(w, plan, 1), plan)
+    assert rel_err(dx, xr.grad) < 1e-2
+    dw = h.conv_wgrad(dy, x, plan)
+    assert rel_err(dw, wr.grad) < 1e-2
+
+
+def test_stem_uint8():
+    torch.manual_seed(0)
+    h = hip()
+    B, T, S = 2, 6, 20
+    x = torch.randint(0, 256, (B, T, S, S, 4), dtype=torch.uint8, device=DEV)
+    x[..., 3] = 0
+    w = torch.randn(64, 3, 3, 7, 7, device=DEV) * 0.05
+    plan = h.conv_plan(x.shape, w.shape, (2, 2, 2), (1, 3, 3))
+    y = h.conv_forward_raw(x, h._pack(w, plan, 0), plan, None)
+    xf = (x[..., :3].float() / 255.0).to(torch.bfloat16)
+    yr = ref_conv(xf, w, (2, 2, 2), (1, 3, 3))
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) < 1e-2
+    dy = torch.randn_like(y)
+    wr = w.to(torch.bfloat16).float().requires_grad_(True)
+    out = F.conv3d(xf.float().permute(0, 4, 1, 2, 3), wr, None, (2, 2, 2), (1, 3, 3)).permute(0, 2, 3, 4, 1)
+    out.backward(dy.float())
+    assert rel_err(h.conv_wgrad(dy, x, plan), wr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("cin,cout,k,p", [(64, 96, (1, 1, 1), (0, 0, 0)), (96, 128, (1, 3, 3), (0, 1, 1)),
+                                          (48, 64, (3, 1, 1), (1, 0, 0))])
+@pytest.mark.parametrize("gsum", [False, True])
+def test_conv_bn_relu_train(cin, cout, k, p, gsum):
+    torch.manual_seed(1)
+    h = hip()
+    B, T, H, W = 3, 4, 8, 8
+    x = torch.randn(B, T, H, W, cin, device=DEV).to(torch.bfloat16)
+    conv = nn.Conv3d(cin, cout, k, 1, p, bias=False).to(DEV)
+    bn = nn.BatchNorm3d(cout).to(DEV)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    bn_ref = nn.BatchNorm3d(cout).to(DEV)
+    bn_ref.load_state_dict(bn.state_dict())
+    xh = x.clone().requires_grad_(True)
+    out = h.conv_bn_relu(xh, conv.weight, bn, (1, 1, 1), p, True, gsum)
+    z = out[0] if gsum else out
+    # reference: same bf16-rounded weights, fp32 math
+    wref = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    zr = aten.conv_bn_relu(xr, wref, bn_ref, (1, 1, 1), p, True)
+    assert rel_err(z, zr) < 2e-2
+    if gsum:
+        assert rel_err(out[1], zr.sum(dim=(1, 2, 3))) < 2e-2
+    dz = torch.randn_like(zr)
+    z.backward(dz.to(torch.bfloat16))
+    zr.backward(dz)
+    assert rel_err(xh.grad, xr.grad) < 3e-2
+    assert rel_err(conv.weight.grad, wref.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_ref.weight.grad) < 3e-2
+    assert rel_err(bn.bias.grad, bn_ref.bias.grad) < 3e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, rtol=2e-2, atol=2e-3)
+    assert torch.allclose(bn.running_var, bn_ref.running_var, rtol=2e-2, atol=2e-3)
+    assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
+
+
+@pytest.mark.parametrize("kernel,stride,tf", [((1, 3, 3), (1, 2, 2), True), ((3, 3, 3), (2, 2, 2), True),
+                                              ((2, 2, 2), (2, 2, 2), True), ((3, 3, 3), (1, 1, 1), False)])
+def test_maxpool(kernel, stride, tf):
+    torch.manual_seed(2)
+    h = hip()
+    x = torch.randn(2, 5, 11, 12, 24, device=DEV).relu().to(torch.bfloat16)
+    xh = x.clone().requires_grad_(True)
+    y = h.maxpool3d(xh, kernel, stride, tf)
+    xr = x.float().requires_grad_(True)
+    yr = aten.maxpool_tf_same(xr, kernel, stride) if tf else aten.maxpool_s1(xr)
+    assert y.shape == yr.shape
+    assert torch.equal(y.float(), yr)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(torch.bfloat16))
+    yr.backward(dy.to(torch.bfloat16).float())
+    assert rel_err(xh.grad, xr.grad) < 1e-2
+
+
+def test_gate_concat():
+    torch.manual_seed(3)
+    h = hip()
+    widths = [64, 128, 32, 48]
+    B, T, H, W = 3, 2, 5, 5
+    zs = [torch.rand(B, T, H, W, c, device=DEV).to(torch.bfloat16) for c in widths]
+    fcs = [nn.Linear(c, c).to(DEV) for c in widths]
+    zh = [z.clone().requires_grad_(True) for z in zs]
+    out = h.gate_concat(zh, [f.weight for f in fcs], [f.bias for f in fcs],
+                        [z.float().sum(dim=(1, 2, 3)) for z in zs])
+    zr = [z.float().requires_grad_(True) for z in zs]
+    fr = [nn.Linear(c, c).to(DEV) for c in widths]
+    for a, b in zip(fr, fcs):
+        a.load_state_dict(b.state_dict())
+    outr = aten.gate_concat(zr, [f.weight for f in fr], [f.bias for f in fr])
+    assert rel_err(out, outr) < 1e-2
+    d = torch.randn_like(outr)
+    out.backward(d.to(torch.bfloat16))
+    outr.backward(d.to(torch.bfloat16).float())
+    for a, b in zip(zh, zr):
+        assert rel_err(a.grad, b.grad) < 2e-2
+    for a, b in zip(fcs, fr):
+        assert rel_err(a.weight.grad, b.weight.grad) < 2e-2
+        assert rel_err(a.bias.grad, b.bias.grad) < 2e-2
+
+
+def test_avgpool():
+    h = hip()
+    x = torch.randn(4, 2, 7, 7, 1024, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    y = h.global_avgpool(x)
+    assert rel_err(y, x.float().mean(dim=(1, 2, 3))) < 1e-4
+    y.sum().backward()
+    assert torch.allclose(x.grad.float(), torch.full_like(x.float(), 1 / 98.0), rtol=1e-2)
+
+
+def test_text_tower():
+    torch.manual_seed(4)
+    h = hip()
+    N, Wd, V = 16, 20, 1000
+    tok = torch.randint(0, V, (N, Wd), device=DEV)
+    table = torch.randn(V, 300, device=DEV)
+    fc1, fc2 = nn.Linear(300, 2048).to(DEV), nn.Linear(2048, 512).to(DEV)
+    out = h.text_tower(tok, table.to(torch.bfloat16), fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+    e = F.embedding(tok, table.to(torch.bfloat16).float())
+    w1 = nn.Parameter(fc1.weight.detach().to(torch.bfloat16).float())
+    b1 = nn.Parameter(fc1.bias.detach().to(torch.bfloat16).float())
+    w2 = nn.Parameter(fc2.weight.detach().clone())
+    b2 = nn.Parameter(fc2.bias.detach().clone())
+    ref = F.linear(aten.text_relu_max(F.linear(e, w1, b1)), w2, b2)
+    assert rel_err(out, ref) < 2e-2
+    d = torch.randn_like(ref)
+    out.backward(d)
+    ref.backward(d)
+    assert rel_err(fc2.weight.grad, w2.grad) < 2e-2
+    assert rel_err(fc1.weight.grad, w1.grad) < 3e-2
+    assert rel_err(fc1.bias.grad, b1.grad) < 3e-2
+
+
+@pytest.mark.parametrize("B,K", [(8, 4), (64, 5), (256, 4)])
+def test_milnce(B, K):
+    torch.manual_seed(5)
+    h = hip()
+    v = torch.randn(B, 512, device=DEV, requires_grad=True)
+    t = torch.randn(B * K, 512, device=DEV, requires_grad=True)
+    loss = h.milnce_loss(v, t)
+    vr = v.detach().clone().requires_grad_(True)
+    tr = t.detach().clone().requires_grad_(True)
+    lr = aten.milnce_loss(vr, tr)
+    assert abs(loss.item() - lr.item()) < 1e-3 * max(1.0, abs(lr.item()))
+    loss.backward()
+    lr.backward()
+    assert rel_err(v.grad, vr.grad) < 1e-4
+    assert rel_err(t.grad, tr.grad) < 1e-4
+
+
+def test_adam_matches_torch():
+    from mil_nce_howto100m_amd.train.optim import FlatAdam
+    torch.manual_seed(6)
+    ps = [nn.Parameter(torch.randn(37, 5, device=DEV)), nn.Parameter(torch.randn(1001, device=DEV))]
+    qs = [nn.Parameter(p.detach().clone()) for p in ps]
+    opt = FlatAdam(ps, lr=1e-2)
+    ref = torch.optim.Adam(qs, lr=1e-2)
+    for _ in range(5):
+        for p, q in zip(ps, qs):
+            g = torch.randn_like(p)
+            p.grad = g.clone()
+            q.grad = g.clone()
+        opt.step()
+        ref.step()
+    for p, q in zip(ps, qs):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+
+
+def test_synth_video_matches_torch():
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    s = SyntheticClips(3, 4, 32, device=torch.device(DEV))
+    ids = s.sample_ids(7)
+    lab = s.labels(ids)
+    a = s.video(ids, lab)
+    b = s._video_torch(ids, lab)
+    assert a.shape == b.shape == (3, 4, 32, 32, 4)
+    assert (a.int() - b.int()).abs().max().item() <= 1
+
+
+def test_stem_prep_reference_layout():
+    h = hip()
+    v = torch.randint(0, 256, (2, 3, 4, 6, 6), dtype=torch.uint8, device=DEV)
+    o = h.prepare_stem_input(v, native=False)
+    assert o.shape == (2, 4, 6, 6, 4)
+    assert torch.equal(o[..., :3], v.permute(0, 2, 3, 4, 1))
+    assert int(o[..., 3].abs().sum()) == 0
