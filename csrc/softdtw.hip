@@ -1,0 +1,202 @@
+// Soft-DTW (soft_dtw_cuda.py:34-112 semantics) and hard DTW with on-device backtracking
+// (dtw.py:22-75 semantics).
+//
+// soft-DTW forward: one workgroup per sequence pair, one lane per row i of R. Cell (i, j) is
+// computed on anti-diagonal pass p = (i-1) + (j-1); the three predecessors are the lane's own
+// previous value (R[i][j-1]) and the previous-row lane's values from passes p-1 (R[i-1][j]) and
+// p-2 (R[i-1][j-1]), exchanged through a 3-deep LDS ring, so only the final R goes to global
+// memory (it is saved for the backward). Up to 1024 rows per pair (16 waves).
+// The distance matrix of pair p is read in place from a (possibly shared) matrix:
+//     D_p[i][j] = D[(p / pair_div) * s_i + (p % pair_div) * s_j + i * ld + j]
+// so the b^2 all-pairs losses (loss.py:93-134) use ONE [b*n, b*m] GEMM output instead of the
+// reference's [b^2, n, m, d] expand.
+// soft-DTW backward: the reverse wavefront of the E recursion with the reference's boundary
+// handling (R = -inf outside, R[N+1][M+1] = R[N][M], +inf cells treated as -inf).
+// R and E are kept in fp64: R grows to ~sum of the path costs and the backward exponent
+// (R' - R - D) / gamma is a difference of such sums, which fp32 resolves only to ~1e-3 at
+// n ~ 100 (the DP is latency-bound, so fp64 costs nothing measurable).
+#include "common.h"
+
+struct PairIndex {
+  int pair_div, ld;
+  long long s_i, s_j;
+  __device__ __forceinline__ long long base(int p) const {
+    return (long long)(p / pair_div) * s_i + (long long)(p % pair_div) * s_j;
+  }
+};
+
+__global__ void softdtw_fwd_kernel(const float* __restrict__ D, PairIndex pi, int N, int M, float gamma_f, float bw,
+                                   double* __restrict__ R, float* __restrict__ out) {
+  extern __shared__ double ring[];  // [3][N+1]
+  const double gamma = gamma_f;
+  const int b = blockIdx.x;
+  const int i = threadIdx.x + 1;  // 1-based row
+  const bool row_ok = i <= N;
+  const float* Dp = D + pi.base(b);
+  double* Rp = R + (long long)b * (N + 2) * (M + 2);
+  const double inv_g = 1.0 / gamma;
+  // boundaries of R: R[0][0] = 0, everything else starts at +inf
+  for (int k = threadIdx.x; k < (N + 2) * (M + 2); k += blockDim.x) Rp[k] = INFINITY;
+  __syncthreads();
+  if (threadIdx.x == 0) Rp[0] = 0.0;
+  const int S = N + 1;
+  // ring slot for "row 0": R[0][j] = 0 if j == 0 else inf ; row i>0 at j<=0: inf
+  for (int k = threadIdx.x; k < 3 * S; k += blockDim.x) ring[k] = INFINITY;
+  __syncthreads();
+  double own_prev = INFINITY;  // R[i][j-1]
+  const int passes = N + M - 1;
+  for (int p = 0; p < passes; ++p) {
+    const int j = p - i + 2;
+    double val = INFINITY;
+    if (row_ok && j >= 1 && j <= M) {
+      // R[i-1][j] from pass p-1, R[i-1][j-1] from pass p-2 (row 0 handled analytically)
+      double up, diag;
+      if (i == 1) {
+        up = INFINITY;                  // R[0][j], j >= 1
+        diag = (j == 1) ? 0.0 : INFINITY;  // R[0][j-1]
+      } else {
+        up = ring[((p + 2) % 3) * S + (i - 1)];
+        diag = ring[((p + 1) % 3) * S + (i - 1)];
+        if (j == 1) diag = INFINITY;     // R[i-1][0]
+      }
+      const double left = own_prev;      // R[i][j-1] (inf at j == 1)
+      if (bw > 0.f && fabsf((float)(i - j)) > bw) {
+        val = INFINITY;
+      } else {
+        const double r0 = -diag * inv_g, r1 = -up * inv_g, r2 = -left * inv_g;
+        const double rmax = fmax(fmax(r0, r1), r2);
+        const double rsum = exp(r0 - rmax) + exp(r1 - rmax) + exp(r2 - rmax);
+        const double softmin = -gamma * (log(rsum) + rmax);
+        val = (double)Dp[(long long)(i - 1) * pi.ld + (j - 1)] + softmin;
+      }
+      Rp[(long long)i * (M + 2) + j] = val;
+      own_prev = val;
+    }
+    if (row_ok) ring[(p % 3) * S + i] = val;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[b] = (float)Rp[(long long)N * (M + 2) + M];
+}
+
+__device__ __forceinline__ double rv(const double* Rp, int i, int j, int N, int M) {
+  if (i == N + 1 && j == M + 1) {
+    const double v = Rp[(long long)N * (M + 2) + M];
+    return isinf(v) ? -INFINITY : v;
+  }
+  if (i == N + 1 || j == M + 1) return -INFINITY;
+  const double v = Rp[(long long)i * (M + 2) + j];
+  return isinf(v) ? -INFINITY : v;
+}
+
+__global__ void softdtw_bwd_kernel(const float* __restrict__ D, const double* __restrict__ R, PairIndex pi, int N,
+                                   int M, float gamma_f, float bw, const float* __restrict__ gout,
+                                   float* __restrict__ G) {
+  extern __shared__ double ring[];  // [3][N+2]
+  const double gamma = gamma_f;
+  const int b = blockIdx.x;
+  const int i = threadIdx.x + 1;
+  const bool row_ok = i <= N;
+  const float* Dp = D + pi.base(b);
+  const double* Rp = R + (long long)b * (N + 2) * (M + 2);
+  float* Gp = G + (long long)b * N * M;
+  const double inv_g = 1.0 / gamma;
+  const double g = gout[b];
+  const int S = N + 2;
+  for (int k = threadIdx.x; k < 3 * S; k += blockDim.x) ring[k] = 0.0;
+  __syncthreads();
+  double own_prev = 0.0;  // E[i][j+1]
+  const int passes = N + M - 1;
+  for (int q = 0; q < passes; ++q) {
+    const int p = passes - 1 - q;  // anti-diagonal index, descending
+    const int j = p - i + 2;
+    double e = 0.0;
+    if (row_ok && j >= 1 && j <= M) {
+      if (!(bw > 0.f && fabsf((float)(i - j)) > bw)) {
+        const double r = rv(Rp, i, j, N, M);
+        const double d_down = (i + 1 <= N) ? (double)Dp[(long long)i * pi.ld + (j - 1)] : 0.0;
+        const double d_right = (j + 1 <= M) ? (double)Dp[(long long)(i - 1) * pi.ld + j] : 0.0;
+        const double d_diag = (i + 1 <= N && j + 1 <= M) ? (double)Dp[(long long)i * pi.ld + j] : 0.0;
+        const double a = exp((rv(Rp, i + 1, j, N, M) - r - d_down) * inv_g);
+        const double bb = exp((rv(Rp, i, j + 1, N, M) - r - d_right) * inv_g);
+        const double c = exp((rv(Rp, i + 1, j + 1, N, M) - r - d_diag) * inv_g);
+        // E[i+1][j] from pass p+1 (row below), E[i+1][j+1] from pass p+2; E[N+1][M+1] = 1
+        double e_down, e_diag;
+        if (i == N) {
+          e_down = 0.0;
+          e_diag = (j == M) ? 1.0 : 0.0;
+        } else {
+          e_down = ring[((q + 2) % 3) * S + (i + 1)];
+          e_diag = (j == M) ? 0.0 : ring[((q + 1) % 3) * S + (i + 1)];
+        }
+        const double e_right = (j == M) ? 0.0 : own_prev;
+        e = e_down * a + e_right * bb + e_diag * c;
+      }
+      Gp[(long long)(i - 1) * M + (j - 1)] = (float)(e * g);
+      own_prev = e;
+    }
+    if (row_ok) ring[(q % 3) * S + i] = e;
+    __syncthreads();
+  }
+}
+
+static int block_for(int n) {
+  int t = ((n + 63) / 64) * 64;
+  return t < 64 ? 64 : t;
+}
+
+MILNCE_API int milnce_softdtw_fwd(const float* D, int B, int N, int M, int ld, int pair_div, long long s_i,
+                                  long long s_j, float gamma, float bandwidth, double* R, float* out,
+                                  hipStream_t stream) {
+  if (N > 1024) return (int)hipErrorInvalidValue;
+  PairIndex pi{pair_div, ld, s_i, s_j};
+  hipLaunchKernelGGL(softdtw_fwd_kernel, dim3(B), dim3(block_for(N)), 3 * (N + 1) * sizeof(double), stream, D, pi, N,
+                     M, gamma, bandwidth, R, out);
+  return (int)hipGetLastError();
+}
+
+MILNCE_API int milnce_softdtw_bwd(const float* D, const double* R, int B, int N, int M, int ld, int pair_div,
+                                  long long s_i, long long s_j, float gamma, float bandwidth, const float* gout,
+                                  float* G, hipStream_t stream) {
+  if (N > 1024) return (int)hipErrorInvalidValue;
+  PairIndex pi{pair_div, ld, s_i, s_j};
+  hipLaunchKernelGGL(softdtw_bwd_kernel, dim3(B), dim3(block_for(N)), 3 * (N + 2) * sizeof(double), stream, D, R, pi,
+                     N, M, gamma, bandwidth, gout, G);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Hard DTW (dtw.py): fp64 min-plus DP and the reference's backtracking, one lane per pair.
+__global__ void dtw_path_kernel(const double* __restrict__ cost, int B, int N, int M, double* __restrict__ tc,
+                                double* __restrict__ path) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const double* c = cost + (long long)b * N * M;
+  double* t = tc + (long long)b * N * M;
+  double* pa = path + (long long)b * N * M;
+  for (int k = 0; k < N * M; ++k) pa[k] = 0.0;
+  pa[(N - 1) * M + (M - 1)] = 1.0;
+  t[0] = c[0];
+  for (int i = 1; i < N; ++i) t[i * M] = t[(i - 1) * M] + c[i * M];
+  for (int j = 1; j < M; ++j) t[j] = t[j - 1] + c[j];
+  for (int i = 1; i < N; ++i)
+    for (int j = 1; j < M; ++j) {
+      const double v = fmin(fmin(t[(i - 1) * M + j - 1], t[(i - 1) * M + j]), t[i * M + j - 1]);
+      t[i * M + j] = v + c[i * M + j];
+    }
+  int i = N - 1, j = M - 1;
+  int guard = N + M + 2;
+  while (!(i == 0 || j == 0) && guard-- > 0) {
+    const double r = t[i * M + j] - c[i * M + j];
+    if (r == t[(i - 1) * M + j - 1]) { pa[(i - 1) * M + j - 1] = 1.0; --i; --j; }
+    else if (r == t[(i - 1) * M + j]) { pa[(i - 1) * M + j] = 1.0; --i; }
+    else if (r == t[i * M + j - 1]) { pa[i * M + j - 1] = 1.0; --j; }
+    else break;  // the reference prints 'error' and loops; we stop
+  }
+  pa[0] = 1.0;
+}
+
+MILNCE_API int milnce_dtw_path(const double* cost, int B, int N, int M, double* tc, double* path,
+                               hipStream_t stream) {
+  hipLaunchKernelGGL(dtw_path_kernel, dim3((B + 63) / 64), dim3(64), 0, stream, cost, B, N, M, tc, path);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""zero-shot retrieval on msrvtt (eval_msrvtt.py); same CLI flags as training (config.py).
+
+    python eval_msrvtt.py --pretrain_cnn_path checkpoint/run1/epoch0150.pth.tar \
+        --eval_video_root <videos> --num_windows_test 10 --num_frames 32 --video_size 224
+
+Uses the real CSV + videos when ffmpeg and the files exist, else a synthetic labelled set.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main(argv=None):
+    from mil_nce_howto100m_amd.config import get_args
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    from mil_nce_howto100m_amd.train.evaluation import eval_hmdb, eval_retrieval
+
+    args = get_args(argv=argv)
+    ctx = pdist.init_distributed(args.dist_backend, args.device)
+    return eval_retrieval(args, ctx.device, "msrvtt")
+
+
+if __name__ == "__main__":
+    main()

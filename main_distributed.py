@@ -1,0 +1,71 @@
+#!/usr/bin/env python3
+"""MIL-NCE pretraining entry point, CLI-compatible with the reference ``main_distributed.py``.
+
+    python main_distributed.py --batch_size 256 --num_frames 16 --video_size 200 \
+        --num_candidates 4 --lr 0.001 --warmup_steps 10000 --epochs 150 --checkpoint_dir run1
+
+Process model (replaces ``main_distributed.py:35-62`` / ``mp.spawn`` + UDP IP probe):
+  * under ``torchrun``/``torch.distributed.run`` (``WORLD_SIZE`` set): one rank per process;
+  * otherwise: one process per visible GPU, spawned here with a 127.0.0.1 rendezvous
+    (the reference forces ``--multiprocessing-distributed`` the same way, ``:48``);
+  * no GPU: single CPU process on gloo (the plumbing configuration).
+``--batch_size`` is global per node and divided across ranks (``:88``). Data is the on-device
+synthetic generator unless ``--synthetic 0`` (which needs ffmpeg + the HowTo100M files).
+"""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def _free_port() -> int:
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def worker(local_rank: int, world: int, port: int, argv):
+    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    run(argv)
+
+
+def run(argv):
+    from mil_nce_howto100m_amd.config import get_args
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    from mil_nce_howto100m_amd.train.engine import run_training
+
+    args = get_args(argv=argv)
+    if args.verbose and int(os.environ.get("RANK", "0")) == 0:
+        print(args, flush=True)
+    ctx = pdist.init_distributed(args.dist_backend, args.device, args.dist_timeout_s)
+    args.rank, args.world_size = ctx.rank, ctx.world_size
+    try:
+        if args.evaluate:
+            from mil_nce_howto100m_amd.train.evaluation import evaluate_hmdb_during_training
+            evaluate_hmdb_during_training(args, ctx)
+        run_training(args, ctx)
+    finally:
+        pdist.destroy()
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if "WORLD_SIZE" in os.environ:
+        return run(argv)
+    import torch
+    n = torch.cuda.device_count()
+    if n <= 1:
+        return run(argv)
+    import torch.multiprocessing as mp
+    mp.spawn(worker, nprocs=n, args=(n, _free_port(), argv))
+
+
+if __name__ == "__main__":
+    main()

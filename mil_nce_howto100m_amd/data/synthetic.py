@@ -107,10 +107,15 @@ class SyntheticSequences:
 
     def __init__(self, batch_size: int, seq_len: int, clips: SyntheticClips, clip_sec: float = 3.2):
         self.b, self.n, self.clips, self.clip_sec = batch_size, seq_len, clips, clip_sec
+        self.epoch_len = clips.epoch_len
+
+    def __len__(self) -> int:
+        return max(1, self.epoch_len // (self.b * self.n * self.clips.world))
 
     def batch(self, step: int) -> Dict[str, torch.Tensor]:
         c = self.clips
-        seq_ids = c.sample_ids(step)  # [b]
+        base = (step * c.world + c.rank) * self.b
+        seq_ids = torch.arange(base, base + self.b, device=c.device, dtype=torch.int64)
         ids = (seq_ids.view(-1, 1) * self.n + torch.arange(self.n, device=c.device).view(1, -1)).reshape(-1)
         labels = c.labels(ids)
         video = c.video(ids, labels)
@@ -118,3 +123,32 @@ class SyntheticSequences:
         start = (torch.arange(self.n, device=c.device).float() * self.clip_sec).view(1, -1).expand(self.b, -1)
         return {"video": video, "text": text, "label": labels.view(self.b, self.n),
                 "start": start.contiguous(), "end": (start + self.clip_sec).contiguous()}
+
+
+class SyntheticEvalSet:
+    """Labelled multi-window clips for the eval pipelines (linear probe / retrieval).
+
+    Video v has latent class ``labels(v)``; each of its ``num_clip`` windows is a different
+    sample of that class; its caption carries the class words. ``split{1,2,3}`` mimic the HMDB
+    CSV (1 = train, 2 = test, 0 = unused). Layout per batch: video uint8 [b, nc, T, S, S, 4].
+    """
+
+    def __init__(self, num_videos: int, num_clip: int = 4, num_frames: int = 16, size: int = 64,
+                 num_classes: int = 8, max_words: int = 30, vocab_size: int = 66250, seed: int = 3,
+                 device: torch.device = torch.device("cpu")):
+        self.n, self.nc = num_videos, num_clip
+        self.clips = SyntheticClips(1, num_frames, size, 1, max_words, vocab_size, num_classes, seed, device)
+
+    def batches(self, batch_size: int):
+        c = self.clips
+        for s in range(0, self.n, batch_size):
+            vids = torch.arange(s, min(self.n, s + batch_size), device=c.device)
+            labels = c.labels(vids)
+            ids = (vids.view(-1, 1) * 1000 + torch.arange(self.nc, device=c.device).view(1, -1)).reshape(-1)
+            video = c.video(ids, labels.repeat_interleave(self.nc))
+            b = vids.shape[0]
+            video = video.view((b, self.nc) + tuple(video.shape[1:]))
+            text = c.text(vids * 1000 + 7, labels)[:, 0]
+            split = [(((vids + k) % 3) != 0).long() + ((vids + k) % 3 == 0).long() * 2 for k in range(3)]
+            yield {"video": video, "text": text, "label": [f"class{int(l)}" for l in labels.tolist()],
+                   "split1": split[0].cpu(), "split2": split[1].cpu(), "split3": split[2].cpu()}

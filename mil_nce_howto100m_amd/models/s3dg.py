@@ -204,14 +204,13 @@ class S3D(nn.Module):
             v = video[..., :3]
         else:
             v = video.permute(0, 2, 3, 4, 1)
+        wdt = self.conv1.conv1.weight.dtype
         if v.dtype == torch.uint8:
-            v = v.float() / 255.0
+            v = v.to(wdt) / 255.0
         v = v.contiguous()
         if video.is_cuda:
-            v = v.to(torch.bfloat16)
-        else:
-            v = v.float()
-        return v
+            return v.to(torch.bfloat16)
+        return v.to(wdt)
 
     def forward_video(self, inputs, mixed5c=False):
         net = self.prepare_video(inputs)

@@ -39,7 +39,7 @@ def gate_concat(branches: Sequence[torch.Tensor], fc_weights: Sequence[torch.Ten
     """SelfGating on each branch (s3dg.py:47-59) followed by channel concat (s3dg.py:45)."""
     outs = []
     for z, w, b in zip(branches, fc_weights, fc_biases):
-        m = z.float().mean(dim=(1, 2, 3))
+        m = z.to(w.dtype).mean(dim=(1, 2, 3))
         g = torch.sigmoid(F.linear(m, w, b)).to(z.dtype)
         outs.append(z * g[:, None, None, None, :])
     return outs[0] if len(outs) == 1 else torch.cat(outs, dim=-1)
@@ -69,7 +69,7 @@ def maxpool_s1(x):
 
 def global_avgpool(x):
     """mean over T, H, W (s3dg.py:323)."""
-    return x.float().mean(dim=(1, 2, 3))
+    return (x.float() if x.dtype in (torch.bfloat16, torch.float16) else x).mean(dim=(1, 2, 3))
 
 
 def text_relu_max(h: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,272 @@
+"""Soft-DTW and hard DTW (``soft_dtw_cuda.py``, ``dtw.py``), MI355X-native.
+
+* GPU: the wavefront DP is a HIP kernel (``csrc/softdtw.hip``), one workgroup per pair, one
+  lane per row, R kept for the backward; the backward is the reverse wavefront. The distance
+  matrix is produced by one batched GEMM (hipBLASLt) — never by the reference's
+  ``[B, N, M, D]`` expand — and the all-pairs form reads every pair's block in place from a
+  single ``[b*n, b*m]`` GEMM output.
+* CPU: a float64 numpy implementation of the same recursions (the oracle for the GPU kernel,
+  mirroring the reference's Numba CPU path ``soft_dtw_cuda.py:185-240``).
+
+Distance functions (``soft_dtw_cuda.py:325-363``): ``cosine`` -> exp(1 - cos) (sic),
+``negative_dot`` -> -<x, y>, ``euclidean`` -> exp(||x - y||) (sic), ``negative_cosine``
+-> -cos (referenced but undefined in the reference), and ``None`` -> squared Euclidean, the
+default the reference docstring promises but never assigns (§2.10 item 13).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from . import use_hip
+
+# ----------------------------------------------------------------------------------------
+# distance matrices via GEMM
+# ----------------------------------------------------------------------------------------
+
+
+def _bmm_t(x, y):
+    return torch.matmul(x, y.transpose(-1, -2))
+
+
+def dist_matrix(x: torch.Tensor, y: torch.Tensor, kind: Optional[str]) -> torch.Tensor:
+    """x [..., n, d], y [..., m, d] -> [..., n, m] (fp32)."""
+    x = x.float()
+    y = y.float()
+    if kind == "negative_dot":
+        return -_bmm_t(x, y)
+    if kind in ("cosine", "negative_cosine"):
+        nx = x.norm(dim=-1, keepdim=True)
+        ny = y.norm(dim=-1, keepdim=True)
+        cos = _bmm_t(x, y) / torch.clamp(nx * ny.transpose(-1, -2), min=1e-8)
+        return torch.exp(1.0 - cos) if kind == "cosine" else -cos
+    xx = (x * x).sum(-1, keepdim=True)
+    yy = (y * y).sum(-1, keepdim=True).transpose(-1, -2)
+    sq = torch.clamp(xx + yy - 2.0 * _bmm_t(x, y), min=0.0)
+    if kind == "euclidean":
+        return torch.exp(torch.sqrt(sq + 1e-12))
+    if kind is None or kind == "sqeuclidean":
+        return sq
+    raise ValueError(f"unknown dist_func {kind}")
+
+
+# ----------------------------------------------------------------------------------------
+# CPU oracle (float64)
+# ----------------------------------------------------------------------------------------
+
+
+def softdtw_forward_np(D: np.ndarray, gamma: float, bandwidth: float):
+    B, N, M = D.shape
+    R = np.full((B, N + 2, M + 2), np.inf)
+    R[:, 0, 0] = 0.0
+    for p in range(N + M - 1):
+        i = np.arange(max(1, p + 2 - M), min(N, p + 1) + 1)
+        j = p + 2 - i
+        if bandwidth > 0:
+            keep = np.abs(i - j) <= bandwidth
+            i, j = i[keep], j[keep]
+        if i.size == 0:
+            continue
+        r0 = -R[:, i - 1, j - 1] / gamma
+        r1 = -R[:, i - 1, j] / gamma
+        r2 = -R[:, i, j - 1] / gamma
+        rmax = np.maximum(np.maximum(r0, r1), r2)
+        with np.errstate(invalid="ignore", over="ignore"):
+            rsum = np.exp(r0 - rmax) + np.exp(r1 - rmax) + np.exp(r2 - rmax)
+            R[:, i, j] = D[:, i - 1, j - 1] - gamma * (np.log(rsum) + rmax)
+    return R
+
+
+def softdtw_backward_np(D: np.ndarray, R: np.ndarray, gamma: float, bandwidth: float) -> np.ndarray:
+    B, N, M = D.shape
+    Dp = np.zeros((B, N + 2, M + 2))
+    Dp[:, 1:N + 1, 1:M + 1] = D
+    R = R.copy()
+    R[:, :, -1] = -np.inf
+    R[:, -1, :] = -np.inf
+    R[:, -1, -1] = R[:, -2, -2]
+    R[np.isinf(R)] = -np.inf
+    E = np.zeros((B, N + 2, M + 2))
+    E[:, -1, -1] = 1.0
+    for p in range(N + M - 2, -1, -1):
+        i = np.arange(max(1, p + 2 - M), min(N, p + 1) + 1)
+        j = p + 2 - i
+        if bandwidth > 0:
+            keep = np.abs(i - j) <= bandwidth
+            i, j = i[keep], j[keep]
+        if i.size == 0:
+            continue
+        with np.errstate(invalid="ignore", over="ignore"):
+            a = np.exp((R[:, i + 1, j] - R[:, i, j] - Dp[:, i + 1, j]) / gamma)
+            b = np.exp((R[:, i, j + 1] - R[:, i, j] - Dp[:, i, j + 1]) / gamma)
+            c = np.exp((R[:, i + 1, j + 1] - R[:, i, j] - Dp[:, i + 1, j + 1]) / gamma)
+        E[:, i, j] = E[:, i + 1, j] * a + E[:, i, j + 1] * b + E[:, i + 1, j + 1] * c
+    return E[:, 1:N + 1, 1:M + 1]
+
+
+class _SoftDTWCPU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, D, gamma, bandwidth):
+        Dn = D.detach().cpu().double().numpy()
+        R = softdtw_forward_np(Dn, gamma, bandwidth)
+        ctx.save_for_backward(D)
+        ctx.R, ctx.gamma, ctx.bw = R, gamma, bandwidth
+        return torch.from_numpy(R[:, -2, -2].copy()).to(D.device, D.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        (D,) = ctx.saved_tensors
+        E = softdtw_backward_np(D.detach().cpu().double().numpy(), ctx.R, ctx.gamma, ctx.bw)
+        E = torch.from_numpy(E).to(D.device, D.dtype)
+        return g.view(-1, 1, 1) * E, None, None
+
+
+# ----------------------------------------------------------------------------------------
+# GPU kernels
+# ----------------------------------------------------------------------------------------
+
+
+class _SoftDTWHIP(torch.autograd.Function):
+    """D: [P, N, M] (layout 'batch') or [b*n, b*m] (layout 'pairs', P = b*b)."""
+
+    @staticmethod
+    def forward(ctx, D, gamma, bandwidth, pairs_b):
+        from ._lib import call, ptr, stream
+        D = D.float().contiguous()
+        if pairs_b:
+            b = pairs_b
+            n, m = D.shape[0] // b, D.shape[1] // b
+            P, ld, div, s_i, s_j = b * b, D.shape[1], b, n * D.shape[1], m
+        else:
+            P, n, m = D.shape
+            ld, div, s_i, s_j = m, 1, n * m, 0
+        R = torch.empty((P, n + 2, m + 2), dtype=torch.float64, device=D.device)
+        out = torch.empty((P,), dtype=torch.float32, device=D.device)
+        call("milnce_softdtw_fwd", ptr(D), P, n, m, ld, div, s_i, s_j, float(gamma), float(bandwidth),
+             ptr(R), ptr(out), stream())
+        ctx.save_for_backward(D, R)
+        ctx.meta = (gamma, bandwidth, pairs_b, P, n, m, ld, div, s_i, s_j)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, ptr, stream
+        D, R = ctx.saved_tensors
+        gamma, bw, pairs_b, P, n, m, ld, div, s_i, s_j = ctx.meta
+        G = torch.empty((P, n, m), dtype=torch.float32, device=D.device)
+        call("milnce_softdtw_bwd", ptr(D), ptr(R), P, n, m, ld, div, s_i, s_j, float(gamma), float(bw),
+             ptr(g.float().contiguous()), ptr(G), stream())
+        if pairs_b:
+            b = pairs_b
+            G = G.view(b, b, n, m).permute(0, 2, 1, 3).reshape(b * n, b * m)
+        return G, None, None, None
+
+
+def softdtw_from_dist(D: torch.Tensor, gamma: float, bandwidth: float = 0.0) -> torch.Tensor:
+    """Batched soft-DTW value of distance matrices D [B, N, M] -> [B]."""
+    if use_hip(D):
+        return _SoftDTWHIP.apply(D, gamma, bandwidth, 0)
+    return _SoftDTWCPU.apply(D, gamma, bandwidth)
+
+
+def softdtw_pairwise_from_dist(Dbig: torch.Tensor, b: int, gamma: float, bandwidth: float = 0.0) -> torch.Tensor:
+    """All b*b pairs from one [b*n, b*m] distance matrix -> [b, b], out[i, j] = sdtw(block(i, j))."""
+    if use_hip(Dbig):
+        return _SoftDTWHIP.apply(Dbig, gamma, bandwidth, b).view(b, b)
+    n, m = Dbig.shape[0] // b, Dbig.shape[1] // b
+    D = Dbig.view(b, n, b, m).permute(0, 2, 1, 3).reshape(b * b, n, m)
+    return _SoftDTWCPU.apply(D, gamma, bandwidth).view(b, b)
+
+
+class SoftDTW(torch.nn.Module):
+    """Drop-in for the reference ``SoftDTW`` (``soft_dtw_cuda.py:274-386``)."""
+
+    def __init__(self, use_cuda: bool = True, gamma: float = 1.0, normalize: bool = False,
+                 bandwidth: Optional[float] = None, dist_func: Optional[str] = None):
+        super().__init__()
+        self.gamma = gamma
+        self.normalize = normalize
+        self.bandwidth = 0.0 if bandwidth is None else float(bandwidth)
+        self.use_cuda = use_cuda  # device placement follows the inputs
+        self.dist_func = dist_func
+
+    def forward(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+        assert X.shape[0] == Y.shape[0] and X.shape[2] == Y.shape[2]
+        if self.normalize:
+            x = torch.cat([X, X, Y])
+            y = torch.cat([Y, X, Y])
+            out = softdtw_from_dist(dist_matrix(x, y, self.dist_func), self.gamma, self.bandwidth)
+            out_xy, out_xx, out_yy = torch.split(out, X.shape[0])
+            return out_xy - 0.5 * (out_xx + out_yy)
+        return softdtw_from_dist(dist_matrix(X, Y, self.dist_func), self.gamma, self.bandwidth)
+
+    def pairwise(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+        """[b, n, d] x [b, m, d] -> [b, b] with out[i, j] = sdtw(X[i], Y[j]); one GEMM."""
+        b, n, d = X.shape
+        m = Y.shape[1]
+        Dbig = dist_matrix(X.reshape(b * n, d), Y.reshape(b * m, d), self.dist_func)
+        return softdtw_pairwise_from_dist(Dbig, b, self.gamma, self.bandwidth)
+
+
+# ----------------------------------------------------------------------------------------
+# hard DTW (dtw.py)
+# ----------------------------------------------------------------------------------------
+
+
+def _dtw_path_np(cost: np.ndarray) -> np.ndarray:
+    B, N, M = cost.shape
+    path = np.zeros_like(cost)
+    path[:, N - 1, M - 1] = 1
+    for b in range(B):
+        c = cost[b]
+        tc = np.full((N, M), np.inf)
+        tc[0, 0] = c[0, 0]
+        for i in range(1, N):
+            tc[i, 0] = tc[i - 1, 0] + c[i, 0]
+        for j in range(1, M):
+            tc[0, j] = tc[0, j - 1] + c[0, j]
+        for i in range(1, N):
+            for j in range(1, M):
+                tc[i, j] = min(tc[i - 1, j - 1], tc[i - 1, j], tc[i, j - 1]) + c[i, j]
+        i, j = N - 1, M - 1
+        while not (i == 0 or j == 0):
+            r = tc[i, j] - c[i, j]
+            if r == tc[i - 1, j - 1]:
+                path[b, i - 1, j - 1] = 1; i -= 1; j -= 1
+            elif r == tc[i - 1, j]:
+                path[b, i - 1, j] = 1; i -= 1
+            elif r == tc[i, j - 1]:
+                path[b, i, j - 1] = 1; j -= 1
+            else:
+                break
+        path[b, 0, 0] = 1
+    return path
+
+
+class DTW(torch.nn.Module):
+    """Hard-DTW alignment loss of ``dtw.py:5-75``: cosine cost, min-plus DP, backtracked path,
+    ``logsumexp(sum_i cost*path) - logsumexp(sum_i cost)`` (gradient through the cost only)."""
+
+    def __init__(self, use_cuda: bool = True):
+        super().__init__()
+        self.use_cuda = use_cuda
+
+    def forward(self, x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        cost = (1.0 - (dist_matrix(x, y, "negative_cosine") * -1.0)).double()
+        with torch.no_grad():
+            if use_hip(cost):
+                from ._lib import call, ptr, stream
+                B, N, M = cost.shape
+                c = cost.detach().contiguous()
+                tc = torch.empty_like(c)
+                path = torch.empty_like(c)
+                call("milnce_dtw_path", ptr(c), B, N, M, ptr(tc), ptr(path), stream())
+            else:
+                path = torch.from_numpy(_dtw_path_np(cost.detach().cpu().numpy())).to(cost.device)
+        pos = torch.logsumexp(torch.sum(cost * path, dim=1), dim=1)
+        neg = torch.logsumexp(torch.sum(cost, dim=1), dim=1)
+        return pos - neg

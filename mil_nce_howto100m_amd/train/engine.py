@@ -81,7 +81,22 @@ class Trainer:
         text = text.reshape(-1, text.shape[-1])
         video_embd, text_embd = self.model(video, text)
         video_embd, text_embd = pdist.all_gather_embeddings(video_embd, text_embd, self.ctx)
-        return self.criterion(video_embd, text_embd)
+        name = getattr(self.args, "loss", "milnce")
+        if name == "milnce":
+            return self.criterion(video_embd, text_embd)
+        # soft-DTW family: sequences of seq_len clips, one caption per clip (BASELINE config 4)
+        n = getattr(self.args, "seq_len", 8)
+        v = video_embd.view(-1, n, video_embd.shape[-1])
+        t = text_embd.view(-1, n, text_embd.shape[-1])
+        if name == "sdtw_cidm":
+            start = batch["start"]
+            if self.ctx.world_size > 1:
+                out = start.new_empty((self.ctx.world_size,) + tuple(start.shape))
+                torch.distributed.all_gather_into_tensor(out, start.contiguous())
+                start = out.view(-1, start.shape[-1])
+            return self.criterion(v, t, start)
+        out = self.criterion(v, t)
+        return sum(out) if isinstance(out, tuple) else out
 
     def train_step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         self.model.train()
@@ -119,11 +134,15 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
 
     ctx = ctx or pdist.context()
     seed_everything(args.seed, ctx.rank)
-    # batch_size is global per node; divided across the ranks like main_distributed.py:88.
-    local_bs = max(1, args.batch_size // max(1, ctx.world_size))
+    # batch_size is per node; divided across the node's GPUs like main_distributed.py:88.
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size)))
+    local_bs = max(1, args.batch_size // max(1, local_world))
     data = SyntheticClips(local_bs, args.num_frames, args.video_size, args.num_candidates,
                           args.max_words, args.vocab_size, seed=args.seed, device=ctx.device,
                           rank=ctx.rank, world_size=ctx.world_size, epoch_len=args.synthetic_len)
+    if getattr(args, "loss", "milnce") != "milnce":
+        from ..data.synthetic import SyntheticSequences
+        data = SyntheticSequences(local_bs, args.seq_len, data)
     steps_per_epoch = len(data) if not args.steps_per_epoch else min(len(data), args.steps_per_epoch)
     model = build_model(args, ctx.device)
     trainer = Trainer(args, model, ctx, steps_per_epoch)
