@@ -12,21 +12,37 @@
 #include "common.h"
 
 // ---------------------------------------------------------------------------------------
-__global__ void bn_finalize_kernel(const float* __restrict__ part, int nparts, int Npad, int C, double count,
-                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                   float* __restrict__ rmean, float* __restrict__ rvar,
-                                   long long* __restrict__ nbt, float momentum, float eps, int training,
-                                   float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (training && c == 0 && nbt != nullptr) nbt[0] += 1;
-  if (c >= C) return;
-  float mean, var;
-  if (training) {
-    double s = 0.0, q = 0.0;
-    for (int i = 0; i < nparts; ++i) {
+// Block = 32 channels x 8 partial-row groups; the partial slab [nparts][2][Npad] is read
+// coalesced along channels and reduced in fp64 (nparts can be ~1000 per-block partials).
+__global__ __launch_bounds__(256) void bn_finalize_kernel(
+    const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
+    float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */) {
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  if (training && blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
+  double s = 0.0, q = 0.0;
+  if (training && c < C) {
+    int i = rg;
+    for (; i + 24 < nparts; i += 32) {
+      const float* p0 = part + (long long)i * 2 * Npad + c;
+      const long long st = 8LL * 2 * Npad;
+      s += (double)p0[0] + (double)p0[st] + (double)p0[2 * st] + (double)p0[3 * st];
+      q += (double)p0[Npad] + (double)p0[st + Npad] + (double)p0[2 * st + Npad] + (double)p0[3 * st + Npad];
+    }
+    for (; i < nparts; i += 8) {
       s += (double)part[(long long)i * 2 * Npad + c];
       q += (double)part[(long long)i * 2 * Npad + Npad + c];
     }
+  }
+  red[0][rg][cl] = s;
+  red[1][rg][cl] = q;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) { s += red[0][k][cl]; q += red[1][k][cl]; }
+  float mean, var;
+  if (training) {
     const double m = s / count;
     double v = q / count - m * m;
     if (v < 0.0) v = 0.0;
@@ -162,18 +178,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
   }
 }
 
-// coef[4][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n, unused}; dgamma/dbeta accumulated into grads.
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C, double count,
-                                       const float* __restrict__ gamma, const float* __restrict__ ss,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                       float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+                                                              double count, const float* __restrict__ gamma,
+                                                              const float* __restrict__ ss, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, float* __restrict__ coef) {
+  __shared__ double red[2][8][32];
+  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   double s1 = 0.0, s2 = 0.0;
-  for (int i = 0; i < nparts; ++i) {
-    s1 += part[(long long)i * 2 * C + c];
-    s2 += part[(long long)i * 2 * C + C + c];
+  if (c < C) {
+    for (int i = rg; i < nparts; i += 8) {
+      s1 += part[(long long)i * 2 * C + c];
+      s2 += part[(long long)i * 2 * C + C + c];
+    }
   }
+  red[0][rg][cl] = s1;
+  red[1][rg][cl] = s2;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  for (int k = 1; k < 8; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
   dbeta[c] = (float)s1;
   dgamma[c] = (float)s2;
   coef[c] = gamma[c] * ss[C + c];
@@ -209,7 +233,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 MILNCE_API int milnce_bn_finalize(const float* part, int nparts, int Npad, int C, double count, const float* gamma,
                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
                                   float eps, int training, float* out, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nparts, Npad, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, Npad, C,
                      count, gamma, beta, rmean, rvar, nbt, momentum, eps, training, out);
   return (int)hipGetLastError();
 }
@@ -237,7 +261,7 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
   const int rows_per_block = (int)((M + nparts - 1) / nparts);
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
                      (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, part, nparts, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, C,
                      (double)M, gamma, ss, dgamma, dbeta, coef);
   const long long nchunks = M * (C / 8);
   long long grid = (nchunks + 255) / 256;

@@ -31,7 +31,8 @@ struct ConvParams {
   int Ktot, Kpad, ldy, M;
   int num_m_tiles, num_n_tiles, grid_m;
   float in_scale;
-  FastDiv fWo, fHo, fTo;
+  long long x_total_bytes;
+  FastDiv fWo, fHo, fTo, fCin;
 };
 
 template <int BK>
@@ -41,9 +42,93 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   else return chunk ^ ((row >> 1) & 7);
 }
 
+// Tap table entry: .x = element offset of the tap inside a clip ((dt*H + dh)*W + dw)*Cin,
+// .y = dt | dh << 8 | dw << 16.
+__device__ __forceinline__ void build_tap_table(int2* tab, int KT, int KH, int KW, int H, int W, int Cin) {
+  const int taps = KT * KH * KW;
+  for (int t = threadIdx.x; t < taps; t += blockDim.x) {
+    const int dw = t % KW, dh = (t / KW) % KH, dt = t / (KW * KH);
+    tab[t] = make_int2(((dt * H + dh) * W + dw) * Cin, dt | (dh << 8) | (dw << 16));
+  }
+}
+
+template <int N, int CPR, int BK>
+__device__ __forceinline__ void load_w_tile(uint4 (&r)[N], const bf16_t* __restrict__ w, int n0, int Kpad, int kt,
+                                            int tid, int ccol) {
+  const bf16_t* base = w + (long long)n0 * Kpad + kt * BK + ccol * 8;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int row = (tid + i * 256) / CPR;
+    r[i] = *(const uint4*)(base + (long long)row * Kpad);
+  }
+}
+
+// Implicit-im2col gather of this thread's A chunks for K tile kt (buffer loads: out-of-range
+// offsets return zero, so padding, tail rows and K padding are branch-free).
+template <int N, int VEC, int ESZ, int BK, bool U8, typename AReg>
+__device__ __forceinline__ void gather_a_tile(AReg (&areg)[N], __amdgpu_buffer_rsrc_t rsrc, const int2* tab,
+                                              const ConvParams& p, const int (&rt)[N], const int (&rh)[N],
+                                              const int (&rw)[N], const uint32_t (&rowoff)[N], int kt, int a_ccol,
+                                              int taps) {
+  const int k = kt * BK + a_ccol * VEC;
+  const int tap = (int)fdiv((uint32_t)k, p.fCin);
+  const int c = k - tap * p.Cin;
+  const bool kval = tap < taps;
+  const int2 te = tab[min(tap, taps - 1)];  // unconditional: no exec-mask branch
+  const int dt = te.y & 0xff, dh = (te.y >> 8) & 0xff, dw = te.y >> 16;
+  const uint32_t koff = (uint32_t)((te.x + c) * ESZ);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
+    const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+                   ((unsigned)wi < (unsigned)p.W);
+    const uint32_t off = v ? rowoff[i] + koff : 0x80000000u;  // > num_records: reads 0
+    if constexpr (U8) {
+      areg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+    } else {
+      auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+      areg[i] = __builtin_bit_cast(uint4, r);
+    }
+  }
+}
+
+template <int NA, int NB, int A_CPR, int B_CPR, int BM, int BN, int BK, bool U8, typename AReg>
+__device__ __forceinline__ void store_tiles(const AReg (&areg)[NA], const uint4 (&breg)[NB], bf16_t* As, bf16_t* Bs,
+                                            int buf, int tid, int a_ccol, int b_ccol, float in_scale) {
+  bf16_t* a = As + buf * BM * BK;
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = (tid + i * 256) / A_CPR;
+    if constexpr (U8) {
+      const uint32_t v = areg[i];
+      uint2 o;
+      o.x = pack2bf((float)(v & 0xff) * in_scale, (float)((v >> 8) & 0xff) * in_scale);
+      o.y = pack2bf((float)((v >> 16) & 0xff) * in_scale, (float)(v >> 24) * in_scale);
+      const int k0 = a_ccol * 4;
+      const int ch = swz<BK>(row, k0 >> 3);
+      *(uint2*)(a + row * BK + ch * 8 + (k0 & 4)) = o;
+    } else {
+      const int ch = swz<BK>(row, a_ccol);
+      *(uint4*)(a + row * BK + ch * 8) = areg[i];
+    }
+  }
+  bf16_t* bsh = Bs + buf * BN * BK;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = (tid + i * 256) / B_CPR;
+    const int ch = swz<BK>(row, b_ccol);
+    *(uint4*)(bsh + row * BK + ch * 8) = breg[i];
+  }
+}
+
+// A operand of the MFMA = weight tile (rows n), B operand = gathered activations (cols m), so
+// each lane's accumulator holds 4 consecutive output channels of one output position: the
+// epilogue packs them into 8-byte LDS writes and the per-channel BN sums accumulate per lane
+// across the persistent M loop (one cross-lane reduction per kernel, not per tile).
 template <int BM, int BN, int BK, bool U8>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   constexpr int VEC = U8 ? 4 : 8;
+  constexpr int ESZ = U8 ? 1 : 2;
   constexpr int A_CPR = BK / VEC;
   constexpr int A_CH = BM * A_CPR / 256;
   constexpr int B_CPR = BK / 8;
@@ -51,13 +136,17 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int KSTEPS = BK / 32;
-  constexpr int EPAD = 16;  // epilogue staging row pad (elements)
+  constexpr int LDE = BN + 8;  // epilogue staging row (elements): 16-B aligned, 2-way max on b64 writes
+  constexpr int KLOOP_ELEMS = 2 * (BM + BN) * BK;
+  constexpr int EPI_ELEMS = BM * LDE;
+  constexpr int TAB_OFF_BYTES = 2 * (KLOOP_ELEMS > EPI_ELEMS ? KLOOP_ELEMS : EPI_ELEMS);
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* As = (bf16_t*)smem;          // [2][BM][BK]
-  bf16_t* Bs = As + 2 * BM * BK;       // [2][BN][BK]
-  bf16_t* Es = (bf16_t*)smem;          // epilogue [BM][BN+EPAD]
+  bf16_t* As = (bf16_t*)smem;          // [2][BM][BK]   activations (MFMA B operand)
+  bf16_t* Bs = As + 2 * BM * BK;       // [2][BN][BK]   weights     (MFMA A operand)
+  bf16_t* Es = (bf16_t*)smem;          // epilogue [BM][LDE]
+  int2* tab = (int2*)(smem + TAB_OFF_BYTES);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -70,22 +159,32 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   const int m_slot = logical / p.num_n_tiles;
   const int n0 = n_tile * BN;
   const int nk = p.Kpad / BK;
-
   const int a_ccol = tid % A_CPR;
   const int b_ccol = tid % B_CPR;
+  const int taps = p.KT * p.KH * p.KW;
+  const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
+  const uint32_t clip_bytes = (uint32_t)(p.x_bstride * ESZ);
 
-  float st_s[TN], st_q[TN];
+  build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
+
+  float st_s[TN][4], st_q[TN][4];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
-
-  const uint8_t* xb = (const uint8_t*)p.x;
-  const int esize = U8 ? 1 : 2;
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { st_s[j][r] = 0.f; st_q[j][r] = 0.f; }
 
   for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
     const int m0 = m_tile * BM;
-    // ---- per-row gather coordinates for this M tile ----
-    const uint8_t* rbase[A_CH];
-    int rt[A_CH], rh[A_CH], rw[A_CH], rowoff[A_CH];
+    // Buffer descriptor based at the tile's first clip: out-of-range offsets read as zero, so
+    // padding / tail rows / K padding need no branches around the loads.
+    const uint32_t b0 = (uint32_t)m0 / thw;
+    const char* base = (const char*)p.x + (long long)b0 * p.x_bstride * ESZ;
+    const long long remain = p.x_total_bytes - (long long)b0 * p.x_bstride * ESZ;
+    const uint32_t nrec = remain > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)remain;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nrec, 0x00020000);
+
+    int rt[A_CH], rh[A_CH], rw[A_CH];
+    uint32_t rowoff[A_CH];  // byte offset of the (unshifted) row origin relative to base
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid + i * 256) / A_CPR;
@@ -97,166 +196,90 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
         const int ho = q - q2 * p.Ho;
         uint32_t b = fdiv(q2, p.fTo);
         const int to = q2 - b * p.To;
-        rbase[i] = xb + (long long)b * p.x_bstride * esize;
         rt[i] = to * p.st - p.pt;
         rh[i] = ho * p.sh - p.ph;
         rw[i] = wo * p.sw - p.pw;
-        rowoff[i] = ((rt[i] * p.H + rh[i]) * p.W + rw[i]) * p.Cin;
+        rowoff[i] = (b - b0) * clip_bytes + (uint32_t)(((rt[i] * p.H + rh[i]) * p.W + rw[i]) * p.Cin * ESZ);
       } else {
-        rbase[i] = xb;
         rt[i] = -(1 << 28);
         rh[i] = 0;
         rw[i] = 0;
         rowoff[i] = 0;
       }
     }
-    // ---- k state (tap, channel) of this thread's A chunk ----
-    int kc = a_ccol * VEC;  // channel within tap
-    int tap = 0, dt = 0, dh = 0, dw = 0;
-    while (kc >= p.Cin) {
-      kc -= p.Cin; ++tap;
-      if (++dw == p.KW) { dw = 0; if (++dh == p.KH) { dh = 0; ++dt; } }
-    }
-    const int taps = p.KT * p.KH * p.KW;
 
     using AReg = typename std::conditional<U8, uint32_t, uint4>::type;
     AReg areg[A_CH];
     uint4 breg[B_CH];
 
-    auto load_a = [&]() {
-      const bool kval = tap < taps;
-      const int toff = ((dt * p.H + dh) * p.W + dw) * p.Cin + kc;
+    f32x4 acc[TN][TM];
 #pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
-        const bool v = kval && (unsigned)ti < (unsigned)p.T && (unsigned)hi < (unsigned)p.H &&
-                       (unsigned)wi < (unsigned)p.W;
-        const int off = rowoff[i] + toff;  // element offset inside the clip
-        if constexpr (U8) {
-          areg[i] = v ? *(const uint32_t*)(rbase[i] + off) : 0u;
-        } else {
-          areg[i] = v ? *(const uint4*)(rbase[i] + (long long)off * 2) : make_uint4(0, 0, 0, 0);
-        }
-      }
-    };
-    auto advance_k = [&]() {
-      kc += BK;
-      while (kc >= p.Cin) {
-        kc -= p.Cin; ++tap;
-        if (++dw == p.KW) { dw = 0; if (++dh == p.KH) { dh = 0; ++dt; } }
-      }
-    };
-    auto load_b = [&](int kt) {
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int i = 0; i < B_CH; ++i) {
-        const int row = (tid + i * 256) / B_CPR;
-        breg[i] = *(const uint4*)(p.w + (long long)(n0 + row) * p.Kpad + kt * BK + b_ccol * 8);
-      }
-    };
-    auto store_ab = [&](int buf) {
-      bf16_t* a = As + buf * BM * BK;
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) {
-        const int row = (tid + i * 256) / A_CPR;
-        if constexpr (U8) {
-          const uint32_t v = areg[i];
-          const float s = p.in_scale;
-          uint2 o;
-          o.x = pack2bf((float)(v & 0xff) * s, (float)((v >> 8) & 0xff) * s);
-          o.y = pack2bf((float)((v >> 16) & 0xff) * s, (float)(v >> 24) * s);
-          const int k0 = a_ccol * 4;
-          const int ch = swz<BK>(row, k0 >> 3);
-          *(uint2*)(a + row * BK + ch * 8 + (k0 & 4)) = o;
-        } else {
-          const int ch = swz<BK>(row, a_ccol);
-          *(uint4*)(a + row * BK + ch * 8) = areg[i];
-        }
-      }
-      bf16_t* bsh = Bs + buf * BN * BK;
-#pragma unroll
-      for (int i = 0; i < B_CH; ++i) {
-        const int row = (tid + i * 256) / B_CPR;
-        const int ch = swz<BK>(row, b_ccol);
-        *(uint4*)(bsh + row * BK + ch * 8) = breg[i];
-      }
-    };
+      for (int i = 0; i < TM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    load_a();
-    load_b(0);
-    store_ab(0);
+    __syncthreads();  // tap table ready / previous tile's epilogue done with LDS
+    gather_a_tile<A_CH, VEC, ESZ, BK, U8>(areg, rsrc, tab, p, rt, rh, rw, rowoff, 0, a_ccol, taps);
+    load_w_tile<B_CH, B_CPR, BK>(breg, p.w, n0, p.Kpad, 0, tid, b_ccol);
+    store_tiles<A_CH, B_CH, A_CPR, B_CPR, BM, BN, BK, U8>(areg, breg, As, Bs, 0, tid, a_ccol, b_ccol, p.in_scale);
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nk) {
-        advance_k();
-        load_a();
-        load_b(kt + 1);
-      }
+      // Always prefetch (the last iteration re-loads the last tile into the free buffer):
+      // keeping the staging path unconditional lets the compiler hold it in registers.
+      const int kn = min(kt + 1, nk - 1);
+      gather_a_tile<A_CH, VEC, ESZ, BK, U8>(areg, rsrc, tab, p, rt, rh, rw, rowoff, kn, a_ccol, taps);
+      load_w_tile<B_CH, B_CPR, BK>(breg, p.w, n0, p.Kpad, kn, tid, b_ccol);
       const bf16_t* a = As + buf * BM * BK;
       const bf16_t* bsh = Bs + buf * BN * BK;
 #pragma unroll
       for (int s = 0; s < KSTEPS; ++s) {
-        bf16x8 af[TM], bfr[TN];
+        bf16x8 xf[TM], wf[TN];
         const int chunk = s * 4 + (lane >> 4);
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
           const int row = wr * WM + i * 16 + (lane & 15);
-          af[i] = *(const bf16x8*)(a + row * BK + swz<BK>(row, chunk) * 8);
+          xf[i] = *(const bf16x8*)(a + row * BK + swz<BK>(row, chunk) * 8);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int row = wc * WN + j * 16 + (lane & 15);
-          bfr[j] = *(const bf16x8*)(bsh + row * BK + swz<BK>(row, chunk) * 8);
+          wf[j] = *(const bf16x8*)(bsh + row * BK + swz<BK>(row, chunk) * 8);
         }
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
       }
-      if (kt + 1 < nk) store_ab(buf ^ 1);
+      store_tiles<A_CH, B_CH, A_CPR, B_CPR, BM, BN, BK, U8>(areg, breg, As, Bs, buf ^ 1, tid, a_ccol, b_ccol,
+                                                            p.in_scale);
       __syncthreads();
     }
 
-    // ---- epilogue: BN partial stats + bf16 tile through LDS ----
-    if (p.stats != nullptr) {
+    // ---- epilogue: lane holds channels n = 4*(lane>>4)+r of output row m = lane&15 ----
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * WM + i * 16 + (lane & 15);
+      const bool rv = (m0 + row) < p.M;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        float s = 0.f, q = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
+        const f32x4 v = acc[j][i];
+        if (p.stats != nullptr && rv) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wr * WM + i * 16 + (lane >> 4) * 4 + r;
-            const float v = (m < p.M) ? acc[i][j][r] : 0.f;
-            s += v;
-            q += v * v;
+            st_s[j][r] += v[r];
+            st_q[j][r] += v[r] * v[r];
           }
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        q += __shfl_xor(q, 16, 64);
-        q += __shfl_xor(q, 32, 64);
-        st_s[j] += s;
-        st_q[j] += q;
+        }
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        const int col = wc * WN + j * 16 + (lane >> 4) * 4;
+        *(uint2*)(Es + row * LDE + col) = o;
       }
     }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = wr * WM + i * 16 + (lane >> 4) * 4 + r;
-          const int col = wc * WN + j * 16 + (lane & 15);
-          Es[row * (BN + EPAD) + col] = f2bf(acc[i][j][r]);
-        }
     __syncthreads();
     constexpr int OCPR = BN / 8;
 #pragma unroll
@@ -265,33 +288,50 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
       const int row = cid / OCPR, cc = cid % OCPR;
       const int m = m0 + row, n = n0 + cc * 8;
       if (m < p.M && n < p.Cout) {
-        *(uint4*)(p.y + (long long)m * p.ldy + n) = *(const uint4*)(Es + row * (BN + EPAD) + cc * 8);
+        *(uint4*)(p.y + (long long)m * p.ldy + n) = *(const uint4*)(Es + row * LDE + cc * 8);
       }
     }
-    __syncthreads();
   }
 
   if (p.stats != nullptr) {
-    // combine the two M-waves (wr = 0, 1) that own the same columns, then one store per column.
-    float* red = (float*)smem;  // [2 (wc)][2 (s,q)][WN]
-    if (wr == 1 && lane < 16) {
+    // reduce over the 16 lanes (output rows) that share a channel group, then over wr
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        red[(wc * 2 + 0) * WN + j * 16 + lane] = st_s[j];
-        red[(wc * 2 + 1) * WN + j * 16 + lane] = st_q[j];
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = st_s[j][r], q = st_q[j][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        st_s[j][r] = s;
+        st_q[j][r] = q;
       }
+    __syncthreads();
+    float* red = (float*)smem;  // [2 (wc)][2 (s,q)][WN]
+    if (wr == 1 && (lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + (lane >> 4) * 4 + r;
+          red[(wc * 2 + 0) * WN + c] = st_s[j][r];
+          red[(wc * 2 + 1) * WN + c] = st_q[j][r];
+        }
     }
     __syncthreads();
-    if (wr == 0 && lane < 16) {
+    if (wr == 0 && (lane & 15) == 0) {
+      const int npad = p.num_n_tiles * BN;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wc * WN + j * 16 + lane;
-        const float s = st_s[j] + red[(wc * 2 + 0) * WN + j * 16 + lane];
-        const float q = st_q[j] + red[(wc * 2 + 1) * WN + j * 16 + lane];
-        const int npad = p.num_n_tiles * BN;
-        p.stats[(long long)m_slot * 2 * npad + col] = s;
-        p.stats[(long long)m_slot * 2 * npad + npad + col] = q;
-      }
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wc * WN + c;
+          p.stats[(long long)m_slot * 2 * npad + col] = st_s[j][r] + red[(wc * 2 + 0) * WN + c];
+          p.stats[(long long)m_slot * 2 * npad + npad + col] = st_q[j][r] + red[(wc * 2 + 1) * WN + c];
+        }
     }
   }
 }
@@ -303,25 +343,102 @@ struct WgradParams {
   const void* x;       // [B, T, H, W, Cin]
   float* slab;         // [splits][Npad][Kpad]
   long long x_bstride;
+  long long x_total_bytes;
+  long long dy_total_bytes;
   int T, H, W, Cin;
   int To, Ho, Wo, Cout, ldd;
   int KT, KH, KW, st, sh, sw, pt, ph, pw;
   int Ktot, Kpad, Npad, M;
   int n_tiles, k_tiles, splits, rows_per_split;
   float in_scale;
-  FastDiv fWo, fHo, fTo;
+  FastDiv fWo, fHo, fTo, fCin;
 };
+
+constexpr int WG_R = 64;  // reduction rows (m) per LDS stage = two 32-deep MFMA k-steps
+
+// Stage this thread's chunks of dY rows [mb, mb+64) and of the im2col X rows.
+template <int DCH, int XCH, int DCPR, int XCPR, int VEC, int ESZ, bool U8, typename XReg>
+__device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH], __amdgpu_buffer_rsrc_t drs,
+                                           __amdgpu_buffer_rsrc_t xrs, const WgradParams& p, int mb, int m_end,
+                                           int tid, int n0, int d_ccol, bool kval, int dt, int dh, int dw, int c) {
+#pragma unroll
+  for (int i = 0; i < DCH; ++i) {
+    const int row = (tid + i * 256) / DCPR;
+    const int m = mb + row;
+    const int n = n0 + d_ccol * 8;
+    const bool v = (m < m_end) & (n < p.Cout);
+    const uint32_t off = v ? (uint32_t)(((long long)m * p.ldd + n) * 2) : 0x80000000u;
+    dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+  }
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int row = (tid + i * 256) / XCPR;
+    const int m = mb + row;
+    const uint32_t q = fdiv((uint32_t)m, p.fWo);
+    const int wo = m - q * p.Wo;
+    const uint32_t q2 = fdiv(q, p.fHo);
+    const int ho = q - q2 * p.Ho;
+    const uint32_t b = fdiv(q2, p.fTo);
+    const int to = q2 - b * p.To;
+    const int ti = to * p.st - p.pt + dt, hi = ho * p.sh - p.ph + dh, wi = wo * p.sw - p.pw + dw;
+    const bool v = kval & (m < m_end) & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+                   ((unsigned)wi < (unsigned)p.W);
+    const long long e = (long long)b * p.x_bstride + ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c;
+    const uint32_t off = v ? (uint32_t)(e * ESZ) : 0x80000000u;
+    if constexpr (U8) {
+      xreg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0);
+    } else {
+      xreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  }
+}
+
+template <int DCH, int XCH, int DCPR, int XCPR, int LDN, int LDK, bool U8, typename XReg>
+__device__ __forceinline__ void wgrad_store(const uint4 (&dreg)[DCH], const XReg (&xreg)[XCH], bf16_t* d, bf16_t* x,
+                                            int tid, int d_ccol, int x_ccol, float in_scale) {
+#pragma unroll
+  for (int i = 0; i < DCH; ++i) {
+    const int row = (tid + i * 256) / DCPR;
+    *(uint4*)(d + row * LDN + d_ccol * 8) = dreg[i];
+  }
+#pragma unroll
+  for (int i = 0; i < XCH; ++i) {
+    const int row = (tid + i * 256) / XCPR;
+    if constexpr (U8) {
+      const uint32_t v = xreg[i];
+      uint2 o;
+      o.x = pack2bf((float)(v & 0xff) * in_scale, (float)((v >> 8) & 0xff) * in_scale);
+      o.y = pack2bf((float)((v >> 16) & 0xff) * in_scale, (float)(v >> 24) * in_scale);
+      *(uint2*)(x + row * LDK + x_ccol * 4) = o;
+    } else {
+      *(uint4*)(x + row * LDK + x_ccol * 8) = xreg[i];
+    }
+  }
+}
+
+// MFMA fragment of 8 reduction rows of column block [col, col+16) of a row-major LDS image:
+// ds_read_b64_tr_b16 gives lane (16g + i) rows {4g..4g+3} then {16+4g..} of column col + i.
+// The same k permutation is used for both operands, so the dot products are unchanged.
+__device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int ld, int k0, int col, int g, int q, int pp) {
+  const bf16_t* a0 = img + (k0 + 4 * g + q) * ld + col + pp * 4;
+  const bf16_t* a1 = img + (k0 + 16 + 4 * g + q) * ld + col + pp * 4;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 template <int TN_, int TK_, bool U8>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
-  constexpr int R = 32;                     // reduction rows per step (one MFMA K)
+  constexpr int R = WG_R;
   constexpr int VEC = U8 ? 4 : 8;
-  constexpr int LDN = TN_ + 16, LDK = TK_ + 16;  // padded row lengths (elements)
-  constexpr int D_CPR = TN_ / 8, X_CPR = TK_ / VEC;
-  constexpr int D_CH = R * D_CPR / 256, X_CH = R * X_CPR / 256;
+  constexpr int ESZ = U8 ? 1 : 2;
+  constexpr int LDN = TN_ + 16, LDK = TK_ + 16;  // padded rows: conflict-free transposed reads
+  constexpr int DCPR = TN_ / 8, XCPR = TK_ / VEC;
+  constexpr int DCH = R * DCPR / 256, XCH = R * XCPR / 256;
   constexpr int WN = TN_ / 2, WK = TK_ / 2;
   constexpr int TI = WN / 16, TJ = WK / 16;
-  static_assert(D_CH >= 1 && X_CH >= 1, "tile too small");
+  static_assert(DCH >= 1 && XCH >= 1, "tile too small");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ds = (bf16_t*)smem;               // [2][R][LDN]
@@ -339,78 +456,24 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const int m_end = min(p.M, m_begin + p.rows_per_split);
 
   // fixed (tap, c) of this thread's X chunk column
-  const int x_ccol = tid % X_CPR;
+  const int x_ccol = tid % XCPR;
   const int kk = k0 + x_ccol * VEC;
-  int tap = kk / p.Cin;
+  const int tap = (int)fdiv((uint32_t)kk, p.fCin);
   const int c = kk - tap * p.Cin;
   const bool kval = kk < p.Ktot;
   const int dw = tap % p.KW;
   const int dh = (tap / p.KW) % p.KH;
   const int dt = tap / (p.KW * p.KH);
-  const int d_ccol = tid % D_CPR;
-  const uint8_t* xb = (const uint8_t*)p.x;
-  const int esize = U8 ? 1 : 2;
+  const int d_ccol = tid % DCPR;
+
+  const uint32_t dnrec = p.dy_total_bytes > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)p.dy_total_bytes;
+  const uint32_t xnrec = p.x_total_bytes > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)p.x_total_bytes;
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)dnrec, 0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)xnrec, 0x00020000);
 
   using XReg = typename std::conditional<U8, uint32_t, uint4>::type;
-  uint4 dreg[D_CH];
-  XReg xreg[X_CH];
-
-  auto load = [&](int mb) {
-#pragma unroll
-    for (int i = 0; i < D_CH; ++i) {
-      const int row = (tid + i * 256) / D_CPR;
-      const int m = mb + row;
-      const int n = n0 + d_ccol * 8;
-      dreg[i] = make_uint4(0, 0, 0, 0);
-      if (m < m_end && n < p.Cout) dreg[i] = *(const uint4*)(p.dy + (long long)m * p.ldd + n);
-    }
-#pragma unroll
-    for (int i = 0; i < X_CH; ++i) {
-      const int row = (tid + i * 256) / X_CPR;
-      const int m = mb + row;
-      bool v = kval && m < m_end;
-      long long off = 0;
-      if (v) {
-        uint32_t q = fdiv((uint32_t)m, p.fWo);
-        const int wo = m - q * p.Wo;
-        uint32_t q2 = fdiv(q, p.fHo);
-        const int ho = q - q2 * p.Ho;
-        uint32_t b = fdiv(q2, p.fTo);
-        const int to = q2 - b * p.To;
-        const int ti = to * p.st - p.pt + dt, hi = ho * p.sh - p.ph + dh, wi = wo * p.sw - p.pw + dw;
-        v = (unsigned)ti < (unsigned)p.T && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
-        off = (long long)b * p.x_bstride + ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c;
-      }
-      if constexpr (U8) {
-        xreg[i] = v ? *(const uint32_t*)(xb + off) : 0u;
-      } else {
-        xreg[i] = v ? *(const uint4*)(xb + off * 2) : make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto store = [&](int buf) {
-    bf16_t* d = Ds + buf * R * LDN;
-#pragma unroll
-    for (int i = 0; i < D_CH; ++i) {
-      const int row = (tid + i * 256) / D_CPR;
-      *(uint4*)(d + row * LDN + d_ccol * 8) = dreg[i];
-    }
-    bf16_t* x = Xs + buf * R * LDK;
-#pragma unroll
-    for (int i = 0; i < X_CH; ++i) {
-      const int row = (tid + i * 256) / X_CPR;
-      if constexpr (U8) {
-        const uint32_t v = xreg[i];
-        const float s = p.in_scale;
-        uint2 o;
-        o.x = pack2bf((float)(v & 0xff) * s, (float)((v >> 8) & 0xff) * s);
-        o.y = pack2bf((float)((v >> 16) & 0xff) * s, (float)(v >> 24) * s);
-        *(uint2*)(x + row * LDK + x_ccol * 4) = o;
-      } else {
-        *(uint4*)(x + row * LDK + x_ccol * 8) = xreg[i];
-      }
-    }
-  };
+  uint4 dreg[DCH];
+  XReg xreg[XCH];
 
   f32x4 acc[TI][TJ];
 #pragma unroll
@@ -418,46 +481,36 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 #pragma unroll
     for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // transposed-read lane geometry: group g = lane>>4 reads rows 4g+q (+16), cols 4p..4p+3
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int nsteps = (m_end - m_begin + R - 1) / R;
   if (nsteps > 0) {
-    load(m_begin);
-    store(0);
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin, m_end, tid, n0, d_ccol, kval,
+                                                    dt, dh, dw, c);
+    wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
-    if (s + 1 < nsteps) load(m_begin + (s + 1) * R);
+    const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin + sn * R, m_end, tid, n0, d_ccol,
+                                                    kval, dt, dh, dw, c);
     const bf16_t* d = Ds + buf * R * LDN;
     const bf16_t* x = Xs + buf * R * LDK;
-    bf16x8 af[TI], bfr[TJ];
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int col = wr * WN + i * 16 + pp * 4;
-      const bf16_t* a0 = d + (4 * g + q) * LDN + col;
-      const bf16_t* a1 = d + (16 + 4 * g + q) * LDN + col;
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
-      s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      af[i] = __builtin_bit_cast(bf16x8, v);
+    for (int ks = 0; ks < R / 32; ++ks) {
+      bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = tr_frag(d, LDN, ks * 32, wr * WN + i * 16, g, q, pp);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = tr_frag(x, LDK, ks * 32, wc * WK + j * 16, g, q, pp);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int col = wc * WK + j * 16 + pp * 4;
-      const bf16_t* b0 = x + (4 * g + q) * LDK + col;
-      const bf16_t* b1 = x + (16 + 4 * g + q) * LDK + col;
-      s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)b0);
-      s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)b1);
-      s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      bfr[j] = __builtin_bit_cast(bf16x8, v);
-    }
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-#pragma unroll
-      for (int j = 0; j < TJ; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    if (s + 1 < nsteps) store(buf ^ 1);
+    wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds + (buf ^ 1) * R * LDN, Xs + (buf ^ 1) * R * LDK,
+                                                     tid, d_ccol, x_ccol, p.in_scale);
     __syncthreads();
   }
   // C[i = n][j = k]: row (n) = 4*(lane>>4) + r, col (k) = lane & 15
@@ -474,21 +527,28 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
       }
 }
 
-// Sum the split slabs and unpack [n][tap][c] -> PyTorch weight layout [n][c_param][tap].
+// Sum the split slabs (coalesced along k) and scatter to the PyTorch weight layout
+// [n][c_param][tap].
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw, int splits,
                                     int Npad, int Kpad, int Cout, int Cin, int Cin_param, int taps,
                                     int accumulate) {
-  const long long total = (long long)Cout * Cin_param * taps;
+  const int Ktot = taps * Cin;
+  const long long total = (long long)Cout * Ktot;
+  const long long plane = (long long)Npad * Kpad;
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
-    const int tap = idx % taps;
-    const long long t2 = idx / taps;
-    const int c = t2 % Cin_param;
-    const int n = t2 / Cin_param;
-    const long long k = (long long)tap * Cin + c;
+    const int n = (int)(idx / Ktot);
+    const int k = (int)(idx - (long long)n * Ktot);
+    const int tap = k / Cin, c = k - tap * Cin;
+    if (c >= Cin_param) continue;
+    const float* sp = slab + (long long)n * Kpad + k;
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += slab[((long long)sp * Npad + n) * Kpad + k];
-    dw[idx] = accumulate ? dw[idx] + s : s;
+    int sp_i = 0;
+    for (; sp_i + 4 <= splits; sp_i += 4)
+      s += sp[sp_i * plane] + sp[(sp_i + 1) * plane] + sp[(sp_i + 2) * plane] + sp[(sp_i + 3) * plane];
+    for (; sp_i < splits; ++sp_i) s += sp[sp_i * plane];
+    const long long o = ((long long)n * Cin_param + c) * taps + tap;
+    dw[o] = accumulate ? dw[o] + s : s;
   }
 }
 
@@ -524,8 +584,8 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, bf16_t* __restri
 template <int BM, int BN, int BK, bool U8>
 static int launch_fwd(ConvParams& p, hipStream_t stream) {
   const size_t kloop = (size_t)2 * (BM + BN) * BK * 2;
-  const size_t epi = (size_t)BM * (BN + 16) * 2;
-  const size_t lds = kloop > epi ? kloop : epi;
+  const size_t epi = (size_t)BM * (BN + 8) * 2;
+  const size_t lds = (kloop > epi ? kloop : epi) + 8 * (size_t)(p.KT * p.KH * p.KW);
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, BK, U8>,
@@ -561,6 +621,8 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.grid_m = grid_m;
   p.in_scale = x_u8 ? (1.0f / 255.0f) : 1.0f;
   p.fWo = make_fastdiv(p.Wo); p.fHo = make_fastdiv(p.Ho); p.fTo = make_fastdiv(p.To);
+  p.fCin = make_fastdiv(Cin);
+  p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
   if (x_u8) {
     if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, true>(p, stream);
     if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, true>(p, stream);
@@ -577,7 +639,13 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 
 template <int TN_, int TK_, bool U8>
 static int launch_wgrad(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)2 * 32 * ((TN_ + 16) + (TK_ + 16)) * 2;
+  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_kernel<TN_, TK_, U8>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
   const int nblocks = p.n_tiles * p.k_tiles * p.splits;
   hipLaunchKernelGGL((conv_wgrad_kernel<TN_, TK_, U8>), dim3(nblocks), dim3(256), lds, stream, p);
   return (int)hipGetLastError();
@@ -602,9 +670,14 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
   p.n_tiles = Npad / tn;
   p.k_tiles = Kpad / tk;
   p.splits = splits;
-  p.rows_per_split = ((p.M + splits - 1) / splits + 31) / 32 * 32;
+  p.rows_per_split = ((p.M + splits - 1) / splits + WG_R - 1) / WG_R * WG_R;
   p.in_scale = x_u8 ? (1.0f / 255.0f) : 1.0f;
   p.fWo = make_fastdiv(p.Wo); p.fHo = make_fastdiv(p.Ho); p.fTo = make_fastdiv(p.To);
+  p.fCin = make_fastdiv(Cin);
+  p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
+  p.dy_total_bytes = (long long)p.M * ldd * 2;
+  // 32-bit buffer offsets (out-of-range = zero fill) address both operands from their base
+  if (p.x_total_bytes > 0x7FFFFFF0LL || p.dy_total_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
   int rc;
   if (x_u8) {
     if (tn == 64 && tk == 64) rc = launch_wgrad<64, 64, true>(p, stream);
@@ -619,7 +692,7 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
   }
   if (rc) return rc;
   const int taps = KT * KH * KW;
-  const long long total = (long long)Cout * Cin_param * taps;
+  const long long total = (long long)Cout * taps * Cin;
   const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, slab, dw, splits, Npad, Kpad,
                      Cout, Cin, Cin_param, taps, accumulate);

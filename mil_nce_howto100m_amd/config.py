@@ -96,6 +96,8 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--ckpt_every_steps", type=int, default=0, help="extra mid-epoch checkpoint interval")
     g.add_argument("--eval_csv", type=str, default="", help="eval CSV (csv/hmdb51.csv, msrvtt_test.csv, ...)")
     g.add_argument("--synthetic_eval_videos", type=int, default=96, help="videos in the synthetic eval set")
+    g.add_argument("--stop_epoch", type=int, default=0,
+                   help="end this run after this epoch (simulated interruption for resume tests)")
     g.add_argument("--hip_graph", type=int, default=0, help="capture the train step in a HIP graph")
     return p
 

@@ -34,9 +34,12 @@ def _bmm_t(x, y):
 
 
 def dist_matrix(x: torch.Tensor, y: torch.Tensor, kind: Optional[str]) -> torch.Tensor:
-    """x [..., n, d], y [..., m, d] -> [..., n, m] (fp32)."""
-    x = x.float()
-    y = y.float()
+    """x [..., n, d], y [..., m, d] -> [..., n, m] (fp32, or fp64 for fp64 inputs)."""
+    if x.dtype != torch.float64:
+        x = x.float()
+        y = y.float()
+    else:
+        y = y.double()
     if kind == "negative_dot":
         return -_bmm_t(x, y)
     if kind in ("cosine", "negative_cosine"):
@@ -136,7 +139,7 @@ class _SoftDTWHIP(torch.autograd.Function):
     @staticmethod
     def forward(ctx, D, gamma, bandwidth, pairs_b):
         from ._lib import call, ptr, stream
-        D = D.float().contiguous()
+        D = D.float().contiguous()  # the kernel reads fp32 distances (R / E are fp64 inside)
         if pairs_b:
             b = pairs_b
             n, m = D.shape[0] // b, D.shape[1] // b

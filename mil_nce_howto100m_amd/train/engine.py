@@ -185,4 +185,6 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
         if ctx.is_main:
             ckpt.save_checkpoint(trainer.state(epoch + 1), cdir, epoch + 1)
         pdist.barrier()
+        if getattr(args, "stop_epoch", 0) and epoch + 1 >= args.stop_epoch:
+            break
     return last

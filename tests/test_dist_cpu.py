@@ -1,0 +1,148 @@
+"""Distributed semantics on CPU/gloo with real multi-process rendezvous (127.0.0.1).
+
+* the embedding all-gather: rank-major order, local-slice backward (utils.py:8-24);
+* the reference gradient scale: world_size=2 DP gradient == full-batch gradient / 2
+  (SURVEY.md §2.10 item 2), and ``--grad_scale exact`` gives the full-batch gradient;
+* bucketed all-reduce + BN buffer broadcast keep replicas identical after steps;
+* checkpoint save on rank 0 + resume on both ranks reproduces the uninterrupted run.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _put(outdir, rank, obj):
+    torch.save(obj, os.path.join(outdir, f"rank{rank}.pt"))
+
+
+def _collect(outdir, world):
+    return [torch.load(os.path.join(outdir, f"rank{r}.pt"), weights_only=False) for r in range(world)]
+
+
+def _init(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    return pdist.init_distributed("gloo", "cpu")
+
+
+def _args(extra=()):
+    from mil_nce_howto100m_amd.config import get_args
+    return get_args(argv=["--batch_size", "4", "--num_frames", "4", "--video_size", "32", "--num_candidates", "2",
+                          "--blocks", "mixed_3b", "--warmup_steps", "1", "--word2vec_path", "", "--vocab_size", "500",
+                          "--lr", "1e-3", *extra])
+
+
+def _worker_gather(rank, world, port, outdir):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.dist import all_gather_embeddings
+    v = torch.full((2, 3), float(rank), requires_grad=True)
+    t = torch.full((4, 3), 10.0 + rank, requires_grad=True)
+    gv, gt = all_gather_embeddings(v, t, ctx)
+    (gv.sum() * 2 + gt.sum() * 3).backward()
+    _put(outdir, rank, (rank, gv.detach(), gt.detach(), v.grad, t.grad))
+    dist.destroy_process_group()
+
+
+def test_allgather_semantics():
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_gather, args=(world, port, out), nprocs=world)
+        res = _collect(out, world)
+    for rank, gv, gt, vg, tg in res:
+        assert torch.equal(gv[:, 0], torch.tensor([0.0, 0.0, 1.0, 1.0]))
+        assert torch.equal(gt[:, 0], torch.tensor([10.0] * 4 + [11.0] * 4))
+        assert torch.equal(vg, torch.full((2, 3), 2.0))  # local slice only, no reduction
+        assert torch.equal(tg, torch.full((4, 3), 3.0))
+
+
+def _worker_grad(rank, world, port, outdir, mode):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+    args = _args(["--grad_scale", mode])
+    seed_everything(1, rank)
+    model = build_model(args, ctx.device)
+    tr = Trainer(args, model, ctx, 10)
+    data = SyntheticClips(2, 4, 32, 2, 20, 500, device=ctx.device, rank=rank, world_size=world)
+    tr.model.eval()  # BN on running stats: per-rank forward == its slice of the full-batch forward
+    tr.bucketer.zero()
+    tr.buffers()
+    loss = tr.forward_loss(data.batch(0))
+    loss.backward()
+    tr.bucketer.finish()
+    _put(outdir, rank, (rank, tr.bucketer.flat * tr.optimizer.grad_scale, float(loss)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,ratio", [("reference", 0.5), ("exact", 1.0)])
+def test_dp_gradient_scale(mode, ratio):
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_grad, args=(world, port, out, mode), nprocs=world)
+        res = _collect(out, world)
+    g0, g1 = res[0][1], res[1][1]
+    assert torch.allclose(g0, g1, atol=1e-6)
+    # single process, full global batch (both ranks' samples, rank-major)
+    ctx = pdist.DistContext()
+    pdist.set_context(ctx)
+    args = _args()
+    seed_everything(1, 0)
+    model = build_model(args, ctx.device)
+    tr = Trainer(args, model, ctx, 10)
+    d0 = SyntheticClips(2, 4, 32, 2, 20, 500, rank=0, world_size=2).batch(0)
+    d1 = SyntheticClips(2, 4, 32, 2, 20, 500, rank=1, world_size=2).batch(0)
+    batch = {k: torch.cat([d0[k], d1[k]]) for k in ("video", "text")}
+    tr.model.eval()
+    tr.bucketer.zero()
+    loss = tr.forward_loss(batch)
+    loss.backward()
+    full = tr.bucketer.flat
+    assert abs(float(loss) - res[0][2]) < 1e-4
+    assert torch.allclose(g0, full * ratio, rtol=1e-3, atol=1e-7)
+
+
+def _worker_train(rank, world, port, ckdir, stop, resume):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.train.engine import run_training
+    args = _args(["--checkpoint_root", ckdir, "--checkpoint_dir", "run", "--epochs", "2", "--stop_epoch", str(stop),
+                  "--steps_per_epoch", "2", "--n_display", "1", "--verbose", "0", "--log_root", ckdir]
+                 + (["--resume"] if resume else []))
+    args.rank, args.world_size = ctx.rank, ctx.world_size
+    run_training(args, ctx)
+    dist.destroy_process_group()
+
+
+def test_checkpoint_resume_equivalence():
+    from mil_nce_howto100m_amd.train import checkpoint as ck
+    world = 2
+    with tempfile.TemporaryDirectory() as d1, tempfile.TemporaryDirectory() as d2:
+        mp.spawn(_worker_train, args=(world, _port(), d1, 2, False), nprocs=world)  # 2 epochs straight
+        mp.spawn(_worker_train, args=(world, _port(), d2, 1, False), nprocs=world)  # 1 epoch
+        mp.spawn(_worker_train, args=(world, _port(), d2, 2, True), nprocs=world)   # resume -> 2
+        a = ck.load_checkpoint(os.path.join(d1, "run", "epoch0002.pth.tar"))
+        b = ck.load_checkpoint(os.path.join(d2, "run", "epoch0002.pth.tar"))
+        assert a["epoch"] == b["epoch"] == 2
+        assert a["scheduler"]["last_epoch"] == b["scheduler"]["last_epoch"] == 4
+        for k in a["state_dict"]:
+            assert torch.allclose(a["state_dict"][k].float(), b["state_dict"][k].float(), atol=1e-6), k
+        sa, sb = a["optimizer"]["state"], b["optimizer"]["state"]
+        assert sa.keys() == sb.keys()
+        for k in sa:
+            assert torch.allclose(sa[k]["exp_avg"], sb[k]["exp_avg"], atol=1e-7)

@@ -22,16 +22,22 @@ def test_model_forward_backward_matches_aten():
     rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()
     assert rel(ve, ver) < 0.08
     assert rel(te, ter) < 0.02
-    loss = ops_mod.milnce_loss(ve, te)
-    lossr = aten.milnce_loss(ver, ter)
-    loss.backward()
-    lossr.backward()
+    # Identical upstream gradients (a fixed random linear functional of the embeddings): the
+    # MIL-NCE softmax would amplify the bf16 forward differences into the comparison.
+    gv = torch.randn(ve.shape, dtype=torch.float64)
+    gt = torch.randn(te.shape, dtype=torch.float64)
+    ((ve.double() * gv.cuda()).sum() + (te.double() * gt.cuda()).sum()).backward()
+    ((ver * gv).sum() + (ter * gt).sum()).backward()
+    errs = []
     for (n1, p1), (n2, p2) in zip(m.named_parameters(), ref.named_parameters()):
         if p2.grad is None:
             continue
         assert p1.grad is not None, n1
-        e = rel(p1.grad, p2.grad)
-        assert e < 0.25, (n1, e)
+        errs.append((n1, rel(p1.grad, p2.grad), p2.grad.norm().item()))
+    for n, e, g in errs:
+        print(f"{n:45s} rel_err={e:.4f} |g|={g:.3e}")
+    bad = [(n, e) for n, e, g in errs if e > 0.12]
+    assert not bad, bad
 
 
 def test_bench_step_runs():

@@ -1,0 +1,7 @@
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests/test_gpu_ops.py tests/test_gpu_model.py -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || true
+tail -8 gpurun_out/pytest_gpu.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_bs256 -o run --output-format csv -- python bench.py --steps 3 --warmup 2 --batch_per_gpu 256 > gpurun_out/prof_bench.log 2>&1 || { tail -20 gpurun_out/prof_bench.log; exit 1; }
+ls -R gpurun_out/prof_bs256 | head -20
