@@ -179,7 +179,8 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 }
 
 // coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int C,
+// part rows have stride 2*ps (ps = C for bn_bwd_reduce partials, Npad for conv-epilogue partials).
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps, int C,
                                                               double count, const float* __restrict__ gamma,
                                                               const float* __restrict__ ss, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta, float* __restrict__ coef) {
@@ -189,8 +190,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   double s1 = 0.0, s2 = 0.0;
   if (c < C) {
     for (int i = rg; i < nparts; i += 8) {
-      s1 += part[(long long)i * 2 * C + c];
-      s2 += part[(long long)i * 2 * C + C + c];
+      s1 += part[(long long)i * 2 * ps + c];
+      s2 += part[(long long)i * 2 * ps + ps + c];
     }
   }
   red[0][rg][cl] = s1;
@@ -253,15 +254,20 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
   return (int)hipGetLastError();
 }
 
-// part must hold nblocks*2*C floats; nblocks = ceil(M / rows_per_block) (queried with part == null).
+// part holds nparts rows of [2][ps] partial sums. have_part = 1: they were produced by the kernel
+// that computed dz (conv dgrad epilogue, gate / pool backward), ps = that kernel's stride;
+// have_part = 0: reduce them here (ps = C).
 MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
-                             const float* gamma, float* part, int nparts, float* dgamma, float* dbeta,
-                             float* coef, void* dy, hipStream_t stream) {
+                             const float* gamma, float* part, int nparts, int ps, int have_part, float* dgamma,
+                             float* dbeta, float* coef, void* dy, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  const int rows_per_block = (int)((M + nparts - 1) / nparts);
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
-                     (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, C,
+  if (!have_part) {
+    const int rows_per_block = (int)((M + nparts - 1) / nparts);
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(nparts), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
+                       (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
+    ps = C;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, ps, C,
                      (double)M, gamma, ss, dgamma, dbeta, coef);
   const long long nchunks = M * (C / 8);
   long long grid = (nchunks + 255) / 256;

@@ -33,6 +33,13 @@ struct ConvParams {
   float in_scale;
   long long x_total_bytes;
   FastDiv fWo, fHo, fTo, fCin;
+  // epilogue statistics: 0 none; 1 BN forward sums of this conv's output (stats);
+  // 2 BN backward partials of the PRODUCER of this dgrad's output: the output is that
+  //   layer's dz, bn_y/bn_ss its raw conv output and [mean, invstd, scale, shift];
+  //   stats += (dz*mask, dz*mask*xhat) with mask = y*scale + shift > 0.
+  int bn_mode;
+  const bf16_t* bn_y;
+  const float* bn_ss;
 };
 
 template <int BK>
@@ -147,6 +154,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   bf16_t* Bs = As + 2 * BM * BK;       // [2][BN][BK]   weights     (MFMA A operand)
   bf16_t* Es = (bf16_t*)smem;          // epilogue [BM][LDE]
   int2* tab = (int2*)(smem + TAB_OFF_BYTES);
+  float* ssl = (float*)(smem + TAB_OFF_BYTES + 8 * 160);  // [4][BN] producer-BN constants (mode 2)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -166,6 +174,14 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   const uint32_t clip_bytes = (uint32_t)(p.x_bstride * ESZ);
 
   build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
+  if (p.bn_mode == 2) {
+    for (int t = tid; t < 4 * BN; t += 256) {
+      const int q = t / BN, c = n0 + (t - q * BN);
+      ssl[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
+    }
+  }
+  const uint32_t bny_rec = (uint32_t)((long long)p.M * p.Cout * 2 > 0x7FFFFFF0LL ? 0x7FFFFFF0LL : (long long)p.M * p.Cout * 2);
+  const auto bny_rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.bn_y, (short)0, (int)bny_rec, 0x00020000);
 
   float st_s[TN][4], st_q[TN][4];
 #pragma unroll
@@ -266,11 +282,27 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const f32x4 v = acc[j][i];
-        if (p.stats != nullptr && rv) {
+        if (p.bn_mode == 1 && rv) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             st_s[j][r] += v[r];
             st_q[j][r] += v[r] * v[r];
+          }
+        } else if (p.bn_mode == 2) {
+          const int cl = wc * WN + j * 16 + (lane >> 4) * 4;  // local channel of element r = 0
+          const uint32_t off = rv ? (uint32_t)(((long long)(m0 + row) * p.Cout + n0 + cl) * 2) : 0x80000000u;
+          const auto yv2 = __builtin_amdgcn_raw_buffer_load_b64(bny_rs, off, 0, 0);
+          const uint2 yv = __builtin_bit_cast(uint2, yv2);
+          const float yf[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
+                               __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float mean = ssl[cl + r], istd = ssl[BN + cl + r], sc = ssl[2 * BN + cl + r],
+                        sh = ssl[3 * BN + cl + r];
+            const float gm = (yf[r] * sc + sh > 0.f) ? v[r] : 0.f;  // out-of-range rows: y = 0 -> sc*0+sh
+            const float gmv = rv ? gm : 0.f;
+            st_s[j][r] += gmv;
+            st_q[j][r] += gmv * (yf[r] - mean) * istd;
           }
         }
         uint2 o;
@@ -293,7 +325,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
     }
   }
 
-  if (p.stats != nullptr) {
+  if (p.bn_mode != 0) {
     // reduce over the 16 lanes (output rows) that share a channel group, then over wr
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -360,14 +392,15 @@ constexpr int WG_R = 64;  // reduction rows (m) per LDS stage = two 32-deep MFMA
 template <int DCH, int XCH, int DCPR, int XCPR, int VEC, int ESZ, bool U8, typename XReg>
 __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH], __amdgpu_buffer_rsrc_t drs,
                                            __amdgpu_buffer_rsrc_t xrs, const WgradParams& p, int mb, int m_end,
-                                           int tid, int n0, int d_ccol, bool kval, int dt, int dh, int dw, int c) {
+                                           int m_base, uint32_t b_first, int tid, int n0, int d_ccol, bool kval,
+                                           int dt, int dh, int dw, int c) {
 #pragma unroll
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
     const int m = mb + row;
     const int n = n0 + d_ccol * 8;
     const bool v = (m < m_end) & (n < p.Cout);
-    const uint32_t off = v ? (uint32_t)(((long long)m * p.ldd + n) * 2) : 0x80000000u;
+    const uint32_t off = v ? (uint32_t)(((long long)(m - m_base) * p.ldd + n) * 2) : 0x80000000u;
     dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
   }
 #pragma unroll
@@ -383,7 +416,7 @@ __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH]
     const int ti = to * p.st - p.pt + dt, hi = ho * p.sh - p.ph + dh, wi = wo * p.sw - p.pw + dw;
     const bool v = kval & (m < m_end) & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                    ((unsigned)wi < (unsigned)p.W);
-    const long long e = (long long)b * p.x_bstride + ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c;
+    const long long e = (long long)(b - b_first) * p.x_bstride + ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c;
     const uint32_t off = v ? (uint32_t)(e * ESZ) : 0x80000000u;
     if constexpr (U8) {
       xreg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0);
@@ -466,10 +499,20 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const int dt = tap / (p.KW * p.KH);
   const int d_ccol = tid % DCPR;
 
-  const uint32_t dnrec = p.dy_total_bytes > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)p.dy_total_bytes;
-  const uint32_t xnrec = p.x_total_bytes > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)p.x_total_bytes;
-  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, (int)dnrec, 0x00020000);
-  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)xnrec, 0x00020000);
+  // Descriptors based at this split's first row / first clip: offsets stay 32-bit whatever the
+  // tensor size, and rows past m_end fall outside the dY record range (read as zero).
+  const int m_clamped = m_begin < m_end ? m_begin : 0;
+  const long long dbase = (long long)m_clamped * p.ldd * 2;
+  const long long dbytes = m_end > m_begin ? (long long)(m_end - m_begin) * p.ldd * 2 : 0;
+  const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
+  const uint32_t b_first = (uint32_t)m_clamped / thw;
+  const long long xbase = (long long)b_first * p.x_bstride * ESZ;
+  const long long xrem = p.x_total_bytes - xbase;
+  const uint32_t xnrec = xrem > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)xrem;
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.dy + dbase), (short)0,
+                                                     (int)(dbytes > 0x7FFFFFF0LL ? 0x7FFFFFF0LL : dbytes), 0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + xbase), (short)0, (int)xnrec,
+                                                     0x00020000);
 
   using XReg = typename std::conditional<U8, uint32_t, uint4>::type;
   uint4 dreg[DCH];
@@ -484,16 +527,16 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int nsteps = (m_end - m_begin + R - 1) / R;
   if (nsteps > 0) {
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin, m_end, tid, n0, d_ccol, kval,
-                                                    dt, dh, dw, c);
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin, m_end, m_clamped, b_first, tid,
+                                                    n0, d_ccol, kval, dt, dh, dw, c);
     wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
     const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin + sn * R, m_end, tid, n0, d_ccol,
-                                                    kval, dt, dh, dw, c);
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin + sn * R, m_end, m_clamped,
+                                                    b_first, tid, n0, d_ccol, kval, dt, dh, dw, c);
     const bf16_t* d = Ds + buf * R * LDN;
     const bf16_t* x = Xs + buf * R * LDK;
 #pragma unroll
@@ -585,7 +628,7 @@ template <int BM, int BN, int BK, bool U8>
 static int launch_fwd(ConvParams& p, hipStream_t stream) {
   const size_t kloop = (size_t)2 * (BM + BN) * BK * 2;
   const size_t epi = (size_t)BM * (BN + 8) * 2;
-  const size_t lds = (kloop > epi ? kloop : epi) + 8 * (size_t)(p.KT * p.KH * p.KW);
+  const size_t lds = (kloop > epi ? kloop : epi) + 8 * 160 + 16 * BN;  // + tap table + producer-BN consts
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, BK, U8>,
@@ -599,13 +642,17 @@ static int launch_fwd(ConvParams& p, hipStream_t stream) {
 
 // x: input, w: packed weight [Npad][Kpad], y: out [M][ldy], stats: [grid_m][2][Npad] or null.
 // Returns grid_m through *grid_m_out (for sizing the stats buffer, call with y == nullptr).
-MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats,
+MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
+                               const float* bn_ss,
                                int B, int T, int H, int W, int Cin, int Cout,
                                int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
                                int Kpad, int Npad, int ldy, int bn, int bk, int grid_m,
                                hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
+  p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss;
+  if (KT * KH * KW > 160) return (int)hipErrorInvalidValue;  // tap table capacity
+  p.bn_mode = stats == nullptr ? 0 : (bn_y == nullptr ? 1 : 2);
   p.T = T; p.H = H; p.W = W; p.Cin = Cin;
   p.To = (T + 2 * pt - KT) / st + 1;
   p.Ho = (H + 2 * ph - KH) / sh + 1;
@@ -676,8 +723,8 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
   p.fCin = make_fastdiv(Cin);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
   p.dy_total_bytes = (long long)p.M * ldd * 2;
-  // 32-bit buffer offsets (out-of-range = zero fill) address both operands from their base
-  if (p.x_total_bytes > 0x7FFFFFF0LL || p.dy_total_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
+  // per-split descriptor bases keep offsets 32-bit; one split's rows must fit in 2 GB
+  if ((long long)p.rows_per_split * ldd * 2 > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
   int rc;
   if (x_u8) {
     if (tn == 64 && tk == 64) rc = launch_wgrad<64, 64, true>(p, stream);

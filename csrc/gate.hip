@@ -5,9 +5,9 @@
 //           epilogue (bn.hip); gate_fc turns them into g = sigmoid(W * mean + b) (one block
 //           per clip and branch), gate_scale writes z_i * g_i straight into its channel slice of
 //           the concatenated block output (no separate th.cat pass).
-// backward: gate_bwd_reduce  dg[b, c] = sum_thw dout * z      (all branches, one launch)
-//           gate_bwd_small   dpre = dg*g*(1-g); dmean = dpre W; dW = dpre^T mean; db = sum_b dpre
-//           gate_bwd_apply   dz_i = dout_i * g_i + dmean_i / THW   (all branches, one launch)
+// backward: gate_bwd_reduce  dpre[b, c] = (sum_thw dout * z) * g * (1 - g)   (all branches)
+//           [hipBLASLt]      dmean = dpre W; dW = dpre^T mean; db = sum_b dpre (tiny GEMMs)
+//           gate_bwd_apply   dz_i = dout_i * g_i + dmean_i / THW              (all branches)
 #include "common.h"
 
 #define MAXSEG 4
@@ -21,6 +21,8 @@ struct SegTable {
   const float* bias[MAXSEG];
   float* dw[MAXSEG];
   float* db[MAXSEG];
+  const bf16_t* bn_y[MAXSEG];   // producer BN raw output of each branch (backward partials), or null
+  const float* bn_ss[MAXSEG];   // its [mean, invstd, scale, shift]
 };
 
 __device__ __forceinline__ int seg_of(const SegTable& t, int c) {
@@ -116,68 +118,88 @@ __global__ __launch_bounds__(256) void gate_bwd_reduce_kernel(SegTable t, const 
   }
 }
 
-// per segment: dpre[b,c] = dg*g*(1-g) (in place in dg), dmean[b,c] = sum_k dpre[b,k] W[k,c]
-__global__ void gate_bwd_dmean_kernel(SegTable t, float* __restrict__ dg, const float* __restrict__ g,
-                                      int Ctot, float* __restrict__ dmean) {
-  const int b = blockIdx.x, s = blockIdx.y;
-  if (s >= t.nseg) return;
-  const int c0 = t.off[s], C = t.off[s + 1] - c0;
-  extern __shared__ float dp[];
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const long long i = (long long)b * Ctot + c0 + c;
+// dpre = dg * g * (1 - g), in place (all segments at once: [B, Ctot])
+__global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict__ g, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     const float gg = g[i];
-    const float v = dg[i] * gg * (1.f - gg);
-    dp[c] = v;
-    dg[i] = v;
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f;
-    for (int k = 0; k < C; ++k) a += dp[k] * t.w[s][(long long)k * C + c];
-    dmean[(long long)b * Ctot + c0 + c] = a;
+    dg[i] = dg[i] * gg * (1.f - gg);
   }
 }
 
-// dW[c, k] += sum_b dpre[b, c] * mean[b, k];  db[c] += sum_b dpre[b, c]
-__global__ void gate_bwd_dw_kernel(SegTable t, const float* __restrict__ dpre, const float* __restrict__ mean,
-                                   int Ctot, int B) {
-  const int s = blockIdx.z;
-  if (s >= t.nseg) return;
-  const int c0 = t.off[s], C = t.off[s + 1] - c0;
-  const int c = blockIdx.y;
-  if (c >= C) return;
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < C; k += gridDim.x * blockDim.x) {
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) a += dpre[(long long)b * Ctot + c0 + c] * mean[(long long)b * Ctot + c0 + k];
-    t.dw[s][(long long)c * C + k] += a;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) a += dpre[(long long)b * Ctot + c0 + c];
-    t.db[s][c] += a;
-  }
-}
-
-// dz_seg[r, c] = dout[r, c] * g[b, c] + dmean[b, c] * inv_thw
+// dz_seg[r, c] = dout[r, c] * g[b, c] + dmean[b, c] * inv_thw.
+// Block-structured (each thread owns one 8-channel chunk of the concat row) so that, when the
+// branches carry producer-BN info, the BN-backward partial sums of every branch's last BN layer
+// (sum dz*mask, sum dz*mask*xhat) are produced here: part[blk][2][Ctot].
 __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ dmean, int Ctot,
-                                                             long long rows, int thw, float inv_thw) {
-  const int cpr = Ctot >> 3;
-  const long long n = rows * cpr;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / cpr;
-    const int c = (int)(i - r * cpr) * 8;
-    const int s = seg_of(t, c);
-    const int C = t.off[s + 1] - t.off[s];
-    const int b = (int)(r / thw);
-    float d[8];
-    unpack8(*(const uint4*)(dout + r * Ctot + c), d);
-    const long long gi = (long long)b * Ctot + c;
+                                                             long long rows, int thw, float inv_thw,
+                                                             int rows_per_block, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int cpr = Ctot >> 3, rpi = 256 / cpr, tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < rpi;
+  const int c = cc * 8;
+  const int s = active ? seg_of(t, c) : 0;
+  const int C = t.off[s + 1] - t.off[s];
+  const int cl = c - t.off[s];
+  const bool bn = part != nullptr && t.bn_y[s] != nullptr;
+  float mean[8], istd[8], sc[8], sh[8], a1[8], a2[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = d[k] * g[gi + k] + dmean[gi + k] * inv_thw;
-    *(uint4*)(t.dz[s] + r * C + (c - t.off[s])) = pack8(d);
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = bn && active ? t.bn_ss[s][cl + k] : 0.f;
+    istd[k] = bn && active ? t.bn_ss[s][C + cl + k] : 0.f;
+    sc[k] = bn && active ? t.bn_ss[s][2 * C + cl + k] : 0.f;
+    sh[k] = bn && active ? t.bn_ss[s][3 * C + cl + k] : 0.f;
+    a1[k] = 0.f;
+    a2[k] = 0.f;
+  }
+  const long long r_begin = (long long)blockIdx.x * rows_per_block;
+  const long long r_end = min(rows, r_begin + rows_per_block);
+  if (active) {
+    for (long long r = r_begin + rr; r < r_end; r += rpi) {
+      const int b = (int)(r / thw);
+      float d[8];
+      unpack8(*(const uint4*)(dout + r * Ctot + c), d);
+      const long long gi = (long long)b * Ctot + c;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d[k] = d[k] * g[gi + k] + dmean[gi + k] * inv_thw;
+      *(uint4*)(t.dz[s] + r * C + cl) = pack8(d);
+      if (bn) {
+        float y[8];
+        unpack8(*(const uint4*)(t.bn_y[s] + r * C + cl), y);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? d[k] : 0.f;
+          a1[k] += gm;
+          a2[k] += gm * (y[k] - mean[k]) * istd[k];
+        }
+      }
+    }
+  }
+  if (part == nullptr) return;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = a1[k];
+  __syncthreads();
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = a1[k];
+      for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
+      part[(long long)blockIdx.x * 2 * Ctot + c + k] = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = a2[k];
+  __syncthreads();
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = a2[k];
+      for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
+      part[(long long)blockIdx.x * 2 * Ctot + Ctot + c + k] = v;
+    }
   }
 }
 
@@ -246,6 +268,8 @@ static SegTable make_table(int nseg, const int* widths, const void* const* z, vo
     t.bias[i] = v && bias ? bias[i] : nullptr;
     t.dw[i] = v && dw ? dw[i] : nullptr;
     t.db[i] = v && db ? db[i] : nullptr;
+    t.bn_y[i] = nullptr;
+    t.bn_ss[i] = nullptr;
   }
   return t;
 }
@@ -270,26 +294,37 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
   return (int)hipGetLastError();
 }
 
-// dg and dmean are [B, Ctot] fp32 scratch (dg zeroed by the caller)
-MILNCE_API int milnce_gate_bwd(int nseg, const int* widths, const void* const* z, void* const* dz,
-                               const float* const* w, float* const* dw, float* const* db, const void* dout,
-                               const float* g, const float* mean, int B, int thw, float* dg, float* dmean,
-                               hipStream_t stream) {
-  SegTable t = make_table(nseg, widths, z, dz, w, nullptr, dw, db);
+// Phase 1: dpre[B, Ctot] = (sum_thw dout * z) * g * (1 - g)   (dpre zeroed by the caller).
+// The tiny per-branch GEMMs (dW = dpre^T mean, dmean = dpre W) run on hipBLASLt in between.
+MILNCE_API int milnce_gate_bwd_reduce(int nseg, const int* widths, const void* const* z, const void* dout,
+                                      const float* g, int B, int thw, float* dpre, hipStream_t stream) {
+  SegTable t = make_table(nseg, widths, z, nullptr, nullptr, nullptr, nullptr, nullptr);
   const int Ctot = t.off[nseg];
-  int cmax = 0;
-  for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
   const int splits = (thw + 511) / 512;
   const int rpb = (thw + splits - 1) / splits;
   hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, Ctot,
-                     thw, rpb, dg);
-  hipLaunchKernelGGL(gate_bwd_dmean_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, dg, g, Ctot,
-                     dmean);
-  hipLaunchKernelGGL(gate_bwd_dw_kernel, dim3((cmax + 255) / 256, cmax, nseg), dim3(256), 0, stream, t, dg, mean,
-                     Ctot, B);
+                     thw, rpb, dpre);
+  const long long n = (long long)B * Ctot;
+  hipLaunchKernelGGL(gate_dpre_kernel, dim3(grid_for(n)), dim3(256), 0, stream, dpre, g, n);
+  return (int)hipGetLastError();
+}
+
+// Phase 2: dz_i = dout_i * g_i + dmean_i / THW, plus (part != null) the producer-BN partials of
+// every branch whose bn_y[i] is given: part must hold nparts * 2 * Ctot floats.
+MILNCE_API int milnce_gate_bwd_apply(int nseg, const int* widths, void* const* dz, const void* dout, const float* g,
+                                     const float* dmean, int B, int thw, const void* const* bn_y,
+                                     const float* const* bn_ss, float* part, int nparts, hipStream_t stream) {
+  SegTable t = make_table(nseg, widths, nullptr, dz, nullptr, nullptr, nullptr, nullptr);
+  for (int i = 0; i < nseg; ++i) {
+    t.bn_y[i] = bn_y ? (const bf16_t*)bn_y[i] : nullptr;
+    t.bn_ss[i] = bn_ss ? bn_ss[i] : nullptr;
+  }
+  const int Ctot = t.off[nseg];
+  if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
   const long long rows = (long long)B * thw;
-  hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(grid_for(rows * (Ctot / 8))), dim3(256), 0, stream, t,
-                     (const bf16_t*)dout, g, dmean, Ctot, rows, thw, 1.f / thw);
+  const int rpb = (int)((rows + nparts - 1) / nparts);
+  hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(nparts), dim3(256), 0, stream, t, (const bf16_t*)dout, g, dmean,
+                     Ctot, rows, thw, 1.f / thw, rpb, part);
   return (int)hipGetLastError();
 }
 

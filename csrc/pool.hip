@@ -75,10 +75,27 @@ __device__ __forceinline__ void win_range(int i, int pad, int k, int s, int n_ou
   if (hi > n_out - 1) hi = n_out - 1;
 }
 
+// With bn_y != null the gather also emits the BN-backward partial sums of the BN layer that
+// produced the pool input (dx is that layer's dz): part[blockIdx][2][C]. Requires 256 % (C/8) == 0
+// so every thread keeps one channel chunk across its grid-stride loop.
 __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolParams p, const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ arg,
-                                                          bf16_t* __restrict__ dx, long long nin_chunks) {
+                                                          bf16_t* __restrict__ dx, long long nin_chunks,
+                                                          const bf16_t* __restrict__ bn_y,
+                                                          const float* __restrict__ bn_ss, float* __restrict__ part) {
   const int cpr = p.C >> 3;
+  const bool bn = bn_y != nullptr;
+  const int c_fixed = (threadIdx.x % cpr) * 8;
+  float mean[8], istd[8], sc[8], sh[8], a1[8], a2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    mean[k] = bn ? bn_ss[c_fixed + k] : 0.f;
+    istd[k] = bn ? bn_ss[p.C + c_fixed + k] : 0.f;
+    sc[k] = bn ? bn_ss[2 * p.C + c_fixed + k] : 0.f;
+    sh[k] = bn ? bn_ss[3 * p.C + c_fixed + k] : 0.f;
+    a1[k] = 0.f;
+    a2[k] = 0.f;
+  }
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nin_chunks;
        i += (long long)gridDim.x * blockDim.x) {
     long long r = i / cpr;
@@ -115,6 +132,30 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolParams p, const bf
       }
     }
     *(uint4*)(dx + i * 8) = pack8(acc);
+    if (bn) {
+      float y[8];
+      unpack8(*(const uint4*)(bn_y + i * 8), y);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? acc[k] : 0.f;
+        a1[k] += gm;
+        a2[k] += gm * (y[k] - mean[k]) * istd[k];
+      }
+    }
+  }
+  if (!bn) return;
+  __shared__ float red[2][8][256];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { red[0][k][threadIdx.x] = a1[k]; red[1][k][threadIdx.x] = a2[k]; }
+  __syncthreads();
+  if ((int)threadIdx.x < cpr) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float s1 = 0.f, s2 = 0.f;
+      for (int j = threadIdx.x; j < 256; j += cpr) { s1 += red[0][k][j]; s2 += red[1][k][j]; }
+      part[(long long)blockIdx.x * 2 * p.C + c_fixed + k] = s1;
+      part[(long long)blockIdx.x * 2 * p.C + p.C + c_fixed + k] = s2;
+    }
   }
 }
 
@@ -145,13 +186,16 @@ MILNCE_API int milnce_maxpool_fwd(const void* x, void* y, void* arg, int B, int 
   return (int)hipGetLastError();
 }
 
+// nparts: grid size used (also the number of partial rows written when bn_y != null).
 MILNCE_API int milnce_maxpool_bwd(const void* dy, const void* arg, void* dx, int B, int T, int H, int W, int C,
                                   int To, int Ho, int Wo, int kt, int kh, int kw, int st, int sh, int sw, int pt0,
-                                  int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad, hipStream_t stream) {
+                                  int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad, const void* bn_y,
+                                  const float* bn_ss, float* part, int nparts, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
+  if (bn_y != nullptr && 256 % (C / 8) != 0) return (int)hipErrorInvalidValue;
   PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
   const long long n = (long long)B * T * H * W * (C / 8);
-  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, stream, p, (const bf16_t*)dy,
-                     (const uint8_t*)arg, (bf16_t*)dx, n);
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(nparts), dim3(256), 0, stream, p, (const bf16_t*)dy,
+                     (const uint8_t*)arg, (bf16_t*)dx, n, (const bf16_t*)bn_y, bn_ss, part);
   return (int)hipGetLastError();
 }

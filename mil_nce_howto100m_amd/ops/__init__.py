@@ -24,6 +24,18 @@ def use_hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_ATEN
 
 
+class force_aten:
+    """Context manager: run the ATen implementations on GPU too (A/B comparisons in tests)."""
+
+    def __enter__(self):
+        global _FORCE_ATEN
+        self._prev, _FORCE_ATEN = _FORCE_ATEN, True
+
+    def __exit__(self, *exc):
+        global _FORCE_ATEN
+        _FORCE_ATEN = self._prev
+
+
 def _hip():
     from . import hip_ops  # imported lazily: loads (and checks) the native library
     return hip_ops

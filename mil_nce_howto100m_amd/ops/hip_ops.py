@@ -131,21 +131,56 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
-    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats),
+    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None,
          plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
          plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, stream())
     return y
 
 
-def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan) -> torch.Tensor:
+def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=None) -> torch.Tensor:
+    """dX of a stride-1 conv. With ``producer_bn = (y, ss)`` of the BN layer that produced X,
+    the epilogue also emits that layer's BN-backward partial sums (attached to dX, consumed by
+    its backward instead of a separate reduction pass over dX and y)."""
     kt, kh, kw = plan.k
     assert plan.s == (1, 1, 1), "dgrad is only needed for stride-1 convs"
     dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dy.device)
     pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
-    call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), None,
+    part = None
+    if producer_bn is not None:
+        part = torch.empty((plan.d_grid_m * 2 * plan.d_Npad,), dtype=F32, device=dy.device)
+    call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), ptr(part),
+         ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
          plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
          plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, stream())
+    if part is not None:
+        attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx
+
+
+_FUSE_BN_BWD = True
+
+
+def set_bn_bwd_fusion(enabled: bool) -> bool:
+    """Toggle producer-side BN-backward partial sums (for A/B tests); returns the old value."""
+    global _FUSE_BN_BWD
+    old, _FUSE_BN_BWD = _FUSE_BN_BWD, bool(enabled)
+    return old
+
+
+def attach_bn_partials(dz: torch.Tensor, part: torch.Tensor, nparts: int, stride: int) -> None:
+    """Mark dz with the BN-backward partial sums its producer computed. The version stamp makes
+    the producer ignore them if autograd accumulated other gradients into dz in place."""
+    dz._milnce_bnpart = (part, nparts, stride)
+    dz._milnce_bnver = dz._version
+
+
+def take_bn_partials(dz: torch.Tensor):
+    if not _FUSE_BN_BWD:
+        return None
+    part = getattr(dz, "_milnce_bnpart", None)
+    if part is None or getattr(dz, "_milnce_bnver", -1) != dz._version:
+        return None
+    return part
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tensor:
@@ -161,7 +196,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tenso
 
 
 def _bn_nparts(M: int) -> int:
-    return int(max(1, min(2048, _ceil(M, 2048))))
+    # >= ~4 blocks per CU for parallelism, >= 64 rows per block, <= 2048 partial rows
+    return int(max(1, min(2048, max(min(1024, _ceil(M, 64)), _ceil(M, 2048)))))
 
 
 class _ConvBNReLU(torch.autograd.Function):
@@ -184,6 +220,8 @@ class _ConvBNReLU(torch.autograd.Function):
              ptr(gsum), stream())
         ctx.save_for_backward(x, weight, y, ss, gamma)
         ctx.plan = plan
+        ctx.x_bn = getattr(x, "_milnce_bn", None)  # (y, ss) of the BN layer that produced x
+        z._milnce_bn = (y, ss)
         if gsum is None:
             return z
         ctx.mark_non_differentiable(gsum)
@@ -196,18 +234,23 @@ class _ConvBNReLU(torch.autograd.Function):
         dz = dz.contiguous()
         C = plan.Cout
         dev = dz.device
-        nparts = _bn_nparts(plan.M)
-        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
+        fused = take_bn_partials(dz)
+        if fused is not None:
+            part, nparts, ps = fused
+        else:
+            nparts = _bn_nparts(plan.M)
+            part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
+            ps = C
         coef = torch.empty((3 * C,), dtype=F32, device=dev)
         dgamma = torch.empty((C,), dtype=F32, device=dev)
         dbeta = torch.empty((C,), dtype=F32, device=dev)
         dy = torch.empty_like(y)
-        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts,
-             ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), stream())
+        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
+             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), stream())
         dx = None
         if ctx.needs_input_grad[0]:
             wd = _pack(weight, plan, 1)
-            dx = conv_dgrad(dy, wd, plan)
+            dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
         dw = conv_wgrad(dy, x, plan) if ctx.needs_input_grad[1] else None
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
 
@@ -248,6 +291,7 @@ class _GateConcat(torch.autograd.Function):
              ptr(gsum), B, thw, ptr(mean), ptr(g), ptr(out), stream())
         ctx.save_for_backward(*zs, *ws, g, mean)
         ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
+        ctx.z_bn = [getattr(z, "_milnce_bn", None) for z in zs]
         return out
 
     @staticmethod
@@ -262,14 +306,34 @@ class _GateConcat(torch.autograd.Function):
         ctot = g.shape[1]
         dev = dout.device
         dzs = [torch.empty_like(z) for z in zs]
-        dws = [torch.zeros_like(w) for w in ws]
-        dbs = [torch.zeros((w.shape[0],), dtype=F32, device=dev) for w in ws]
-        dg = torch.zeros((B, ctot), dtype=F32, device=dev)
+        widths = _arr(ctypes.c_int, ctx.widths)
+        dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
+        call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zs]), ptr(dout),
+             ptr(g), B, ctx.thw, ptr(dpre), stream())
+        # per-branch fc backward: plain GEMMs on hipBLASLt
         dmean = torch.empty((B, ctot), dtype=F32, device=dev)
-        call("milnce_gate_bwd", nseg, _arr(ctypes.c_int, ctx.widths), _arr(ctypes.c_void_p, [ptr(z) for z in zs]),
-             _arr(ctypes.c_void_p, [ptr(d) for d in dzs]), _arr(ctypes.c_void_p, [ptr(w) for w in ws]),
-             _arr(ctypes.c_void_p, [ptr(d) for d in dws]), _arr(ctypes.c_void_p, [ptr(d) for d in dbs]),
-             ptr(dout), ptr(g), ptr(mean), B, ctx.thw, ptr(dg), ptr(dmean), stream())
+        dws, dbs = [], []
+        off = 0
+        for w, c in zip(ws, ctx.widths):
+            dp = dpre[:, off:off + c]
+            dws.append(dp.t().mm(mean[:, off:off + c]))
+            dbs.append(dp.sum(0))
+            dmean[:, off:off + c].copy_(dp.mm(w))
+            off += c
+        have_bn = all(zb is not None for zb in ctx.z_bn)
+        rows = B * ctx.thw
+        nparts = int(max(1, min(2048, _ceil(rows, 64))))
+        part = torch.empty((nparts * 2 * ctot,), dtype=F32, device=dev) if have_bn else None
+        call("milnce_gate_bwd_apply", nseg, widths, _arr(ctypes.c_void_p, [ptr(d) for d in dzs]), ptr(dout),
+             ptr(g), ptr(dmean), B, ctx.thw,
+             _arr(ctypes.c_void_p, [ptr(zb[0]) for zb in ctx.z_bn]) if have_bn else None,
+             _arr(ctypes.c_void_p, [ptr(zb[1]) for zb in ctx.z_bn]) if have_bn else None,
+             ptr(part), nparts, stream())
+        if have_bn:
+            off = 0
+            for d, c in zip(dzs, ctx.widths):
+                attach_bn_partials(d, part[off:], nparts, ctot)
+                off += c
         return (None, None, *dzs, *dws, *dbs)
 
 
@@ -312,6 +376,8 @@ class _MaxPool(torch.autograd.Function):
         call("milnce_maxpool_fwd", ptr(x), ptr(y), ptr(arg), *geo, stream())
         ctx.save_for_backward(arg)
         ctx.geo = geo
+        xb = getattr(x, "_milnce_bn", None)
+        ctx.x_bn = xb if (xb is not None and 256 % (C // 8) == 0) else None
         return y
 
     @staticmethod
@@ -320,7 +386,14 @@ class _MaxPool(torch.autograd.Function):
         geo = ctx.geo
         B, T, H, W, C = geo[:5]
         dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dy.device)
-        call("milnce_maxpool_bwd", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo, stream())
+        nparts = int(max(1, min(4096, _ceil(B * T * H * W * (C // 8), 256))))
+        xb = ctx.x_bn
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dy.device) if xb is not None else None
+        call("milnce_maxpool_bwd", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo,
+             ptr(xb[0]) if xb is not None else None, ptr(xb[1]) if xb is not None else None, ptr(part), nparts,
+             stream())
+        if part is not None:
+            attach_bn_partials(dx, part, nparts, C)
         return dx, None, None, None
 
 

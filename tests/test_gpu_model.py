@@ -7,37 +7,51 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+def _grads(model):
+    return {n: p.grad.detach().double().cpu() for n, p in model.named_parameters() if p.grad is not None}
+
+
 def test_model_forward_backward_matches_aten():
+    """HIP path vs an fp64 CPU oracle, benchmarked against MIOpen/ATen bf16 on the same GPU.
+
+    bf16 activations make some weight gradients intrinsically noisy against fp64 (e.g. a conv
+    whose input has a large mean multiplies the rounding residue of the zero-mean BN
+    gradient), so the criterion is: the HIP path is about as accurate as standard bf16
+    training (ATen/MIOpen with bf16 activations), layer by layer.
+    """
+    from mil_nce_howto100m_amd import ops
     from mil_nce_howto100m_amd.models import S3D
-    from mil_nce_howto100m_amd.ops import aten
     torch.manual_seed(0)
     m = S3D(512, blocks=["mixed_3b", "mixed_3c", "mixed_4b"]).cuda()
+    m_aten = copy.deepcopy(m)
     ref = copy.deepcopy(m).cpu().double()
     v = torch.randint(0, 256, (4, 3, 8, 64, 64), dtype=torch.uint8)
     t = torch.randint(0, 66250, (8, 20))
-    ve, te = m(v.cuda(), t.cuda())
-    import mil_nce_howto100m_amd.ops as ops_mod
-    # oracle: CPU fp64 ATen path with identical parameters
-    ver, ter = ref(v.double() / 255.0, t)
-    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()
-    assert rel(ve, ver) < 0.08
-    assert rel(te, ter) < 0.02
-    # Identical upstream gradients (a fixed random linear functional of the embeddings): the
-    # MIL-NCE softmax would amplify the bf16 forward differences into the comparison.
-    gv = torch.randn(ve.shape, dtype=torch.float64)
-    gt = torch.randn(te.shape, dtype=torch.float64)
-    ((ve.double() * gv.cuda()).sum() + (te.double() * gt.cuda()).sum()).backward()
-    ((ver * gv).sum() + (ter * gt).sum()).backward()
-    errs = []
-    for (n1, p1), (n2, p2) in zip(m.named_parameters(), ref.named_parameters()):
-        if p2.grad is None:
-            continue
-        assert p1.grad is not None, n1
-        errs.append((n1, rel(p1.grad, p2.grad), p2.grad.norm().item()))
-    for n, e, g in errs:
-        print(f"{n:45s} rel_err={e:.4f} |g|={g:.3e}")
-    bad = [(n, e) for n, e, g in errs if e > 0.12]
-    assert not bad, bad
+    gv = torch.randn(4, 512, dtype=torch.float64)
+    gt = torch.randn(8, 512, dtype=torch.float64)
+
+    def run(model, vid, txt):
+        ve, te = model(vid, txt)
+        ((ve.double() * gv.to(ve.device)).sum() + (te.double() * gt.to(te.device)).sum()).backward()
+        return ve.detach().double().cpu(), te.detach().double().cpu()
+
+    ve, te = run(m, v.cuda(), t.cuda())
+    with ops.force_aten():
+        va, ta = run(m_aten, v.cuda(), t.cuda())
+    vr, tr = run(ref, v.double() / 255.0, t)
+    rel = lambda a, b: ((a - b).norm() / b.norm()).item()
+    e_hip, e_aten = rel(ve, vr), rel(va, vr)
+    print(f"video embd rel err: hip {e_hip:.4f} aten-bf16 {e_aten:.4f}")
+    assert e_hip < max(0.05, 2.0 * e_aten)
+    assert rel(te, tr) < 0.02
+    gh, ga, gr = _grads(m), _grads(m_aten), _grads(ref)
+    worse = []
+    for n in gr:
+        eh, ea = rel(gh[n], gr[n]), rel(ga[n], gr[n])
+        print(f"{n:45s} hip={eh:.4f} aten_bf16={ea:.4f}")
+        if eh > max(0.1, 2.5 * ea):
+            worse.append((n, eh, ea))
+    assert not worse, worse
 
 
 def test_bench_step_runs():

@@ -313,3 +313,38 @@ def test_hard_dtw_path_matches_cpu():
     assert torch.allclose(l.detach().cpu(), lc, rtol=1e-6, atol=1e-6)
     l.mean().backward()
     assert torch.isfinite(x.grad).all()
+
+
+def _stack_grads(h, x, convs, bns):
+    xh = x.clone().requires_grad_(True)
+    z = h.conv_bn_relu(xh, convs[0].weight, bns[0], (1, 1, 1), (0, 1, 1), True)
+    assert hasattr(z, "_milnce_bn")
+    z = h.conv_bn_relu(z, convs[1].weight, bns[1], (1, 1, 1), (1, 0, 0), True)
+    # a pool after the second unit exercises the pool-backward partials too
+    z = h.maxpool3d(z, (1, 3, 3), (1, 2, 2), True)
+    torch.manual_seed(12)
+    z.backward(torch.randn_like(z))
+    out = [xh.grad] + [p.grad.clone() for m in list(convs) + list(bns) for p in m.parameters()]
+    for m in list(convs) + list(bns):
+        for p in m.parameters():
+            p.grad = None
+    return out
+
+
+def test_fused_bn_backward_partials_match_unfused():
+    """dgrad-epilogue / pool-backward BN partial sums == the standalone reduction pass."""
+    torch.manual_seed(11)
+    h = hip()
+    B, T, H, W, c0, c1, c2 = 2, 4, 6, 6, 32, 48, 64
+    x = torch.randn(B, T, H, W, c0, device=DEV).to(torch.bfloat16)
+    convs = [nn.Conv3d(c0, c1, (1, 3, 3), 1, (0, 1, 1), bias=False).to(DEV),
+             nn.Conv3d(c1, c2, (3, 1, 1), 1, (1, 0, 0), bias=False).to(DEV)]
+    bns = [nn.BatchNorm3d(c1).to(DEV), nn.BatchNorm3d(c2).to(DEV)]
+    fused = _stack_grads(h, x, convs, bns)
+    old = h.set_bn_bwd_fusion(False)
+    try:
+        plain = _stack_grads(h, x, convs, bns)
+    finally:
+        h.set_bn_bwd_fusion(old)
+    for a, b in zip(fused, plain):
+        assert rel_err(a, b) < 5e-3
