@@ -180,25 +180,44 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
 // part rows have stride 2*ps (ps = C for bn_bwd_reduce partials, Npad for conv-epilogue partials).
-__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps, int C,
-                                                              double count, const float* __restrict__ gamma,
-                                                              const float* __restrict__ ss, float* __restrict__ dgamma,
-                                                              float* __restrict__ dbeta, float* __restrict__ coef) {
-  __shared__ double red[2][8][32];
+// 1024 threads = 32 channels x 32 row groups; each thread keeps two independent fp64 chains
+// so consecutive partial rows are in flight together (the reduction is latency-, not
+// bandwidth-bound: a few MB spread over C/32 blocks).
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps,
+                                                               int C, double count, const float* __restrict__ gamma,
+                                                               const float* __restrict__ ss,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ coef) {
+  __shared__ double red[2][32][33];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
-  double s1 = 0.0, s2 = 0.0;
+  double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
   if (c < C) {
-    for (int i = rg; i < nparts; i += 8) {
+    int i = rg;
+    for (; i + 96 < nparts; i += 128) {  // four rows per thread in flight
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* a = part + (long long)(i + 32 * u) * 2 * ps + c;
+        v[2 * u] = a[0];
+        v[2 * u + 1] = a[ps];
+      }
+      s1 += (double)v[0] + (double)v[2];
+      s2 += (double)v[1] + (double)v[3];
+      t1 += (double)v[4] + (double)v[6];
+      t2 += (double)v[5] + (double)v[7];
+    }
+    for (; i < nparts; i += 32) {
       s1 += part[(long long)i * 2 * ps + c];
       s2 += part[(long long)i * 2 * ps + ps + c];
     }
   }
-  red[0][rg][cl] = s1;
-  red[1][rg][cl] = s2;
+  red[0][rg][cl] = s1 + t1;
+  red[1][rg][cl] = s2 + t2;
   __syncthreads();
   if (rg != 0 || c >= C) return;
-  for (int k = 1; k < 8; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
+  s1 = 0.0; s2 = 0.0;
+  for (int k = 0; k < 32; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
   dbeta[c] = (float)s1;
   dgamma[c] = (float)s2;
   coef[c] = gamma[c] * ss[C + c];
@@ -206,27 +225,36 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[2 * C + c] = (float)(s2 / count);
 }
 
+// dy = coef0 * (dz*mask - coef1 - xhat*coef2). Each thread owns one 8-channel chunk (its
+// per-channel constants live in registers) and walks rows [r_begin, r_end) of its block.
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dz, int ldz, const bf16_t* __restrict__ y, int ldy,
-    const float* __restrict__ ss, const float* __restrict__ coef, int C, long long nchunks,
-    bf16_t* __restrict__ dy) {
-  const int cpr = C >> 3;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < nchunks;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / cpr;
-    const int c0 = (int)(i - r * cpr) * 8;
+    const float* __restrict__ ss, const float* __restrict__ coef, int C, long long M, int rows_per_block,
+    bf16_t* __restrict__ dy, int lddy) {
+  const int cpr = C >> 3, rpi = 256 / cpr;
+  const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
+  if (rr >= rpi) return;
+  const int c0 = cc * 8;
+  float sc[8], sh[8], mean[8], istd[8], k0[8], k1[8], k2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    mean[k] = ss[c]; istd[k] = ss[C + c]; sc[k] = ss[2 * C + c]; sh[k] = ss[3 * C + c];
+    k0[k] = coef[c]; k1[k] = coef[C + c]; k2[k] = coef[2 * C + c];
+  }
+  const long long r_begin = (long long)blockIdx.x * rows_per_block;
+  const long long r_end = min(M, r_begin + rows_per_block);
+  for (long long r = r_begin + rr; r < r_end; r += rpi) {
     float g[8], v[8], o[8];
     unpack8(*(const uint4*)(dz + r * ldz + c0), g);
     unpack8(*(const uint4*)(y + r * ldy + c0), v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float sc = ss[2 * C + c], sh = ss[3 * C + c];
-      const float gm = (v[k] * sc + sh > 0.f) ? g[k] : 0.f;
-      const float xh = (v[k] - ss[c]) * ss[C + c];
-      o[k] = coef[c] * (gm - coef[C + c] - xh * coef[2 * C + c]);
+      const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? g[k] : 0.f;
+      const float xh = (v[k] - mean[k]) * istd[k];
+      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
     }
-    *(uint4*)(dy + r * C + c0) = pack8(o);
+    *(uint4*)(dy + r * lddy + c0) = pack8(o);
   }
 }
 
@@ -259,7 +287,7 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
 // have_part = 0: reduce them here (ps = C).
 MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
                              const float* gamma, float* part, int nparts, int ps, int have_part, float* dgamma,
-                             float* dbeta, float* coef, void* dy, hipStream_t stream) {
+                             float* dbeta, float* coef, void* dy, int lddy, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   if (!have_part) {
     const int rows_per_block = (int)((M + nparts - 1) / nparts);
@@ -267,12 +295,14 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
                        (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
     ps = C;
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, ps, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(1024), 0, stream, part, nparts, ps, C,
                      (double)M, gamma, ss, dgamma, dbeta, coef);
-  const long long nchunks = M * (C / 8);
-  long long grid = (nchunks + 255) / 256;
-  if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((int)grid), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
-                     (const bf16_t*)y, ldy, ss, coef, C, nchunks, (bf16_t*)dy);
+  const int rpi = 256 / (C / 8);
+  long long nblk = (M + 16LL * rpi - 1) / (16LL * rpi);  // >= 16 rows per thread
+  if (nblk > 8192) nblk = 8192;
+  if (nblk < 1) nblk = 1;
+  const int rpb = (int)((M + nblk - 1) / nblk);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((int)nblk), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
+                     (const bf16_t*)y, ldy, ss, coef, C, M, rpb, (bf16_t*)dy, lddy);
   return (int)hipGetLastError();
 }

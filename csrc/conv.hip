@@ -40,6 +40,7 @@ struct ConvParams {
   int bn_mode;
   const bf16_t* bn_y;
   const float* bn_ss;
+  int bn_ld;  // row stride of bn_y (elements)
 };
 
 template <int BK>
@@ -132,8 +133,11 @@ __device__ __forceinline__ void store_tiles(const AReg (&areg)[NA], const uint4 
 // each lane's accumulator holds 4 consecutive output channels of one output position: the
 // epilogue packs them into 8-byte LDS writes and the per-channel BN sums accumulate per lane
 // across the persistent M loop (one cross-lane reduction per kernel, not per tile).
-template <int BM, int BN, int BK, bool U8>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
+// EPI (compile time, so the plain forward does not carry the backward epilogue's registers):
+// 0 no statistics, 1 BN forward sums, 2 producer-BN backward partials (see ConvParams).
+// __launch_bounds__(256, 2): 2 waves per SIMD = 2 blocks per CU (VGPR budget 256).
+template <int BM, int BN, int BK, bool U8, int EPI>
+__global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
   constexpr int VEC = U8 ? 4 : 8;
   constexpr int ESZ = U8 ? 1 : 2;
   constexpr int A_CPR = BK / VEC;
@@ -174,16 +178,16 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
   const uint32_t clip_bytes = (uint32_t)(p.x_bstride * ESZ);
 
   build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
-  if (p.bn_mode == 2) {
+  if constexpr (EPI == 2) {
     for (int t = tid; t < 4 * BN; t += 256) {
       const int q = t / BN, c = n0 + (t - q * BN);
       ssl[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
     }
   }
-  const uint32_t bny_rec = (uint32_t)((long long)p.M * p.Cout * 2 > 0x7FFFFFF0LL ? 0x7FFFFFF0LL : (long long)p.M * p.Cout * 2);
-  const auto bny_rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.bn_y, (short)0, (int)bny_rec, 0x00020000);
-
   float st_s[TN][4], st_q[TN][4];
+  float e_s[8], e_q[8];  // EPI 2: partials of this thread's fixed 8-channel chunk (tid % (BN/8))
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -282,27 +286,13 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const f32x4 v = acc[j][i];
-        if (p.bn_mode == 1 && rv) {
+        if constexpr (EPI == 1) {
+          if (rv) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             st_s[j][r] += v[r];
             st_q[j][r] += v[r] * v[r];
           }
-        } else if (p.bn_mode == 2) {
-          const int cl = wc * WN + j * 16 + (lane >> 4) * 4;  // local channel of element r = 0
-          const uint32_t off = rv ? (uint32_t)(((long long)(m0 + row) * p.Cout + n0 + cl) * 2) : 0x80000000u;
-          const auto yv2 = __builtin_amdgcn_raw_buffer_load_b64(bny_rs, off, 0, 0);
-          const uint2 yv = __builtin_bit_cast(uint2, yv2);
-          const float yf[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
-                               __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float mean = ssl[cl + r], istd = ssl[BN + cl + r], sc = ssl[2 * BN + cl + r],
-                        sh = ssl[3 * BN + cl + r];
-            const float gm = (yf[r] * sc + sh > 0.f) ? v[r] : 0.f;  // out-of-range rows: y = 0 -> sc*0+sh
-            const float gmv = rv ? gm : 0.f;
-            st_s[j][r] += gmv;
-            st_q[j][r] += gmv * (yf[r] - mean) * istd;
           }
         }
         uint2 o;
@@ -319,13 +309,49 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(ConvParams p) {
       const int cid = tid + it * 256;
       const int row = cid / OCPR, cc = cid % OCPR;
       const int m = m0 + row, n = n0 + cc * 8;
-      if (m < p.M && n < p.Cout) {
-        *(uint4*)(p.y + (long long)m * p.ldy + n) = *(const uint4*)(Es + row * LDE + cc * 8);
+      const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
+      const bool ok = (m < p.M) & (n < p.Cout);
+      if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
+      if constexpr (EPI == 2) {
+        // BN-backward partials from the bf16 dz actually stored (same values the standalone
+        // reduction would read); the chunk column cc == tid % OCPR is fixed for this thread.
+        if (ok) {
+          float d8[8], y8[8];
+          unpack8(dv, d8);
+          unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int cl = cc * 8 + k;
+            const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
+            e_s[k] += gm;
+            e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
+          }
+        }
       }
     }
   }
 
-  if (p.bn_mode != 0) {
+  if constexpr (EPI == 2) {
+    constexpr int OCPR = BN / 8;
+    __syncthreads();
+    float* red = (float*)smem;  // [2][8][256]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[k * 256 + tid] = e_s[k]; red[(8 + k) * 256 + tid] = e_q[k]; }
+    __syncthreads();
+    if (tid < OCPR) {
+      const int npad = p.num_n_tiles * BN;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int j = tid; j < 256; j += OCPR) { s1 += red[k * 256 + j]; s2 += red[(8 + k) * 256 + j]; }
+        const int col = n0 + tid * 8 + k;
+        p.stats[(long long)m_slot * 2 * npad + col] = s1;
+        p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
+      }
+    }
+  }
+
+  if constexpr (EPI == 1) {
     // reduce over the 16 lanes (output rows) that share a channel group, then over wr
 #pragma unroll
     for (int j = 0; j < TN; ++j)
@@ -624,35 +650,48 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, bf16_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------
-template <int BM, int BN, int BK, bool U8>
-static int launch_fwd(ConvParams& p, hipStream_t stream) {
+template <int BM, int BN, int BK, bool U8, int EPI>
+static int launch_fwd_epi(ConvParams& p, hipStream_t stream) {
   const size_t kloop = (size_t)2 * (BM + BN) * BK * 2;
   const size_t epi = (size_t)BM * (BN + 8) * 2;
   const size_t lds = (kloop > epi ? kloop : epi) + 8 * 160 + 16 * BN;  // + tap table + producer-BN consts
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, BK, U8>,
+    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_kernel<BM, BN, BK, U8, EPI>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   const int nblocks = p.num_n_tiles * p.grid_m;
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, BK, U8>), dim3(nblocks), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, BK, U8, EPI>), dim3(nblocks), dim3(256), lds, stream, p);
   return (int)hipGetLastError();
+}
+
+template <int BM, int BN, int BK, bool U8>
+static int launch_fwd(ConvParams& p, hipStream_t stream) {
+  if constexpr (U8) {
+    if (p.bn_mode == 0) return launch_fwd_epi<BM, BN, BK, true, 0>(p, stream);
+    return p.bn_mode == 1 ? launch_fwd_epi<BM, BN, BK, true, 1>(p, stream) : (int)hipErrorInvalidValue;
+  } else {
+    if (p.bn_mode == 0) return launch_fwd_epi<BM, BN, BK, false, 0>(p, stream);
+    if (p.bn_mode == 1) return launch_fwd_epi<BM, BN, BK, false, 1>(p, stream);
+    return launch_fwd_epi<BM, BN, BK, false, 2>(p, stream);
+  }
 }
 
 // x: input, w: packed weight [Npad][Kpad], y: out [M][ldy], stats: [grid_m][2][Npad] or null.
 // Returns grid_m through *grid_m_out (for sizing the stats buffer, call with y == nullptr).
 MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
-                               const float* bn_ss,
+                               const float* bn_ss, int bn_ld,
                                int B, int T, int H, int W, int Cin, int Cout,
                                int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
                                int Kpad, int Npad, int ldy, int bn, int bk, int grid_m,
                                hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
-  p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss;
+  p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss; p.bn_ld = bn_ld;
   if (KT * KH * KW > 160) return (int)hipErrorInvalidValue;  // tap table capacity
   p.bn_mode = stats == nullptr ? 0 : (bn_y == nullptr ? 1 : 2);
+  if (p.bn_mode == 2 && (Cout % 8 || ldy != Cout)) return (int)hipErrorInvalidValue;
   p.T = T; p.H = H; p.W = W; p.Cin = Cin;
   p.To = (T + 2 * pt - KT) / st + 1;
   p.Ho = (H + 2 * ph - KH) / sh + 1;

@@ -23,6 +23,7 @@ struct SegTable {
   float* db[MAXSEG];
   const bf16_t* bn_y[MAXSEG];   // producer BN raw output of each branch (backward partials), or null
   const float* bn_ss[MAXSEG];   // its [mean, invstd, scale, shift]
+  int bn_ld[MAXSEG];            // row stride of bn_y
 };
 
 __device__ __forceinline__ int seg_of(const SegTable& t, int c) {
@@ -53,24 +54,29 @@ __global__ void gate_fc_kernel(SegTable t, const float* __restrict__ gsum, float
   }
 }
 
-// out[row, c] = z_seg[row, c - off] * g[b, c]
-__global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float* __restrict__ g, int Ctot,
-                                                         long long rows, int thw, bf16_t* __restrict__ out) {
-  const int cpr = Ctot >> 3;
-  const long long n = rows * cpr;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / cpr;
-    const int c = (int)(i - r * cpr) * 8;
-    const int s = seg_of(t, c);
-    const int C = t.off[s + 1] - t.off[s];
-    const int b = (int)(r / thw);
+// out[row, c] = z_seg[row, c - off] * g[b, c]. Grid (splits, B): every thread owns one fixed
+// 8-channel chunk of the concat row (its gate values are loaded once) and walks rows of clip b.
+__global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float* __restrict__ g, int Ctot, int thw,
+                                                         int rows_per_block, bf16_t* __restrict__ out) {
+  const int cpr = Ctot >> 3, rpi = 256 / cpr, tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  if (rr >= rpi) return;
+  const int c = cc * 8;
+  const int s = seg_of(t, c);
+  const int C = t.off[s + 1] - t.off[s], cl = c - t.off[s];
+  const int b = blockIdx.y;
+  float gg[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) gg[k] = g[(size_t)b * Ctot + c + k];
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
+  const bf16_t* zs = t.z[s] + (size_t)b * thw * C + cl;
+  bf16_t* o = out + (size_t)b * thw * Ctot + c;
+  for (int r = r_begin + rr; r < r_end; r += rpi) {
     float f[8];
-    unpack8(*(const uint4*)(t.z[s] + r * C + (c - t.off[s])), f);
-    const float* gg = g + (long long)b * Ctot + c;
+    unpack8(*(const uint4*)(zs + (size_t)r * C), f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f[k] *= gg[k];
-    *(uint4*)(out + r * Ctot + c) = pack8(f);
+    *(uint4*)(o + (size_t)r * Ctot) = pack8(f);
   }
 }
 
@@ -127,14 +133,14 @@ __global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict
 }
 
 // dz_seg[r, c] = dout[r, c] * g[b, c] + dmean[b, c] * inv_thw.
-// Block-structured (each thread owns one 8-channel chunk of the concat row) so that, when the
-// branches carry producer-BN info, the BN-backward partial sums of every branch's last BN layer
-// (sum dz*mask, sum dz*mask*xhat) are produced here: part[blk][2][Ctot].
+// Grid (splits, B), each thread owns one fixed 8-channel chunk of the concat row, so when the
+// branches carry producer-BN info the BN-backward partial sums of every branch's last BN layer
+// (sum dz*mask, sum dz*mask*xhat) are produced here: part[b * splits + split][2][Ctot].
 __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ g,
-                                                             const float* __restrict__ dmean, int Ctot,
-                                                             long long rows, int thw, float inv_thw,
-                                                             int rows_per_block, float* __restrict__ part) {
+                                                             const float* __restrict__ dmean, int Ctot, int thw,
+                                                             float inv_thw, int rows_per_block,
+                                                             float* __restrict__ part) {
   __shared__ float red[256 * 8];
   const int cpr = Ctot >> 3, rpi = 256 / cpr, tid = threadIdx.x;
   const int cc = tid % cpr, rr = tid / cpr;
@@ -144,33 +150,37 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
   const int C = t.off[s + 1] - t.off[s];
   const int cl = c - t.off[s];
   const bool bn = part != nullptr && t.bn_y[s] != nullptr;
-  float mean[8], istd[8], sc[8], sh[8], a1[8], a2[8];
+  const int b = blockIdx.y;
+  float mean[8], istd[8], sc[8], sh[8], a1[8], a2[8], gg[8], dm[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mean[k] = bn && active ? t.bn_ss[s][cl + k] : 0.f;
     istd[k] = bn && active ? t.bn_ss[s][C + cl + k] : 0.f;
     sc[k] = bn && active ? t.bn_ss[s][2 * C + cl + k] : 0.f;
     sh[k] = bn && active ? t.bn_ss[s][3 * C + cl + k] : 0.f;
+    gg[k] = active ? g[(size_t)b * Ctot + c + k] : 0.f;
+    dm[k] = active ? dmean[(size_t)b * Ctot + c + k] * inv_thw : 0.f;
     a1[k] = 0.f;
     a2[k] = 0.f;
   }
-  const long long r_begin = (long long)blockIdx.x * rows_per_block;
-  const long long r_end = min(rows, r_begin + rows_per_block);
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
   if (active) {
-    for (long long r = r_begin + rr; r < r_end; r += rpi) {
-      const int b = (int)(r / thw);
+    const size_t row0 = (size_t)b * thw;
+    for (int r = r_begin + rr; r < r_end; r += rpi) {
+      const size_t row = row0 + r;
       float d[8];
-      unpack8(*(const uint4*)(dout + r * Ctot + c), d);
-      const long long gi = (long long)b * Ctot + c;
+      unpack8(*(const uint4*)(dout + row * Ctot + c), d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = d[k] * g[gi + k] + dmean[gi + k] * inv_thw;
-      *(uint4*)(t.dz[s] + r * C + cl) = pack8(d);
+      for (int k = 0; k < 8; ++k) d[k] = d[k] * gg[k] + dm[k];
+      const uint4 dv = pack8(d);
+      *(uint4*)(t.dz[s] + row * C + cl) = dv;
       if (bn) {
-        float y[8];
-        unpack8(*(const uint4*)(t.bn_y[s] + r * C + cl), y);
+        float y[8], dr[8];
+        unpack8(dv, dr);  // partials from the stored (bf16) gradient
+        unpack8(*(const uint4*)(t.bn_y[s] + row * t.bn_ld[s] + cl), y);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? d[k] : 0.f;
+          const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? dr[k] : 0.f;
           a1[k] += gm;
           a2[k] += gm * (y[k] - mean[k]) * istd[k];
         }
@@ -178,6 +188,7 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
     }
   }
   if (part == nullptr) return;
+  const size_t prow = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[k * 256 + tid] = a1[k];
   __syncthreads();
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
     for (int k = 0; k < 8; ++k) {
       float v = a1[k];
       for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
-      part[(long long)blockIdx.x * 2 * Ctot + c + k] = v;
+      part[prow * 2 * Ctot + c + k] = v;
     }
   }
   __syncthreads();
@@ -198,7 +209,7 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
     for (int k = 0; k < 8; ++k) {
       float v = a2[k];
       for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
-      part[(long long)blockIdx.x * 2 * Ctot + Ctot + c + k] = v;
+      part[prow * 2 * Ctot + Ctot + c + k] = v;
     }
   }
 }
@@ -270,6 +281,7 @@ static SegTable make_table(int nseg, const int* widths, const void* const* z, vo
     t.db[i] = v && db ? db[i] : nullptr;
     t.bn_y[i] = nullptr;
     t.bn_ss[i] = nullptr;
+    t.bn_ld[i] = 0;
   }
   return t;
 }
@@ -288,9 +300,12 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
   for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
   hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum,
                      1.f / thw, Ctot, mean, g);
-  const long long rows = (long long)B * thw;
-  hipLaunchKernelGGL(gate_scale_kernel, dim3(grid_for(rows * (Ctot / 8))), dim3(256), 0, stream, t, g, Ctot, rows,
-                     thw, (bf16_t*)out);
+  if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
+  const int rpi = 256 / (Ctot / 8);
+  const int splits = (thw + 32 * rpi - 1) / (32 * rpi);  // >= 32 row iterations per thread
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(gate_scale_kernel, dim3(splits, B), dim3(256), 0, stream, t, g, Ctot, thw, rpb,
+                     (bf16_t*)out);
   return (int)hipGetLastError();
 }
 
@@ -310,21 +325,24 @@ MILNCE_API int milnce_gate_bwd_reduce(int nseg, const int* widths, const void* c
 }
 
 // Phase 2: dz_i = dout_i * g_i + dmean_i / THW, plus (part != null) the producer-BN partials of
-// every branch whose bn_y[i] is given: part must hold nparts * 2 * Ctot floats.
+// every branch whose bn_y[i] is given: nparts = B * splits, part must hold nparts * 2 * Ctot floats.
 MILNCE_API int milnce_gate_bwd_apply(int nseg, const int* widths, void* const* dz, const void* dout, const float* g,
                                      const float* dmean, int B, int thw, const void* const* bn_y,
-                                     const float* const* bn_ss, float* part, int nparts, hipStream_t stream) {
+                                     const float* const* bn_ss, const int* bn_ld, float* part, int nparts,
+                                     hipStream_t stream) {
   SegTable t = make_table(nseg, widths, nullptr, dz, nullptr, nullptr, nullptr, nullptr);
   for (int i = 0; i < nseg; ++i) {
     t.bn_y[i] = bn_y ? (const bf16_t*)bn_y[i] : nullptr;
     t.bn_ss[i] = bn_ss ? bn_ss[i] : nullptr;
+    t.bn_ld[i] = bn_ld ? bn_ld[i] : widths[i];
   }
   const int Ctot = t.off[nseg];
   if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
-  const long long rows = (long long)B * thw;
-  const int rpb = (int)((rows + nparts - 1) / nparts);
-  hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(nparts), dim3(256), 0, stream, t, (const bf16_t*)dout, g, dmean,
-                     Ctot, rows, thw, 1.f / thw, rpb, part);
+  if (nparts % B) return (int)hipErrorInvalidValue;  // nparts = B * splits
+  const int splits = nparts / B;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, g, dmean,
+                     Ctot, thw, 1.f / thw, rpb, part);
   return (int)hipGetLastError();
 }
 

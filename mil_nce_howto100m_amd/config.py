@@ -99,6 +99,12 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--stop_epoch", type=int, default=0,
                    help="end this run after this epoch (simulated interruption for resume tests)")
     g.add_argument("--hip_graph", type=int, default=0, help="capture the train step in a HIP graph")
+    g.add_argument("--watchdog_s", type=float, default=0.0,
+                   help="abort a rank (exit 3, stacks dumped) after this many seconds without a finished step")
+    g.add_argument("--phase_timers", type=int, default=0,
+                   help="HIP-event timers per step phase, reported in the JSONL metrics")
+    g.add_argument("--fault_at_step", type=int, default=-1,
+                   help="fault injection: raise on this global step (tests kill-and-resume)")
     return p
 
 

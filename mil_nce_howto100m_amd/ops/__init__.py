@@ -50,6 +50,16 @@ def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool
     return (z, None) if want_gsum else z
 
 
+def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = False):
+    """Several 1x1x1 conv -> BN -> ReLU units on the same input (one fused GEMM on GPU).
+    Returns the list of outputs and the gating sum of the first (None on the ATen path)."""
+    if use_hip(x):
+        out = _hip().conv1x1_group_bn_relu(x, weights, bns, training, want_gsum0)
+        n = len(weights)
+        return list(out[:n]), (out[n] if want_gsum0 else None)
+    return [aten.conv_bn_relu(x, w, bn, (1, 1, 1), (0, 0, 0), training) for w, bn in zip(weights, bns)], None
+
+
 def gate_concat(branches, fc_weights, fc_biases, gsums=None):
     if use_hip(branches[0]):
         return _hip().gate_concat(branches, fc_weights, fc_biases, gsums)

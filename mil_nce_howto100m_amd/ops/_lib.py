@@ -20,19 +20,19 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libmilnce_hip.so")
 P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
 
 SIGNATURES: Dict[str, list] = {
-    "milnce_conv_fwd": [P, I, P, P, P, P, P] + [I] * 6 + [I] * 9 + [I] * 6 + [P],
+    "milnce_conv_fwd": [P, I, P, P, P, P, P, I] + [I] * 6 + [I] * 9 + [I] * 6 + [P],
     "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 6 + [P],
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
-    "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, P],
+    "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, P],
     "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P],
     "milnce_gate_bwd_reduce": [I, P, P, P, P, I, I, P, P],
-    "milnce_gate_bwd_apply": [I, P, P, P, P, P, I, I, P, P, P, I, P],
+    "milnce_gate_bwd_apply": [I, P, P, P, P, P, I, I, P, P, P, P, I, P],
     "milnce_avgpool": [P, I, I, I, P, P],
     "milnce_avgpool_bwd": [P, I, I, I, P, P],
     "milnce_maxpool_fwd": [P, P, P] + [I] * 21 + [P],
-    "milnce_maxpool_bwd": [P, P, P] + [I] * 21 + [P, P, P, I, P],
+    "milnce_maxpool_bwd": [P, P, P] + [I] * 21 + [P, I, P, P, I, P],
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],

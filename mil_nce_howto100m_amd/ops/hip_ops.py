@@ -131,14 +131,14 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
-    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None,
+    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
          plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
          plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, stream())
     return y
 
 
 def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=None) -> torch.Tensor:
-    """dX of a stride-1 conv. With ``producer_bn = (y, ss)`` of the BN layer that produced X,
+    """dX of a stride-1 conv. With ``producer_bn = (y, ss, ld)`` of the BN layer that produced X,
     the epilogue also emits that layer's BN-backward partial sums (attached to dX, consumed by
     its backward instead of a separate reduction pass over dX and y)."""
     kt, kh, kw = plan.k
@@ -150,6 +150,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
         part = torch.empty((plan.d_grid_m * 2 * plan.d_Npad,), dtype=F32, device=dy.device)
     call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), ptr(part),
          ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
+         producer_bn[2] if part is not None else 0,
          plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
          plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, stream())
     if part is not None:
@@ -220,8 +221,8 @@ class _ConvBNReLU(torch.autograd.Function):
              ptr(gsum), stream())
         ctx.save_for_backward(x, weight, y, ss, gamma)
         ctx.plan = plan
-        ctx.x_bn = getattr(x, "_milnce_bn", None)  # (y, ss) of the BN layer that produced x
-        z._milnce_bn = (y, ss)
+        ctx.x_bn = getattr(x, "_milnce_bn", None)  # (y, ss, ld) of the BN layer that produced x
+        z._milnce_bn = (y, ss, C)
         if gsum is None:
             return z
         ctx.mark_non_differentiable(gsum)
@@ -246,7 +247,7 @@ class _ConvBNReLU(torch.autograd.Function):
         dbeta = torch.empty((C,), dtype=F32, device=dev)
         dy = torch.empty_like(y)
         call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
-             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), stream())
+             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, stream())
         dx = None
         if ctx.needs_input_grad[0]:
             wd = _pack(weight, plan, 1)
@@ -263,6 +264,115 @@ def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool
     out = _ConvBNReLU.apply(x, weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
                             tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum))
     return out
+
+
+class _Conv1x1GroupBNReLU(torch.autograd.Function):
+    """Several 1x1x1 conv -> BN -> ReLU units that read the same input (Inception branches
+    0, 1a and 2a, ``s3dg.py:13-18``) as ONE implicit GEMM with the output channels
+    concatenated: the input is read once, the small branch widths (16/24/32/48) stop wasting
+    most of an N tile, and the backward is one dgrad GEMM (no per-branch dX sums) and one wgrad.
+    Each branch keeps its own BatchNorm (statistics are per channel, so slicing the fused
+    output is exact). Returns the branch outputs, plus the gating sum of the first one."""
+
+    @staticmethod
+    def forward(ctx, x, n, training, want_gsum0, hyper, *args):
+        ws = args[:n]
+        bns = [args[n + 5 * i: n + 5 * i + 5] for i in range(n)]  # gamma, beta, rmean, rvar, nbt
+        widths = [int(w.shape[0]) for w in ws]
+        ctot = sum(widths)
+        wcat = torch.cat([w.detach() for w in ws], 0)
+        plan = conv_plan(x.shape, wcat.shape, (1, 1, 1), (0, 0, 0))
+        dev = x.device
+        wp = _pack(wcat, plan, 0)
+        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+        y = conv_forward_raw(x, wp, plan, stats)
+        thw = plan.To * plan.Ho * plan.Wo
+        zs, sss, gsum = [], [], None
+        off = 0
+        y2 = y.view(-1, ctot)
+        for i, (c, (gamma, beta, rmean, rvar, nbt)) in enumerate(zip(widths, bns)):
+            ss = torch.empty((4 * c,), dtype=F32, device=dev)
+            st = stats[off:] if training else None
+            call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
+                 ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
+                 float(hyper[i][1]), int(training), ptr(ss), stream())
+            z = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev)
+            g = torch.zeros((plan.B, c), dtype=F32, device=dev) if (i == 0 and want_gsum0) else None
+            ysl = y2[:, off:off + c]
+            call("milnce_bn_relu_apply", ptr(ysl), ctot, ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g), stream())
+            z._milnce_bn = (ysl, ss, ctot)
+            zs.append(z)
+            sss.append(ss)
+            if g is not None:
+                gsum = g
+            off += c
+        ctx.save_for_backward(x, wcat, y, *sss, *[b[0] for b in bns])
+        ctx.plan, ctx.widths, ctx.n = plan, widths, n
+        ctx.x_bn = getattr(x, "_milnce_bn", None)
+        if gsum is not None:
+            ctx.mark_non_differentiable(gsum)
+            return (*zs, gsum)
+        return tuple(zs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        n, widths, plan = ctx.n, ctx.widths, ctx.plan
+        saved = ctx.saved_tensors
+        x, wcat, y = saved[:3]
+        sss = saved[3:3 + n]
+        gammas = saved[3 + n:3 + 2 * n]
+        ctot = sum(widths)
+        dev = y.device
+        dY = torch.empty((plan.M, ctot), dtype=BF16, device=dev)
+        y2 = y.view(-1, ctot)
+        dgs, dbs = [], []
+        off = 0
+        for i, c in enumerate(widths):
+            dz = grads[i]
+            if dz is None:
+                dz = torch.zeros((plan.M, c), dtype=BF16, device=dev)
+            dz = dz.contiguous()
+            fused = take_bn_partials(dz)
+            if fused is not None:
+                part, nparts, ps = fused
+            else:
+                nparts = _bn_nparts(plan.M)
+                part = torch.empty((nparts * 2 * c,), dtype=F32, device=dev)
+                ps = c
+            coef = torch.empty((3 * c,), dtype=F32, device=dev)
+            dgamma = torch.empty((c,), dtype=F32, device=dev)
+            dbeta = torch.empty((c,), dtype=F32, device=dev)
+            call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
+                 ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
+                 ptr(dY[:, off:]), ctot, stream())
+            dgs.append(dgamma)
+            dbs.append(dbeta)
+            off += c
+        dYv = dY.view(plan.B, plan.To, plan.Ho, plan.Wo, ctot)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = conv_dgrad(dYv, _pack(wcat, plan, 1), plan, ctx.x_bn)
+        dwcat = conv_wgrad(dYv, x, plan)
+        dws, off = [], 0
+        for c in widths:
+            dws.append(dwcat[off:off + c])
+            off += c
+        bn_grads = []
+        for dg, db in zip(dgs, dbs):
+            bn_grads += [dg, db, None, None, None]
+        return (dx, None, None, None, None, *dws, *bn_grads)
+
+
+def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = False):
+    """Fused 1x1x1 conv-BN-ReLU units sharing input x; see ``_Conv1x1GroupBNReLU``."""
+    if x.dtype != BF16:
+        x = x.to(BF16)
+    x = x.contiguous()
+    args = list(weights)
+    for bn in bns:
+        args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
+    return _Conv1x1GroupBNReLU.apply(x, len(weights), bool(training), bool(want_gsum0), hyper, *args)
 
 
 # =========================================================================================
@@ -321,13 +431,13 @@ class _GateConcat(torch.autograd.Function):
             dmean[:, off:off + c].copy_(dp.mm(w))
             off += c
         have_bn = all(zb is not None for zb in ctx.z_bn)
-        rows = B * ctx.thw
-        nparts = int(max(1, min(2048, _ceil(rows, 64))))
+        nparts = B * int(max(1, min(_ceil(2048, B), _ceil(ctx.thw, 128))))
         part = torch.empty((nparts * 2 * ctot,), dtype=F32, device=dev) if have_bn else None
         call("milnce_gate_bwd_apply", nseg, widths, _arr(ctypes.c_void_p, [ptr(d) for d in dzs]), ptr(dout),
              ptr(g), ptr(dmean), B, ctx.thw,
              _arr(ctypes.c_void_p, [ptr(zb[0]) for zb in ctx.z_bn]) if have_bn else None,
              _arr(ctypes.c_void_p, [ptr(zb[1]) for zb in ctx.z_bn]) if have_bn else None,
+             _arr(ctypes.c_int, [int(zb[2]) for zb in ctx.z_bn]) if have_bn else None,
              ptr(part), nparts, stream())
         if have_bn:
             off = 0
@@ -356,6 +466,9 @@ def _pool_out(n: int, k: int, s: int, p0: int, p1: int) -> int:
     return o
 
 
+_POOL_SPECIAL = {((1, 3, 3), (1, 2, 2)), ((3, 3, 3), (2, 2, 2)), ((2, 2, 2), (2, 2, 2))}
+
+
 class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, kernel, stride, tf_same):
@@ -377,7 +490,8 @@ class _MaxPool(torch.autograd.Function):
         ctx.save_for_backward(arg)
         ctx.geo = geo
         xb = getattr(x, "_milnce_bn", None)
-        ctx.x_bn = xb if (xb is not None and 256 % (C // 8) == 0) else None
+        special = (tuple(kernel), tuple(stride)) in _POOL_SPECIAL  # csrc/pool.hip MILNCE_POOL_SHAPES
+        ctx.x_bn = xb if (xb is not None and (special or (256 % (C // 8) == 0 and xb[2] == C))) else None
         return y
 
     @staticmethod
@@ -386,12 +500,12 @@ class _MaxPool(torch.autograd.Function):
         geo = ctx.geo
         B, T, H, W, C = geo[:5]
         dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dy.device)
-        nparts = int(max(1, min(4096, _ceil(B * T * H * W * (C // 8), 256))))
+        nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
         xb = ctx.x_bn
         part = torch.empty((nparts * 2 * C,), dtype=F32, device=dy.device) if xb is not None else None
         call("milnce_maxpool_bwd", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo,
-             ptr(xb[0]) if xb is not None else None, ptr(xb[1]) if xb is not None else None, ptr(part), nparts,
-             stream())
+             ptr(xb[0]) if xb is not None else None, int(xb[2]) if xb is not None else 0,
+             ptr(xb[1]) if xb is not None else None, ptr(part), nparts, stream())
         if part is not None:
             attach_bn_partials(dx, part, nparts, C)
         return dx, None, None, None

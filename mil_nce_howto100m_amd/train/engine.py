@@ -28,6 +28,7 @@ from ..losses import build_loss
 from ..models import S3D
 from ..parallel import dist as pdist
 from ..parallel.ddp import BufferBroadcaster, GradBucketer, broadcast_parameters
+from ..utils import StepTimer, Watchdog
 from . import checkpoint as ckpt
 from .logging import MetricsLogger, log, train_line
 from .optim import FlatAdam, FlatSGD, cosine_schedule_with_warmup
@@ -73,14 +74,21 @@ class Trainer:
                                                      steps_per_epoch * args.epochs)
         self.criterion = build_loss(args)
         self.global_step = 0
+        self.timer = StepTimer(bool(getattr(args, "phase_timers", 0)), self.device)
 
     # ---------------------------------------------------------------------------------
     def forward_loss(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
         video = batch["video"]
         text = batch["text"]
         text = text.reshape(-1, text.shape[-1])
-        video_embd, text_embd = self.model(video, text)
-        video_embd, text_embd = pdist.all_gather_embeddings(video_embd, text_embd, self.ctx)
+        with self.timer.phase("forward"):
+            video_embd, text_embd = self.model(video, text)
+        with self.timer.phase("all_gather"):
+            video_embd, text_embd = pdist.all_gather_embeddings(video_embd, text_embd, self.ctx)
+        with self.timer.phase("loss"):
+            return self._loss(batch, video_embd, text_embd)
+
+    def _loss(self, batch, video_embd, text_embd) -> torch.Tensor:
         name = getattr(self.args, "loss", "milnce")
         if name == "milnce":
             return self.criterion(video_embd, text_embd)
@@ -99,22 +107,33 @@ class Trainer:
         return sum(out) if isinstance(out, tuple) else out
 
     def train_step(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
+        fault = getattr(self.args, "fault_at_step", -1)
+        if fault >= 0 and self.global_step == fault:
+            raise RuntimeError(f"injected fault at step {fault} (--fault_at_step)")
         self.model.train()
         self.bucketer.zero()
         if self.buffers is not None:
-            self.buffers()
+            with self.timer.phase("broadcast_buffers"):
+                self.buffers()
         loss = self.forward_loss(batch)
-        loss.backward()
-        self.bucketer.finish()
-        self.optimizer.step()
-        self.scheduler.step()
+        with self.timer.phase("backward"):
+            loss.backward()
+        with self.timer.phase("allreduce_wait"):
+            self.bucketer.finish()
+        with self.timer.phase("optimizer"):
+            self.optimizer.step()
+            self.scheduler.step()
         self.global_step += 1
         return loss.detach()
 
     # ---------------------------------------------------------------------------------
-    def state(self, epoch: int) -> dict:
-        return {"epoch": epoch, "state_dict": ckpt.model_state_dict(self.model),
-                "optimizer": self.optimizer.state_dict(), "scheduler": self.scheduler.state_dict()}
+    def state(self, epoch: int, step_in_epoch: int = 0) -> dict:
+        """Reference checkpoint dict; a mid-epoch checkpoint adds ``step_in_epoch``."""
+        st = {"epoch": epoch, "state_dict": ckpt.model_state_dict(self.model),
+              "optimizer": self.optimizer.state_dict(), "scheduler": self.scheduler.state_dict()}
+        if step_in_epoch:
+            st["step_in_epoch"] = step_in_epoch
+        return st
 
     def load_state(self, state: dict) -> int:
         ckpt.load_model_weights(self.model, state["state_dict"], strict=True)
@@ -152,23 +171,30 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
         os.makedirs(cdir, exist_ok=True)
     pdist.barrier()
     start_epoch = args.start_epoch
+    start_step = 0
     if args.resume:
         path = ckpt.get_last_checkpoint(cdir)
         if path:
             log("=> loading checkpoint '{}'".format(path), args, ctx.rank)
-            start_epoch = trainer.load_state(ckpt.load_checkpoint(path, map_location=ctx.device))
+            state = ckpt.load_checkpoint(path, map_location=ctx.device)
+            start_epoch = trainer.load_state(state)
+            start_step = int(state.get("step_in_epoch", 0))
             log("=> loaded checkpoint '{}' (epoch {})".format(path, start_epoch), args, ctx.rank)
         else:
             log("=> no checkpoint found at '{}'".format(cdir), args, ctx.rank)
     total_bs = local_bs * ctx.world_size
     log("Starting training loop for rank: {}, total batch size: {}".format(ctx.rank, total_bs), args, ctx.rank)
     last = {}
+    watchdog = Watchdog(getattr(args, "watchdog_s", 0.0), ctx.rank,
+                        dump_dir=getattr(args, "log_root", "log") or "log").start()
     for epoch in range(start_epoch, args.epochs):
         running = torch.zeros((), device=ctx.device)
         t0 = time.time()
-        for i in range(steps_per_epoch):
+        first = start_step if epoch == start_epoch else 0
+        for i in range(first, steps_per_epoch):
             batch = data.batch(epoch * steps_per_epoch + i)
             running += trainer.train_step(batch)
+            watchdog.beat(trainer.global_step)
             if (i + 1) % args.n_display == 0:
                 avg = float(running.item()) / args.n_display  # the only host sync
                 d = time.time() - t0
@@ -176,15 +202,22 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
                 if args.verbose:
                     log(train_line(epoch + 1, d, total_bs * float(i) / max(1, data.epoch_len), avg, lr), args, ctx.rank)
                 metrics.write(epoch=epoch + 1, step=trainer.global_step, loss=avg, lr=lr,
-                              pairs_per_s=total_bs * args.n_display / max(d, 1e-9))
+                              pairs_per_s=total_bs * args.n_display / max(d, 1e-9),
+                              phase_ms=trainer.timer.summary())
                 last = {"loss": avg, "lr": lr}
                 running.zero_()
                 t0 = time.time()
-            if args.ckpt_every_steps and trainer.global_step % args.ckpt_every_steps == 0 and ctx.is_main:
-                ckpt.save_checkpoint(trainer.state(epoch), cdir, epoch)
+            if (args.ckpt_every_steps and trainer.global_step % args.ckpt_every_steps == 0
+                    and i + 1 < steps_per_epoch):
+                # mid-epoch checkpoint: same file family (epoch%04d of the epoch in progress),
+                # plus step_in_epoch so --resume continues from the next step
+                if ctx.is_main:
+                    ckpt.save_checkpoint(trainer.state(epoch, i + 1), cdir, epoch)
+                pdist.barrier()
         if ctx.is_main:
             ckpt.save_checkpoint(trainer.state(epoch + 1), cdir, epoch + 1)
         pdist.barrier()
         if getattr(args, "stop_epoch", 0) and epoch + 1 >= args.stop_epoch:
             break
+    watchdog.stop()
     return last

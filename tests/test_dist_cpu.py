@@ -146,3 +146,59 @@ def test_checkpoint_resume_equivalence():
         assert sa.keys() == sb.keys()
         for k in sa:
             assert torch.allclose(sa[k]["exp_avg"], sb[k]["exp_avg"], atol=1e-7)
+
+
+def _worker_fault(rank, world, port, ckdir, extra):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.train.engine import run_training
+    args = _args(["--checkpoint_root", ckdir, "--checkpoint_dir", "run", "--epochs", "2",
+                  "--steps_per_epoch", "3", "--n_display", "1", "--verbose", "0", "--log_root", ckdir, *extra])
+    args.rank, args.world_size = ctx.rank, ctx.world_size
+    try:
+        run_training(args, ctx)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_fault_injection_mid_epoch_resume():
+    """Kill both ranks mid-epoch (injected fault), --resume from the step checkpoint, and land on
+    exactly the state of an uninterrupted run."""
+    from mil_nce_howto100m_amd.train import checkpoint as ck
+    world = 2
+    with tempfile.TemporaryDirectory() as d1, tempfile.TemporaryDirectory() as d2:
+        mp.spawn(_worker_fault, args=(world, _port(), d1, []), nprocs=world)
+        with pytest.raises(Exception):
+            mp.spawn(_worker_fault, args=(world, _port(), d2, ["--ckpt_every_steps", "1", "--fault_at_step", "5"]),
+                     nprocs=world)
+        mid = ck.load_checkpoint(ck.get_last_checkpoint(os.path.join(d2, "run")))
+        assert mid["epoch"] == 1 and mid["step_in_epoch"] == 2  # global step 5 = epoch 1, step 2
+        mp.spawn(_worker_fault, args=(world, _port(), d2, ["--resume"]), nprocs=world)
+        a = ck.load_checkpoint(os.path.join(d1, "run", "epoch0002.pth.tar"))
+        b = ck.load_checkpoint(os.path.join(d2, "run", "epoch0002.pth.tar"))
+        assert a["scheduler"]["last_epoch"] == b["scheduler"]["last_epoch"] == 6
+        for k in a["state_dict"]:
+            assert torch.allclose(a["state_dict"][k].float(), b["state_dict"][k].float(), atol=1e-6), k
+
+
+def test_watchdog_fires_without_progress():
+    import time
+    from mil_nce_howto100m_amd.utils import Watchdog
+    with tempfile.TemporaryDirectory() as d:
+        wd = Watchdog(0.3, rank=0, dump_dir=d, abort=False, poll_s=0.05).start()
+        for _ in range(8):  # steady progress: silent
+            time.sleep(0.1)
+            wd.beat(1)
+        assert not wd.fired.is_set()
+        assert wd.fired.wait(3.0)
+        wd.stop()
+        assert "no training progress" in open(os.path.join(d, "watchdog_rank0.txt")).read()
+
+
+def test_phase_timers_cpu():
+    from mil_nce_howto100m_amd.utils import StepTimer
+    t = StepTimer(True, torch.device("cpu"))
+    for _ in range(3):
+        with t.phase("forward"):
+            sum(range(1000))
+    s = t.summary()
+    assert set(s) == {"forward"} and s["forward"] >= 0.0

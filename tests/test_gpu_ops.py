@@ -132,6 +132,43 @@ def test_conv_bn_relu_train(cin, cout, k, p, gsum):
     assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("widths", [(64, 96, 16), (160, 112, 24)])
+def test_conv1x1_group_matches_separate_units(widths):
+    """Fused Inception 1x1x1 branches (one GEMM, per-branch BN) vs an fp32 reference per branch."""
+    torch.manual_seed(5)
+    h = hip()
+    B, T, H, W, cin = 3, 4, 7, 7, 192
+    x = torch.randn(B, T, H, W, cin, device=DEV).to(torch.bfloat16)
+    convs = [nn.Conv3d(cin, c, 1, bias=False).to(DEV) for c in widths]
+    bns = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+    with torch.no_grad():
+        for bn in bns:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    refs = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+    for r, bn in zip(refs, bns):
+        r.load_state_dict(bn.state_dict())
+    xh = x.clone().requires_grad_(True)
+    out = h.conv1x1_group_bn_relu(xh, [c.weight for c in convs], bns, True, True)
+    zs, gsum = out[:3], out[3]
+    xr = x.float().requires_grad_(True)
+    wrs = [c.weight.detach().to(torch.bfloat16).float().requires_grad_(True) for c in convs]
+    zrs = [aten.conv_bn_relu(xr, w, r, (1, 1, 1), (0, 0, 0), True) for w, r in zip(wrs, refs)]
+    for z, zr in zip(zs, zrs):
+        assert rel_err(z, zr) < 2e-2
+    assert rel_err(gsum, zrs[0].sum(dim=(1, 2, 3))) < 2e-2
+    dzs = [torch.randn_like(zr) for zr in zrs]
+    torch.autograd.backward(list(zs), [d.to(torch.bfloat16) for d in dzs])
+    torch.autograd.backward(zrs, dzs)
+    assert rel_err(xh.grad, xr.grad) < 3e-2
+    for c, w, bn, r in zip(convs, wrs, bns, refs):
+        assert rel_err(c.weight.grad, w.grad) < 3e-2
+        assert rel_err(bn.weight.grad, r.weight.grad) < 3e-2
+        assert rel_err(bn.bias.grad, r.bias.grad) < 3e-2
+        assert torch.allclose(bn.running_mean, r.running_mean, rtol=2e-2, atol=2e-3)
+        assert torch.allclose(bn.running_var, r.running_var, rtol=2e-2, atol=2e-3)
+
+
 @pytest.mark.parametrize("kernel,stride,tf", [((1, 3, 3), (1, 2, 2), True), ((3, 3, 3), (2, 2, 2), True),
                                               ((2, 2, 2), (2, 2, 2), True), ((3, 3, 3), (1, 1, 1), False)])
 def test_maxpool(kernel, stride, tf):
