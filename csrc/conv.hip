@@ -395,6 +395,304 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// v3 forward / dgrad (bf16 input): both operand tiles are fetched global -> LDS directly by
+// buffer_load ... lds (LDS-DMA: no staging VGPRs, no ds_write pass) into a STAGES-deep ring, with
+// the tile for k-step kt + STAGES - 1 in flight while kt is computed; a counted vmcnt + raw
+// s_barrier retire one stage per k-step (a __syncthreads() would drain every DMA in flight).
+// The LDS image stays XOR-swizzled: a DMA writes lane-linearly, so each lane instead fetches the
+// source chunk that belongs in its slot. Wave w's j-th DMA of a tile covers rows
+// j*4*RPI + w*RPI + lane/CPR, so the swizzle term -- and hence the lane's k chunk and its
+// (tap, channel) -- is the same for all of the lane's rows: one tap lookup per stage.
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  // n is one of a few compile-time values at every call site (see the callers)
+  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if (n <= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if (n <= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n <= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n <= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (n <= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int BN, int BK, int STAGES, int EPI>
+__global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
+  constexpr int BM = 128;
+  constexpr int CPR = BK / 8;              // 16-B chunks per tile row
+  constexpr int RPI = 64 / CPR;            // rows per DMA instruction (1 KiB)
+  constexpr int A_INST = BM / RPI / 4;     // DMA instructions per wave per stage (A)
+  constexpr int B_INST = BN / RPI / 4;     // (B)
+  constexpr int NDMA = A_INST + B_INST;
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int KSTEPS = BK / 32;
+  constexpr int LDE = BN + 8;
+  constexpr int STAGE_ELEMS = (BM + BN) * BK;
+  constexpr int RING_BYTES = STAGES * STAGE_ELEMS * 2;
+  constexpr int EPI_BYTES = BM * LDE * 2;
+  constexpr int TAB_OFF_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  static_assert(A_INST >= 1 && B_INST >= 1, "tile too small for the DMA mapping");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* ring = (bf16_t*)smem;  // stage s: A [BM][BK] then B [BN][BK]
+  bf16_t* Es = (bf16_t*)smem;    // epilogue staging [BM][LDE] (after the ring drained)
+  int2* tab = (int2*)(smem + TAB_OFF_BYTES);
+  float* ssl = (float*)(smem + TAB_OFF_BYTES + 8 * 160);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases go to M0
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nblocks = p.num_n_tiles * p.grid_m;
+  const int logical = xcd_remap(blockIdx.x, nblocks);
+  const int n_tile = logical % p.num_n_tiles;
+  const int m_slot = logical / p.num_n_tiles;
+  const int n0 = n_tile * BN;
+  const int nk = p.Kpad / BK;
+  const int taps = p.KT * p.KH * p.KW;
+  const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
+  const uint32_t clip_bytes = (uint32_t)(p.x_bstride * 2);
+
+  // this lane's DMA slot and the (row-invariant) source chunk
+  const int slot = lane % CPR;
+  const int lrow = wave * RPI + lane / CPR;  // row of instruction j: j * 4 * RPI + lrow
+  const int src_chunk = swz<BK>(lrow, slot);
+
+  build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
+  if constexpr (EPI == 2) {
+    for (int t = tid; t < 4 * BN; t += 256) {
+      const int q = t / BN, c = n0 + (t - q * BN);
+      ssl[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
+    }
+  }
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long long)p.num_n_tiles * BN * p.Kpad * 2),
+                                                     0x00020000);
+  float st_s[TN][4], st_q[TN][4];
+  float e_s[8], e_q[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { st_s[j][r] = 0.f; st_q[j][r] = 0.f; }
+
+  for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
+    const int m0 = m_tile * BM;
+    const uint32_t b0 = (uint32_t)m0 / thw;
+    const char* base = (const char*)p.x + (long long)b0 * p.x_bstride * 2;
+    const long long remain = p.x_total_bytes - (long long)b0 * p.x_bstride * 2;
+    const uint32_t nrec = remain > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)remain;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nrec, 0x00020000);
+
+    int rt[A_INST], rh[A_INST], rw[A_INST];
+    uint32_t rowoff[A_INST];
+#pragma unroll
+    for (int i = 0; i < A_INST; ++i) {
+      const int m = m0 + i * 4 * RPI + lrow;
+      if (m < p.M) {
+        uint32_t q = fdiv((uint32_t)m, p.fWo);
+        const int wo = m - q * p.Wo;
+        uint32_t q2 = fdiv(q, p.fHo);
+        const int ho = q - q2 * p.Ho;
+        uint32_t b = fdiv(q2, p.fTo);
+        const int to = q2 - b * p.To;
+        rt[i] = to * p.st - p.pt;
+        rh[i] = ho * p.sh - p.ph;
+        rw[i] = wo * p.sw - p.pw;
+        rowoff[i] = (b - b0) * clip_bytes + (uint32_t)(((rt[i] * p.H + rh[i]) * p.W + rw[i]) * p.Cin * 2);
+      } else {
+        rt[i] = -(1 << 28);
+        rh[i] = 0;
+        rw[i] = 0;
+        rowoff[i] = 0;
+      }
+    }
+
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+    __syncthreads();  // tap table ready; previous tile's epilogue done with the LDS
+
+    auto issue = [&](int kt) {
+      bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
+      bf16_t* sb = sa + BM * BK;
+      const int k = kt * BK + src_chunk * 8;
+      const int tap = (int)fdiv((uint32_t)k, p.fCin);
+      const int c = k - tap * p.Cin;
+      const bool kval = tap < taps;
+      const int2 te = tab[min(tap, taps - 1)];
+      const int dt = te.y & 0xff, dh = (te.y >> 8) & 0xff, dw = te.y >> 16;
+      const uint32_t koff = (uint32_t)((te.x + c) * 2);
+#pragma unroll
+      for (int i = 0; i < A_INST; ++i) {
+        const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
+        const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+                       ((unsigned)wi < (unsigned)p.W);
+        const uint32_t off = v ? rowoff[i] + koff : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * 4 * RPI + wave * RPI) * BK), 16, off,
+                                                 0, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < B_INST; ++i) {
+        const int n = n0 + i * 4 * RPI + lrow;
+        const uint32_t off = (uint32_t)(((long long)n * p.Kpad + kt * BK + src_chunk * 8) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * 4 * RPI + wave * RPI) * BK), 16, off,
+                                                 0, 0, 0);
+      }
+    };
+
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nk) issue(s);
+
+    for (int kt = 0; kt < nk; ++kt) {
+      // stage kt must have landed: later stages (issued: min(nk-1, kt+STAGES-2) - kt of them) may stay in flight
+      const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
+      wait_vmcnt_le(ahead * NDMA);
+      __builtin_amdgcn_s_barrier();
+      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+      const bf16_t* a = ring + (kt % STAGES) * STAGE_ELEMS;
+      const bf16_t* bsh = a + BM * BK;
+#pragma unroll
+      for (int s = 0; s < KSTEPS; ++s) {
+        bf16x8 xf[TM], wf[TN];
+        const int chunk = s * 4 + (lane >> 4);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wr * WM + i * 16 + (lane & 15);
+          xf[i] = *(const bf16x8*)(a + row * BK + swz<BK>(row, chunk) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wc * WN + j * 16 + (lane & 15);
+          wf[j] = *(const bf16x8*)(bsh + row * BK + swz<BK>(row, chunk) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave done reading the ring before the epilogue reuses it
+
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wr * WM + i * 16 + (lane & 15);
+      const bool rv = (m0 + row) < p.M;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const f32x4 v = acc[j][i];
+        if constexpr (EPI == 1) {
+          if (rv) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              st_s[j][r] += v[r];
+              st_q[j][r] += v[r] * v[r];
+            }
+          }
+        }
+        uint2 o;
+        o.x = pack2bf(v[0], v[1]);
+        o.y = pack2bf(v[2], v[3]);
+        const int col = wc * WN + j * 16 + (lane >> 4) * 4;
+        *(uint2*)(Es + row * LDE + col) = o;
+      }
+    }
+    __syncthreads();
+    constexpr int OCPR = BN / 8;
+#pragma unroll
+    for (int it = 0; it < BM * OCPR / 256; ++it) {
+      const int cid = tid + it * 256;
+      const int row = cid / OCPR, cc = cid % OCPR;
+      const int m = m0 + row, n = n0 + cc * 8;
+      const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
+      const bool ok = (m < p.M) & (n < p.Cout);
+      if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
+      if constexpr (EPI == 2) {
+        if (ok) {
+          float d8[8], y8[8];
+          unpack8(dv, d8);
+          unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int cl = cc * 8 + k;
+            const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
+            e_s[k] += gm;
+            e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
+          }
+        }
+      }
+    }
+  }
+
+  if constexpr (EPI == 2) {
+    constexpr int OCPR = BN / 8;
+    __syncthreads();
+    float* red = (float*)smem;  // [2][8][256]
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[k * 256 + tid] = e_s[k]; red[(8 + k) * 256 + tid] = e_q[k]; }
+    __syncthreads();
+    if (tid < OCPR) {
+      const int npad = p.num_n_tiles * BN;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int j = tid; j < 256; j += OCPR) { s1 += red[k * 256 + j]; s2 += red[(8 + k) * 256 + j]; }
+        const int col = n0 + tid * 8 + k;
+        p.stats[(long long)m_slot * 2 * npad + col] = s1;
+        p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
+      }
+    }
+  }
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = st_s[j][r], q = st_q[j][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        st_s[j][r] = s;
+        st_q[j][r] = q;
+      }
+    __syncthreads();
+    float* red = (float*)smem;  // [2 (wc)][2 (s,q)][WN]
+    if (wr == 1 && (lane & 15) == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + (lane >> 4) * 4 + r;
+          red[(wc * 2 + 0) * WN + c] = st_s[j][r];
+          red[(wc * 2 + 1) * WN + c] = st_q[j][r];
+        }
+    }
+    __syncthreads();
+    if (wr == 0 && (lane & 15) == 0) {
+      const int npad = p.num_n_tiles * BN;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = j * 16 + (lane >> 4) * 4 + r;
+          const int col = n0 + wc * WN + c;
+          p.stats[(long long)m_slot * 2 * npad + col] = st_s[j][r] + red[(wc * 2 + 0) * WN + c];
+          p.stats[(long long)m_slot * 2 * npad + npad + col] = st_q[j][r] + red[(wc * 2 + 1) * WN + c];
+        }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // wgrad: dW[n, k] partial over an m-range -> slab[split][Npad][Kpad] (fp32)
 struct WgradParams {
   const bf16_t* dy;    // [M, ldd] bf16
@@ -413,13 +711,37 @@ struct WgradParams {
 };
 
 constexpr int WG_R = 64;  // reduction rows (m) per LDS stage = two 32-deep MFMA k-steps
+constexpr int WG_R_MAX = 64;
 
-// Stage this thread's chunks of dY rows [mb, mb+64) and of the im2col X rows.
+// Per-stage row table (one decomposition per row instead of one per row and chunk column):
+// .x = element offset of the row's unshifted input origin relative to the split's first clip,
+// .y = (rt + 64) | (rh + 64) << 10 | (rw + 64) << 20 (rows past m_end: all fields 0 -> invalid).
+__device__ __forceinline__ void wgrad_row_table(int2* tab, const WgradParams& p, int mb, int m_end, uint32_t b_first,
+                                                int tid) {
+  if (tid < WG_R_MAX) {
+    const int m = mb + tid;
+    int2 e = make_int2(0, 0);
+    if (m < m_end) {
+      const uint32_t q = fdiv((uint32_t)m, p.fWo);
+      const int wo = m - q * p.Wo;
+      const uint32_t q2 = fdiv(q, p.fHo);
+      const int ho = q - q2 * p.Ho;
+      const uint32_t b = fdiv(q2, p.fTo);
+      const int to = q2 - b * p.To;
+      const int rt = to * p.st - p.pt, rh = ho * p.sh - p.ph, rw = wo * p.sw - p.pw;
+      e.x = (int)((long long)(b - b_first) * p.x_bstride + ((long long)(rt * p.H + rh) * p.W + rw) * p.Cin);
+      e.y = (rt + 64) | ((rh + 64) << 10) | ((rw + 64) << 20);
+    }
+    tab[tid] = e;
+  }
+}
+
+// Stage this thread's chunks of dY rows [mb, mb+R) and of the im2col X rows.
 template <int DCH, int XCH, int DCPR, int XCPR, int VEC, int ESZ, bool U8, typename XReg>
 __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH], __amdgpu_buffer_rsrc_t drs,
-                                           __amdgpu_buffer_rsrc_t xrs, const WgradParams& p, int mb, int m_end,
-                                           int m_base, uint32_t b_first, int tid, int n0, int d_ccol, bool kval,
-                                           int dt, int dh, int dw, int c) {
+                                           __amdgpu_buffer_rsrc_t xrs, const WgradParams& p, const int2* tab,
+                                           int mb, int m_end, int m_base, int tid, int n0, int d_ccol, bool kval,
+                                           int dt, int dh, int dw, int tapoff) {
 #pragma unroll
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
@@ -432,18 +754,11 @@ __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH]
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
     const int row = (tid + i * 256) / XCPR;
-    const int m = mb + row;
-    const uint32_t q = fdiv((uint32_t)m, p.fWo);
-    const int wo = m - q * p.Wo;
-    const uint32_t q2 = fdiv(q, p.fHo);
-    const int ho = q - q2 * p.Ho;
-    const uint32_t b = fdiv(q2, p.fTo);
-    const int to = q2 - b * p.To;
-    const int ti = to * p.st - p.pt + dt, hi = ho * p.sh - p.ph + dh, wi = wo * p.sw - p.pw + dw;
-    const bool v = kval & (m < m_end) & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+    const int2 e = tab[row];
+    const int ti = (e.y & 1023) - 64 + dt, hi = ((e.y >> 10) & 1023) - 64 + dh, wi = (e.y >> 20) - 64 + dw;
+    const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                    ((unsigned)wi < (unsigned)p.W);
-    const long long e = (long long)(b - b_first) * p.x_bstride + ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c;
-    const uint32_t off = v ? (uint32_t)(e * ESZ) : 0x80000000u;
+    const uint32_t off = v ? (uint32_t)((e.x + tapoff) * ESZ) : 0x80000000u;
     if constexpr (U8) {
       xreg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0);
     } else {
@@ -502,13 +817,17 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ds = (bf16_t*)smem;               // [2][R][LDN]
   bf16_t* Xs = Ds + 2 * R * LDN;            // [2][R][LDK]
+  int2* rtab = (int2*)(Xs + 2 * R * LDK);   // [2][R] row tables
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  const int nblocks = p.n_tiles * p.k_tiles * p.splits;
+  const int ntiles = p.n_tiles * p.k_tiles;
+  const int nblocks = ntiles * p.splits;
+  // split-major order: an XCD's contiguous logical range covers every tile of a few m-splits,
+  // so the dY / X rows of a split are fetched once into that XCD's L2 and reused by all tiles.
   const int logical = xcd_remap(blockIdx.x, nblocks);
-  const int tile = logical / p.splits;
-  const int split = logical % p.splits;
+  const int split = logical / ntiles;
+  const int tile = logical % ntiles;
   const int n0 = (tile % p.n_tiles) * TN_;
   const int k0 = (tile / p.n_tiles) * TK_;
   const int m_begin = split * p.rows_per_split;
@@ -523,6 +842,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const int dw = tap % p.KW;
   const int dh = (tap / p.KW) % p.KH;
   const int dt = tap / (p.KW * p.KH);
+  const int tapoff = ((dt * p.H + dh) * p.W + dw) * p.Cin + c;
   const int d_ccol = tid % DCPR;
 
   // Descriptors based at this split's first row / first clip: offsets stay 32-bit whatever the
@@ -553,16 +873,21 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int nsteps = (m_end - m_begin + R - 1) / R;
   if (nsteps > 0) {
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin, m_end, m_clamped, b_first, tid,
-                                                    n0, d_ccol, kval, dt, dh, dw, c);
+    wgrad_row_table(rtab, p, m_begin, m_end, b_first, tid);
+    wgrad_row_table(rtab + R, p, m_begin + R, m_end, b_first, tid);
+    __syncthreads();
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
+                                                    n0, d_ccol, kval, dt, dh, dw, tapoff);
     wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
     const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, m_begin + sn * R, m_end, m_clamped,
-                                                    b_first, tid, n0, d_ccol, kval, dt, dh, dw, c);
+    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sn & 1) * R, m_begin + sn * R,
+                                                    m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+    // row table of stage s + 2 into the slot stage s used (its last reader was iteration s - 1)
+    if (s + 2 < nsteps) wgrad_row_table(rtab + buf * R, p, m_begin + (s + 2) * R, m_end, b_first, tid);
     const bf16_t* d = Ds + buf * R * LDN;
     const bf16_t* x = Xs + buf * R * LDK;
 #pragma unroll
@@ -666,8 +991,43 @@ static int launch_fwd_epi(ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+template <int BN, int BK, int STAGES, int EPI>
+static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
+  constexpr size_t ring = (size_t)STAGES * (128 + BN) * BK * 2;
+  constexpr size_t epi = (size_t)128 * (BN + 8) * 2;
+  const size_t lds = (ring > epi ? ring : epi) + 8 * 160 + 16 * BN;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v3_kernel<BN, BK, STAGES, EPI>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int nblocks = p.num_n_tiles * p.grid_m;
+  hipLaunchKernelGGL((conv_fwd_v3_kernel<BN, BK, STAGES, EPI>), dim3(nblocks), dim3(256), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+static int g_conv_impl = 3;  // 3: LDS-DMA ring (bf16 inputs); 2: register-staged kernel
+
+MILNCE_API int milnce_conv_set_impl(int impl) {
+  const int old = g_conv_impl;
+  g_conv_impl = impl;
+  return old;
+}
+
+template <int BN, int BK>
+static int launch_v3_epi(ConvParams& p, hipStream_t stream) {
+  constexpr int S = BK == 64 ? 3 : 4;  // ring <= 96 KiB (BN 128) or 72 KiB (BN 64)
+  if (p.bn_mode == 0) return launch_fwd_v3<BN, BK, S, 0>(p, stream);
+  if (p.bn_mode == 1) return launch_fwd_v3<BN, BK, S, 1>(p, stream);
+  return launch_fwd_v3<BN, BK, S, 2>(p, stream);
+}
+
 template <int BM, int BN, int BK, bool U8>
 static int launch_fwd(ConvParams& p, hipStream_t stream) {
+  if constexpr (!U8) {
+    if (g_conv_impl == 3) return launch_v3_epi<BN, BK>(p, stream);
+  }
   if constexpr (U8) {
     if (p.bn_mode == 0) return launch_fwd_epi<BM, BN, BK, true, 0>(p, stream);
     return p.bn_mode == 1 ? launch_fwd_epi<BM, BN, BK, true, 1>(p, stream) : (int)hipErrorInvalidValue;
@@ -684,7 +1044,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
                                const float* bn_ss, int bn_ld,
                                int B, int T, int H, int W, int Cin, int Cout,
                                int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
-                               int Kpad, int Npad, int ldy, int bn, int bk, int grid_m,
+                               int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
                                hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
@@ -695,7 +1055,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.T = T; p.H = H; p.W = W; p.Cin = Cin;
   p.To = (T + 2 * pt - KT) / st + 1;
   p.Ho = (H + 2 * ph - KH) / sh + 1;
-  p.Wo = (W + 2 * pw - KW) / sw + 1;
+  p.Wo = wo_override > 0 ? wo_override : (W + 2 * pw - KW) / sw + 1;  // override: asymmetric w padding
   p.Cout = Cout;
   p.KT = KT; p.KH = KH; p.KW = KW; p.st = st; p.sh = sh; p.sw = sw; p.pt = pt; p.ph = ph; p.pw = pw;
   p.Ktot = KT * KH * KW * Cin; p.Kpad = Kpad; p.ldy = ldy;
@@ -725,7 +1085,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 
 template <int TN_, int TK_, bool U8>
 static int launch_wgrad(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2;
+  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2 + 2 * WG_R * sizeof(int2);
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_kernel<TN_, TK_, U8>,
@@ -740,14 +1100,14 @@ static int launch_wgrad(WgradParams& p, hipStream_t stream) {
 MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u8, float* slab, float* dw,
                                  int B, int T, int H, int W, int Cin, int Cin_param, int Cout,
                                  int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
-                                 int Kpad, int Npad, int tn, int tk, int splits, int accumulate,
+                                 int Kpad, int Npad, int tn, int tk, int splits, int accumulate, int wo_override,
                                  hipStream_t stream) {
   WgradParams p;
   p.dy = (const bf16_t*)dy; p.x = x; p.slab = slab;
   p.T = T; p.H = H; p.W = W; p.Cin = Cin;
   p.To = (T + 2 * pt - KT) / st + 1;
   p.Ho = (H + 2 * ph - KH) / sh + 1;
-  p.Wo = (W + 2 * pw - KW) / sw + 1;
+  p.Wo = wo_override > 0 ? wo_override : (W + 2 * pw - KW) / sw + 1;
   p.Cout = Cout; p.ldd = ldd;
   p.KT = KT; p.KH = KH; p.KW = KW; p.st = st; p.sh = sh; p.sw = sw; p.pt = pt; p.ph = ph; p.pw = pw;
   p.Ktot = KT * KH * KW * Cin; p.Kpad = Kpad; p.Npad = Npad;

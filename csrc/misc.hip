@@ -93,8 +93,7 @@ MILNCE_API int milnce_synth_video(const int* labels, const int* ids, int B, int 
   return (int)hipGetLastError();
 }
 
-// [B,3,T,H,W] -> [B,T,H,W,4] uint8 (src_kind 0) or [B,T,H,W,8] bf16 (1: float32 in [0,1], 2: bf16;
-// 8 channels so the bf16 operand load stays 16-B wide; channels 3..7 are zero).
+// [B,3,T,H,W] -> [B,T,H,W,4] uint8 (src_kind 0) or bf16 (1: float32 in [0,1], 2: bf16); channel 3 is zero.
 __global__ void stem_prep_kernel(const void* __restrict__ src, int kind, int T, int H, int W, void* __restrict__ dst,
                                  long long npix) {
   const long long plane = (long long)T * H * W;
@@ -111,14 +110,37 @@ __global__ void stem_prep_kernel(const void* __restrict__ src, int kind, int T, 
       for (int c = 0; c < 3; ++c)
         f[c] = kind == 1 ? ((const float*)src)[(b * 3 + c) * plane + s]
                          : bf2f(((const bf16_t*)src)[(b * 3 + c) * plane + s]);
-      uint4 o;
+      uint2 o;
       o.x = pack2bf(f[0], f[1]);
       o.y = pack2bf(f[2], 0.f);
-      o.z = 0u;
-      o.w = 0u;
-      ((uint4*)dst)[i] = o;
+      ((uint2*)dst)[i] = o;
     }
   }
+}
+
+// uint8 [n] -> bf16 [n] * (1/255): the native clip [B,T,H,W,4] becomes the stem's bf16 operand,
+// read by the conv as width pairs [B,T,H,W/2,8] (see hip_ops.stem_conv_bn_relu). 8 B in, 16 B out.
+__global__ void u8_to_bf16_kernel(const uint2* __restrict__ src, uint4* __restrict__ dst, long long n8) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const uint2 v = src[i];
+    const float s = 1.0f / 255.0f;
+    float f[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[k] = (float)((v.x >> (8 * k)) & 0xff) * s;
+      f[4 + k] = (float)((v.y >> (8 * k)) & 0xff) * s;
+    }
+    dst[i] = pack8(f);
+  }
+}
+
+MILNCE_API int milnce_u8_to_bf16(const void* src, void* dst, long long n, hipStream_t stream) {
+  if (n % 8) return (int)hipErrorInvalidValue;
+  const long long n8 = n / 8;
+  long long grid = (n8 + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(u8_to_bf16_kernel, dim3((int)grid), dim3(256), 0, stream, (const uint2*)src, (uint4*)dst, n8);
+  return (int)hipGetLastError();
 }
 
 MILNCE_API int milnce_stem_prep(const void* src, int kind, int B, int T, int H, int W, void* dst, hipStream_t stream) {

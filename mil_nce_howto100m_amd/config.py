@@ -99,6 +99,9 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--stop_epoch", type=int, default=0,
                    help="end this run after this epoch (simulated interruption for resume tests)")
     g.add_argument("--hip_graph", type=int, default=0, help="capture the train step in a HIP graph")
+    g.add_argument("--grad_cache_chunks", type=int, default=0,
+                   help="GradCache-style step in this many micro-batches per GPU: exact global-negative "
+                        "MIL-NCE with bounded activation memory (BASELINE config 5); 0/1: off")
     g.add_argument("--watchdog_s", type=float, default=0.0,
                    help="abort a rank (exit 3, stacks dumped) after this many seconds without a finished step")
     g.add_argument("--phase_timers", type=int, default=0,

@@ -9,7 +9,8 @@ so checkpoints load in both directions. The *execution* is different:
     op; on GPU it is an MFMA implicit-GEMM conv whose epilogue emits BN partial statistics;
   * the four ``SelfGating`` modules of an Inception block and its ``th.cat`` (``s3dg.py:38-45``)
     are one op that writes each gated branch into its channel slice of the block output;
-  * the stem consumes uint8 clips directly (``/255`` is folded into the conv's operand load).
+  * the stem reads the clip as width pairs (8 channels), so its 3x7x7 stride-2 conv becomes an
+    ordinary 16-B-operand implicit GEMM (``ops.hip_ops.stem_conv_bn_relu``).
 
 "Separable" is the reference's full-channel (2+1)D factorisation — a ``1 x k x k`` conv
 followed by a ``k x 1 x 1`` conv, both Cin->Cout dense (``s3dg.py:74-99``), not depthwise.
@@ -198,7 +199,8 @@ class S3D(nn.Module):
 
         Accepted: reference float ``[B,3,T,H,W]`` in [0,1]; uint8 ``[B,3,T,H,W]`` (raw loader
         output); native uint8 ``[B,T,H,W,4]`` (RGB + zero pad channel, from the synthetic
-        generator). GPU stem input: uint8/bf16 ``[B,T,H,W,4]``; CPU: float ``[B,T,H,W,3]``.
+        generator). GPU stem input: bf16 ``[B,T,H,W,4]`` (channel 3 zero, read as width pairs by
+        the stem); CPU: float ``[B,T,H,W,3]``.
         """
         native = video.dim() == 5 and video.shape[-1] == 4 and video.shape[1] != 3
         if video.is_cuda and ops.use_hip(video) and not self.space_to_depth:
@@ -220,7 +222,11 @@ class S3D(nn.Module):
         net = self.prepare_video(inputs)
         if self.space_to_depth:
             net = ops.space_to_depth(net)
-        net = self.conv1(net)
+            net = self.conv1(net)
+        elif net.is_cuda and ops.use_hip(net):
+            net = ops.stem_conv_bn_relu(net, self.conv1.conv1.weight, self.conv1.bn1, self.training)
+        else:
+            net = self.conv1(net)
         if self.space_to_depth:
             net = net[:, 1:, 1:, 1:, :].contiguous()
         net = ops.maxpool_tf_same(net, *self.maxpool_2a)

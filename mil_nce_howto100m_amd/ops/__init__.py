@@ -50,6 +50,11 @@ def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool
     return (z, None) if want_gsum else z
 
 
+def stem_conv_bn_relu(x, weight, bn, training: bool):
+    """S3D-G conv1 unit on the prepared bf16 [B,T,H,W,4] clip (GPU paired-width stem)."""
+    return _hip().stem_conv_bn_relu(x, weight, bn, training)
+
+
 def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = False):
     """Several 1x1x1 conv -> BN -> ReLU units on the same input (one fused GEMM on GPU).
     Returns the list of outputs and the gating sum of the first (None on the ATen path)."""

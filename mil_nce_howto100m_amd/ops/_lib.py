@@ -20,8 +20,8 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libmilnce_hip.so")
 P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
 
 SIGNATURES: Dict[str, list] = {
-    "milnce_conv_fwd": [P, I, P, P, P, P, P, I] + [I] * 6 + [I] * 9 + [I] * 6 + [P],
-    "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 6 + [P],
+    "milnce_conv_fwd": [P, I, P, P, P, P, P, I] + [I] * 6 + [I] * 9 + [I] * 7 + [P],
+    "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 7 + [P],
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
@@ -36,6 +36,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],
+    "milnce_u8_to_bf16": [P, P, L, P],
     "milnce_text_relu_max": [P, I, I, I, P, P, P],
     "milnce_text_relu_max_bwd": [P, P, P, I, I, I, P, P],
     "milnce_loss_fwd": [P, I, I, P, P, P, P],

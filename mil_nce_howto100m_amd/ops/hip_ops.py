@@ -62,6 +62,7 @@ class ConvPlan:
     w_Npad: int
     w_Kpad: int
     w_splits: int
+    wo_override: int = 0  # asymmetric w padding (paired-width stem): explicit output width
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -79,8 +80,8 @@ def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
     return bn, bk, npad, kpad, grid_m
 
 
-def conv_plan(x_shape, w_shape, stride, padding) -> ConvPlan:
-    key = (tuple(x_shape), tuple(w_shape), tuple(stride), tuple(padding))
+def conv_plan(x_shape, w_shape, stride, padding, wo_override: int = 0) -> ConvPlan:
+    key = (tuple(x_shape), tuple(w_shape), tuple(stride), tuple(padding), wo_override)
     plan = _PLANS.get(key)
     if plan is not None:
         return plan
@@ -90,7 +91,7 @@ def conv_plan(x_shape, w_shape, stride, padding) -> ConvPlan:
     pt, ph, pw = padding
     To = (T + 2 * pt - kt) // st + 1
     Ho = (H + 2 * ph - kh) // sh + 1
-    Wo = (W + 2 * pw - kw) // sw + 1
+    Wo = wo_override if wo_override else (W + 2 * pw - kw) // sw + 1
     M = B * To * Ho * Wo
     taps = kt * kh * kw
     Ktot = taps * Cin
@@ -108,7 +109,7 @@ def conv_plan(x_shape, w_shape, stride, padding) -> ConvPlan:
     splits = max(1, min(_ceil(4 * _NUM_CU, tiles), _ceil(M, 32 * 8)))
     plan = ConvPlan(B, T, H, W, Cin, Cin_p, Cout, (kt, kh, kw), (st, sh, sw), (pt, ph, pw), To, Ho, Wo, M, Ktot,
                     bn, bk, npad, kpad, grid_m, d_bn, d_bk, d_npad, d_kpad, d_grid_m, w_tn, w_tk, w_npad, w_kpad,
-                    splits)
+                    splits, wo_override)
     _PLANS[key] = plan
     return plan
 
@@ -133,7 +134,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     pt, ph, pw = plan.p
     call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
          plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-         plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, stream())
+         plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, stream())
     return y
 
 
@@ -152,7 +153,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
          ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
          producer_bn[2] if part is not None else 0,
          plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
-         plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, stream())
+         plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, stream())
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx
@@ -192,7 +193,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tenso
     dw = torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     call("milnce_conv_wgrad", ptr(dy), plan.Cout, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
          plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-         plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, stream())
+         plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, plan.wo_override, stream())
     return dw
 
 
@@ -204,8 +205,8 @@ def _bn_nparts(M: int) -> int:
 class _ConvBNReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
-                want_gsum):
-        plan = conv_plan(x.shape, weight.shape, stride, padding)
+                want_gsum, wo_override=0):
+        plan = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
         dev = x.device
         wp = _pack(weight, plan, 0)
         stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
@@ -253,7 +254,7 @@ class _ConvBNReLU(torch.autograd.Function):
             wd = _pack(weight, plan, 1)
             dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
         dw = conv_wgrad(dy, x, plan) if ctx.needs_input_grad[1] else None
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
@@ -264,6 +265,54 @@ def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool
     out = _ConvBNReLU.apply(x, weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
                             tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum))
     return out
+
+
+# -----------------------------------------------------------------------------------------
+# Paired-width stem. The 3x7x7 stride-(2,2,2) stem conv over RGB(+0) pixels has 4-byte operand
+# chunks. Reading the bf16 clip [B,T,H,W,4] as width PAIRS [B,T,H,W/2,8] turns it into an
+# ordinary conv with 8 input channels, kernel (3,7,4), stride (2,2,1), padding (1,3,2|1):
+#     x2[w2][p*4 + c] = x[2*w2 + p][c],  w2[co][p*4 + c][kt][kh][kw4] = w[co][c][kt][kh][2*kw4 + p - 1]
+# (zero where c == 3 or the tap index falls outside 0..6), so every operand load is 16 B. The
+# weight remap is a differentiable gather, so autograd folds dW2 back into dW.
+_STEM_MAP: Dict[torch.device, Tuple[torch.Tensor, torch.Tensor]] = {}
+
+
+def _stem_pair_map(device) -> Tuple[torch.Tensor, torch.Tensor]:
+    hit = _STEM_MAP.get(device)
+    if hit is not None:
+        return hit
+    idx = torch.zeros((8, 3, 7, 4), dtype=torch.long)
+    mask = torch.zeros((8, 3, 7, 4), dtype=F32)
+    for p_ in range(2):
+        for c in range(4):
+            for kt in range(3):
+                for kh in range(7):
+                    for kw4 in range(4):
+                        dw = 2 * kw4 + p_ - 1
+                        if c < 3 and 0 <= dw < 7:
+                            idx[p_ * 4 + c, kt, kh, kw4] = ((c * 3 + kt) * 7 + kh) * 7 + dw
+                            mask[p_ * 4 + c, kt, kh, kw4] = 1.0
+    hit = (idx.reshape(-1).to(device), mask.reshape(-1).to(device))
+    _STEM_MAP[device] = hit
+    return hit
+
+
+def stem_conv_bn_relu(x, weight, bn, training: bool):
+    """S3D-G conv1 (``s3dg.py:226``: 3->64, k (3,7,7), s 2, p (1,3,3)) + BN + ReLU on the bf16
+    clip ``[B,T,H,W,4]`` (channel 3 zero) via the paired-width formulation above."""
+    B, T, H, W, C = x.shape
+    if C != 4 or W % 2 or tuple(weight.shape) != (64, 3, 3, 7, 7):
+        raise ValueError(f"stem expects [B,T,H,W even,4] bf16 and a (64,3,3,7,7) weight, got {tuple(x.shape)}")
+    if x.dtype != BF16:
+        raise TypeError("stem input must be bf16 (see prepare_stem_input)")
+    idx, mask = _stem_pair_map(x.device)
+    cout = weight.shape[0]
+    w2 = (weight.reshape(cout, -1).index_select(1, idx) * mask).view(cout, 8, 3, 7, 4)
+    x2 = x.contiguous().view(B, T, H, W // 2, 8)
+    wo = (W + 2 * 3 - 7) // 2 + 1
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    return _ConvBNReLU.apply(x2, w2, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                             (2, 2, 1), (1, 3, 2), momentum, bn.eps, bool(training), False, wo)
 
 
 class _Conv1x1GroupBNReLU(torch.autograd.Function):
@@ -630,21 +679,27 @@ def synth_video(labels_i32, ids_i32, T, S, seed):
 
 
 def prepare_stem_input(video, native: bool):
+    """Any accepted clip format -> the stem's bf16 ``[B,T,H,W,4]`` operand (values /255 for
+    uint8 input; channel 3 zero). Native clips are uint8 ``[B,T,H,W,4]`` already."""
     if native:
         v = video.contiguous()
-        if v.dtype not in (torch.uint8, BF16):
-            v = v.to(BF16)
-        return v
-    B, C, T, H, W = video.shape
-    assert C == 3
-    video = video.contiguous()
-    if video.dtype == torch.uint8:
-        out = torch.empty((B, T, H, W, 4), dtype=torch.uint8, device=video.device)
-        kind = 0
+        if v.dtype == BF16:
+            return v
+        if v.dtype != torch.uint8:
+            return v.to(BF16)
     else:
-        if video.dtype not in (F32, BF16):
-            video = video.float()
-        kind = 1 if video.dtype == F32 else 2
-        out = torch.empty((B, T, H, W, 8), dtype=BF16, device=video.device)
-    call("milnce_stem_prep", ptr(video), kind, B, T, H, W, ptr(out), stream())
+        B, C, T, H, W = video.shape
+        assert C == 3
+        video = video.contiguous()
+        if video.dtype == torch.uint8:
+            v = torch.empty((B, T, H, W, 4), dtype=torch.uint8, device=video.device)
+            call("milnce_stem_prep", ptr(video), 0, B, T, H, W, ptr(v), stream())
+        else:
+            if video.dtype not in (F32, BF16):
+                video = video.float()
+            out = torch.empty((B, T, H, W, 4), dtype=BF16, device=video.device)
+            call("milnce_stem_prep", ptr(video), 1 if video.dtype == F32 else 2, B, T, H, W, ptr(out), stream())
+            return out
+    out = torch.empty(v.shape, dtype=BF16, device=v.device)
+    call("milnce_u8_to_bf16", ptr(v), ptr(out), v.numel(), stream())
     return out

@@ -58,6 +58,7 @@ class GradBucketer:
         self.bucket_size.append(cur_count)
         self._pending: List[int] = list(self.bucket_size)
         self._handles: List[Optional[object]] = [None] * len(self.buckets)
+        self.sync_enabled = True  # False: accumulate only (micro-batches before the last)
         self._hooks = []
         if world_size > 1:
             for p in self.params:
@@ -79,10 +80,18 @@ class GradBucketer:
                                            async_op=True)
 
     def _on_grad(self, p: torch.Tensor) -> None:
+        if not self.sync_enabled:
+            return
         b = self.bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0 and self._handles[b] is None:
             self._launch(b)
+
+    def set_sync(self, enabled: bool) -> None:
+        """Gradient accumulation: with sync off, backward passes only accumulate into the flat
+        buffer; the pass run with sync on issues every bucket as its last gradient lands."""
+        self.sync_enabled = bool(enabled)
+        self._pending = list(self.bucket_size)
 
     def finish(self) -> None:
         """Issue buckets whose params got no gradient this step, then wait for all."""

@@ -115,9 +115,13 @@ class Trainer:
         if self.buffers is not None:
             with self.timer.phase("broadcast_buffers"):
                 self.buffers()
-        loss = self.forward_loss(batch)
-        with self.timer.phase("backward"):
-            loss.backward()
+        chunks = int(getattr(self.args, "grad_cache_chunks", 0) or 0)
+        if chunks > 1:
+            loss = self._grad_cache_backward(batch, chunks)
+        else:
+            loss = self.forward_loss(batch)
+            with self.timer.phase("backward"):
+                loss.backward()
         with self.timer.phase("allreduce_wait"):
             self.bucketer.finish()
         with self.timer.phase("optimizer"):
@@ -125,6 +129,48 @@ class Trainer:
             self.scheduler.step()
         self.global_step += 1
         return loss.detach()
+
+    def _grad_cache_backward(self, batch: Dict[str, torch.Tensor], chunks: int) -> torch.Tensor:
+        """GradCache two-pass step: the loss still sees every rank's
+        full local batch as negatives, but activations are only held for one micro-batch.
+
+        1. embeddings of all micro-batches without an autograd graph (BN running statistics
+           are restored afterwards, so they advance once per micro-batch as in pass 2);
+        2. all-gather + loss + backward to the (local) embeddings only;
+        3. per micro-batch: re-forward with the graph, backward the cached embedding gradient
+           (gradient all-reduce is issued during the last micro-batch only).
+        BatchNorm sees micro-batch statistics, the usual gradient-accumulation semantics.
+        """
+        video, text = batch["video"], batch["text"]
+        b = video.shape[0]
+        bounds = [(i * b // chunks, (i + 1) * b // chunks) for i in range(chunks)]
+        bounds = [(s, e) for s, e in bounds if e > s]
+        bufs = [t for t in self.model.buffers()]
+        saved = [t.clone() for t in bufs]
+        with torch.no_grad(), self.timer.phase("gc_embed"):
+            vs, ts = [], []
+            for s, e in bounds:
+                v, t = self.model(video[s:e], text[s:e].reshape(-1, text.shape[-1]))
+                vs.append(v)
+                ts.append(t)
+            for t, v in zip(bufs, saved):
+                t.copy_(v)
+        ve = torch.cat(vs).detach().requires_grad_(True)
+        te = torch.cat(ts).detach().requires_grad_(True)
+        with self.timer.phase("all_gather"):
+            vg, tg = pdist.all_gather_embeddings(ve, te, self.ctx)
+        with self.timer.phase("loss"):
+            loss = self._loss(batch, vg, tg)
+        loss.backward()
+        k = text.shape[1] if text.dim() == 3 else 1
+        with self.timer.phase("backward"):
+            for i, (s, e) in enumerate(bounds):
+                self.bucketer.set_sync(i == len(bounds) - 1)
+                v, t = self.model(video[s:e], text[s:e].reshape(-1, text.shape[-1]))
+                surrogate = (v * ve.grad[s:e].to(v.dtype)).sum() + (t * te.grad[s * k:e * k].to(t.dtype)).sum()
+                surrogate.backward()
+            self.bucketer.set_sync(True)
+        return loss
 
     # ---------------------------------------------------------------------------------
     def state(self, epoch: int, step_in_epoch: int = 0) -> dict:

@@ -299,9 +299,40 @@ def test_stem_prep_reference_layout():
     h = hip()
     v = torch.randint(0, 256, (2, 3, 4, 6, 6), dtype=torch.uint8, device=DEV)
     o = h.prepare_stem_input(v, native=False)
-    assert o.shape == (2, 4, 6, 6, 4)
-    assert torch.equal(o[..., :3], v.permute(0, 2, 3, 4, 1))
-    assert int(o[..., 3].abs().sum()) == 0
+    assert o.shape == (2, 4, 6, 6, 4) and o.dtype == torch.bfloat16
+    ref = (v.permute(0, 2, 3, 4, 1).float() / 255.0).to(torch.bfloat16)
+    assert torch.equal(o[..., :3], ref)
+    assert int(o[..., 3].float().abs().sum()) == 0
+    f = torch.rand(2, 3, 4, 6, 6, device=DEV)
+    of = h.prepare_stem_input(f, native=False)
+    assert torch.equal(of[..., :3], f.permute(0, 2, 3, 4, 1).to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("S", [20, 36])
+def test_paired_width_stem(S):
+    """conv1 via the width-pair formulation == the (3,7,7) stride-2 conv + BN + ReLU (fp32 ref)."""
+    torch.manual_seed(4)
+    h = hip()
+    B, T = 2, 6
+    u8 = torch.randint(0, 256, (B, T, S, S, 4), dtype=torch.uint8, device=DEV)
+    u8[..., 3] = 0
+    x = h.prepare_stem_input(u8, native=True)
+    conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
+    bn = nn.BatchNorm3d(64).to(DEV)
+    bn_ref = nn.BatchNorm3d(64).to(DEV)
+    bn_ref.load_state_dict(bn.state_dict())
+    z = h.stem_conv_bn_relu(x, conv.weight, bn, True)
+    wr = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    xr = x[..., :3].float()
+    zr = aten.conv_bn_relu(xr, wr, bn_ref, (2, 2, 2), (1, 3, 3), True)
+    assert z.shape == zr.shape
+    assert rel_err(z, zr) < 2e-2
+    dz = torch.randn_like(zr)
+    z.backward(dz.to(torch.bfloat16))
+    zr.backward(dz)
+    assert rel_err(conv.weight.grad, wr.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_ref.weight.grad) < 3e-2
+    assert torch.allclose(bn.running_mean, bn_ref.running_mean, rtol=2e-2, atol=2e-3)
 
 
 @pytest.mark.parametrize("dist", ["cosine", "negative_dot", None])

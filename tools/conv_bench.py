@@ -50,7 +50,7 @@ def main():
     print(f"{'shape (B,T,H,W,Cin)->Cout k s':58s} {'GFLOP':>7s} {'fwd ms':>7s} {'TF/s':>6s} {'dgr ms':>7s} "
           f"{'TF/s':>6s} {'wgr ms':>7s} {'TF/s':>6s}")
     for key, plan in sorted(hip_ops._PLANS.items(), key=lambda kv: -kv[1].M * kv[1].Cout * kv[1].Ktot):
-        xs, ws, s, p = key
+        xs, ws, s, p, _wo = key
         u8 = plan.Cin % 8 != 0
         x = (torch.randint(0, 255, xs, dtype=torch.uint8, device="cuda") if u8
              else torch.randn(xs, device="cuda").to(torch.bfloat16))
