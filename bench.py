@@ -33,6 +33,11 @@ def main():
     ap.add_argument("--device", type=str, default="auto")
     ap.add_argument("--blocks", type=str, default="")
     ap.add_argument("--profile_steps", type=int, default=0, help="extra steps under torch profiler")
+    ap.add_argument("--loss", type=str, default="milnce",
+                    help="milnce (configs 2/3) | cdtw | sdtw_cidm | sdtw_negative | sdtw_3 (config 4)")
+    ap.add_argument("--seq_len", type=int, default=8, help="clips per sequence for the soft-DTW losses")
+    ap.add_argument("--grad_cache_chunks", type=int, default=0,
+                    help="GradCache micro-batches per GPU (config 5: 32f, 1024 clips/GPU)")
     opts = ap.parse_args()
 
     import torch
@@ -50,10 +55,15 @@ def main():
     args = get_args(argv=["--batch_size", str(b * ctx.world_size), "--num_frames", str(opts.num_frames),
                           "--video_size", str(opts.size), "--num_candidates", str(opts.num_candidates),
                           "--warmup_steps", "10000", "--lr", "0.001", "--epochs", "150",
-                          "--word2vec_path", "", "--blocks", opts.blocks])
+                          "--word2vec_path", "", "--blocks", opts.blocks, "--loss", opts.loss,
+                          "--seq_len", str(opts.seq_len), "--grad_cache_chunks", str(opts.grad_cache_chunks)])
     seed_everything(args.seed, ctx.rank)
     data = SyntheticClips(b, opts.num_frames, opts.size, opts.num_candidates, args.max_words, args.vocab_size,
                           seed=args.seed, device=ctx.device, rank=ctx.rank, world_size=ctx.world_size)
+    if opts.loss != "milnce":
+        from mil_nce_howto100m_amd.data.synthetic import SyntheticSequences
+        assert b % opts.seq_len == 0, "batch_per_gpu must be a multiple of seq_len"
+        data = SyntheticSequences(b // opts.seq_len, opts.seq_len, data)
     model = build_model(args, ctx.device)
     trainer = Trainer(args, model, ctx, len(data))
     cuda = ctx.device.type == "cuda"
@@ -108,11 +118,14 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16" if cuda else "fp32",
             "data": "synthetic (on-device generator, random-init weights)",
-            "config": {"model": "S3D-G + word2vec text tower, MIL-NCE",
+            "config": {"model": "S3D-G + word2vec text tower, " + ("MIL-NCE" if opts.loss == "milnce"
+                                                                    else f"{opts.loss} (soft-DTW)"),
                        "global_batch": b * ctx.world_size, "seq_len": opts.num_frames,
                        "frames": opts.num_frames, "resolution": opts.size,
                        "num_candidates": opts.num_candidates,
-                       "parallelism": f"dp{ctx.world_size}"},
+                       "parallelism": f"dp{ctx.world_size}",
+                       "grad_cache_chunks": opts.grad_cache_chunks,
+                       **({"sdtw_seq_len": opts.seq_len} if opts.loss != "milnce" else {})},
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
         }

@@ -1007,26 +1007,27 @@ static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-static int g_conv_impl = 3;  // 3: LDS-DMA ring (bf16 inputs); 2: register-staged kernel
-
-MILNCE_API int milnce_conv_set_impl(int impl) {
-  const int old = g_conv_impl;
-  g_conv_impl = impl;
-  return old;
-}
-
-template <int BN, int BK>
+// Kernel variants (the host autotunes per conv shape, ops/hip_ops.py):
+//   2: register-staged double buffer; 3: LDS-DMA ring, BK as planned, 3 stages;
+//   4: LDS-DMA ring, 2 stages (2 blocks/CU at BN 128); 5: LDS-DMA ring, BK 32, 4 stages.
+template <int BN, int BK, int S>
 static int launch_v3_epi(ConvParams& p, hipStream_t stream) {
-  constexpr int S = BK == 64 ? 3 : 4;  // ring <= 96 KiB (BN 128) or 72 KiB (BN 64)
   if (p.bn_mode == 0) return launch_fwd_v3<BN, BK, S, 0>(p, stream);
   if (p.bn_mode == 1) return launch_fwd_v3<BN, BK, S, 1>(p, stream);
   return launch_fwd_v3<BN, BK, S, 2>(p, stream);
 }
 
+template <int BN, int BK>
+static int launch_v3_impl(ConvParams& p, int impl, hipStream_t stream) {
+  if (impl == 5) return launch_v3_epi<BN, 32, 4>(p, stream);
+  if (impl == 4) return launch_v3_epi<BN, BK, 2>(p, stream);
+  return launch_v3_epi<BN, BK, 3>(p, stream);
+}
+
 template <int BM, int BN, int BK, bool U8>
-static int launch_fwd(ConvParams& p, hipStream_t stream) {
+static int launch_fwd(ConvParams& p, int impl, hipStream_t stream) {
   if constexpr (!U8) {
-    if (g_conv_impl == 3) return launch_v3_epi<BN, BK>(p, stream);
+    if (impl >= 3) return launch_v3_impl<BN, BK>(p, impl, stream);
   }
   if constexpr (U8) {
     if (p.bn_mode == 0) return launch_fwd_epi<BM, BN, BK, true, 0>(p, stream);
@@ -1045,7 +1046,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
                                int B, int T, int H, int W, int Cin, int Cout,
                                int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
                                int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
-                               hipStream_t stream) {
+                               int impl, hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
   p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss; p.bn_ld = bn_ld;
@@ -1070,15 +1071,15 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.fCin = make_fastdiv(Cin);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
   if (x_u8) {
-    if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, true>(p, stream);
-    if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, true>(p, stream);
-    if (bn == 128 && bk == 32) return launch_fwd<128, 128, 32, true>(p, stream);
-    if (bn == 128 && bk == 64) return launch_fwd<128, 128, 64, true>(p, stream);
+    if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, true>(p, impl, stream);
+    if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, true>(p, impl, stream);
+    if (bn == 128 && bk == 32) return launch_fwd<128, 128, 32, true>(p, impl, stream);
+    if (bn == 128 && bk == 64) return launch_fwd<128, 128, 64, true>(p, impl, stream);
   } else {
-    if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, false>(p, stream);
-    if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, false>(p, stream);
-    if (bn == 128 && bk == 32) return launch_fwd<128, 128, 32, false>(p, stream);
-    if (bn == 128 && bk == 64) return launch_fwd<128, 128, 64, false>(p, stream);
+    if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, false>(p, impl, stream);
+    if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, false>(p, impl, stream);
+    if (bn == 128 && bk == 32) return launch_fwd<128, 128, 32, false>(p, impl, stream);
+    if (bn == 128 && bk == 64) return launch_fwd<128, 128, 64, false>(p, impl, stream);
   }
   return (int)hipErrorInvalidValue;
 }

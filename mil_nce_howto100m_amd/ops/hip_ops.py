@@ -8,6 +8,7 @@ the stem) which go to hipBLASLt through ``torch.mm``. Shapes are planned once pe
 from __future__ import annotations
 
 import ctypes
+import os
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -28,7 +29,7 @@ def _ceil(a: int, b: int) -> int:
 # =========================================================================================
 # Conv + BN + ReLU
 # =========================================================================================
-@dataclass(frozen=True)
+@dataclass
 class ConvPlan:
     B: int
     T: int
@@ -63,6 +64,8 @@ class ConvPlan:
     w_Kpad: int
     w_splits: int
     wo_override: int = 0  # asymmetric w padding (paired-width stem): explicit output width
+    impl: int = 0         # forward kernel variant (csrc/conv.hip launch_v3_impl); 0 = not tuned yet
+    d_impl: int = 0       # dgrad kernel variant
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -127,14 +130,46 @@ def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
     return out
 
 
+_IMPLS = (2, 3, 4, 5)
+_AUTOTUNE = os.environ.get("MILNCE_CONV_AUTOTUNE", "1") != "0"
+_DEFAULT_IMPL = int(os.environ.get("MILNCE_CONV_IMPL", "2"))
+
+
+def _tune(launch, impls=_IMPLS) -> int:
+    """Time each kernel variant on the real operands (outputs are simply overwritten) and keep
+    the fastest; run once per conv shape and direction, then cached in the plan."""
+    if not _AUTOTUNE:
+        return _DEFAULT_IMPL
+    best, best_t = _DEFAULT_IMPL, float("inf")
+    s = torch.cuda.current_stream()
+    for impl in impls:
+        launch(impl)  # warm (first launch sets kernel attributes)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(s)
+        for _ in range(2):
+            launch(impl)
+        b.record(s)
+        b.synchronize()
+        t = a.elapsed_time(b)
+        if t < best_t:
+            best, best_t = impl, t
+    return best
+
+
 def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: Optional[torch.Tensor]):
     y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=x.device)
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
-    call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
-         plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-         plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, stream())
+
+    def launch(impl):
+        call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
+             plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
+             plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, impl, stream())
+
+    if plan.impl == 0:
+        plan.impl = _tune(launch) if x.dtype != torch.uint8 else 2
+    launch(plan.impl)
     return y
 
 
@@ -149,11 +184,17 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
     part = None
     if producer_bn is not None:
         part = torch.empty((plan.d_grid_m * 2 * plan.d_Npad,), dtype=F32, device=dy.device)
-    call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), ptr(part),
-         ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
-         producer_bn[2] if part is not None else 0,
-         plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
-         plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, stream())
+
+    def launch(impl):
+        call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), ptr(part),
+             ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
+             producer_bn[2] if part is not None else 0,
+             plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
+             plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, impl, stream())
+
+    if plan.d_impl == 0:
+        plan.d_impl = _tune(launch)
+    launch(plan.d_impl)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx
