@@ -73,6 +73,13 @@ def main():
             torch.cuda.synchronize()
 
     step = 0
+    if opts.warmup == 0 and cuda:
+        # setup, not a training step: one forward/backward so per-shape conv autotuning
+        # (first use of each conv plan) does not land inside the timed region
+        trainer.model.train()
+        trainer.forward_loss(data.batch(0)).backward()
+        trainer.bucketer.finish()
+        trainer.bucketer.zero()
     for _ in range(opts.warmup):
         loss = trainer.train_step(data.batch(step))
         step += 1

@@ -921,6 +921,169 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
       }
 }
 
+// ---------------------------------------------------------------------------------------
+// v3 wgrad: dY and im2col(X) tiles [R rows][TN|TK] arrive by LDS-DMA into a STAGES-deep ring
+// (no staging VGPRs, no ds_write pass). The images are unpadded with a 16-B chunk XOR of
+// 2*(row & 7), which keeps the ds_read_b64_tr_b16 fragment reads conflict-free (the eight rows a
+// 32-lane group touches land on distinct chunk pairs); each lane DMAs the source chunk that
+// belongs in its lane-linear slot. Row tables (one row decomposition per stage) are computed
+// STAGES steps ahead in a (STAGES+1)-deep table ring.
+__device__ __forceinline__ int wg_swz(int row, int chunk, int cpr) {
+  return chunk ^ ((2 * (row & 7)) & (cpr - 1));
+}
+
+__device__ __forceinline__ bf16x8 tr_frag_sw(const bf16_t* img, int cols, int cpr, int k0, int col, int g, int q,
+                                             int pp) {
+  const int r0 = k0 + 4 * g + q, r1 = r0 + 16;
+  const int c = col / 8 + (pp >> 1), h = (pp & 1) * 4;
+  const bf16_t* a0 = img + r0 * cols + wg_swz(r0, c, cpr) * 8 + h;
+  const bf16_t* a1 = img + r1 * cols + wg_swz(r1, c, cpr) * 8 + h;
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+template <int TN_, int TK_, int STAGES>
+__global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
+  constexpr int R = WG_R;
+  constexpr int DCPR = TN_ / 8, XCPR = TK_ / 8;
+  constexpr int DRPI = 64 / DCPR, XRPI = 64 / XCPR;  // rows per DMA instruction
+  constexpr int D_INST = R / DRPI / 4, X_INST = R / XRPI / 4;
+  constexpr int NDMA = D_INST + X_INST;
+  constexpr int WN = TN_ / 2, WK = TK_ / 2;
+  constexpr int TI = WN / 16, TJ = WK / 16;
+  constexpr int STAGE_ELEMS = R * (TN_ + TK_);
+  constexpr int NTAB = STAGES + 1;
+  static_assert(D_INST >= 1 && X_INST >= 1, "tile too small for the DMA mapping");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* ring = (bf16_t*)smem;                               // stage: dY [R][TN] then X [R][TK]
+  int2* rtab = (int2*)(smem + STAGES * STAGE_ELEMS * 2);      // [NTAB][R]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int ntiles = p.n_tiles * p.k_tiles;
+  const int nblocks = ntiles * p.splits;
+  const int logical = xcd_remap(blockIdx.x, nblocks);
+  const int split = logical / ntiles;
+  const int tile = logical % ntiles;
+  const int n0 = (tile % p.n_tiles) * TN_;
+  const int k0 = (tile / p.n_tiles) * TK_;
+  const int m_begin = split * p.rows_per_split;
+  const int m_end = min(p.M, m_begin + p.rows_per_split);
+
+  // dY DMA lane mapping (row-invariant source chunk)
+  const int d_slot = lane % DCPR, d_lrow = wave * DRPI + lane / DCPR;
+  const int d_chunk = wg_swz(d_lrow, d_slot, DCPR);
+  const int n_lane = n0 + d_chunk * 8;
+  const bool n_ok = n_lane < p.Cout;
+  // X DMA lane mapping: fixed (tap, c) for the whole kernel
+  const int x_slot = lane % XCPR, x_lrow = wave * XRPI + lane / XCPR;
+  const int x_chunk = wg_swz(x_lrow, x_slot, XCPR);
+  const int kk = k0 + x_chunk * 8;
+  const int tap = (int)fdiv((uint32_t)kk, p.fCin);
+  const int c = kk - tap * p.Cin;
+  const bool kval = kk < p.Ktot;
+  const int dw = tap % p.KW, dh = (tap / p.KW) % p.KH, dt = tap / (p.KW * p.KH);
+  const int tapoff = ((dt * p.H + dh) * p.W + dw) * p.Cin + c;
+
+  const int m_clamped = m_begin < m_end ? m_begin : 0;
+  const long long dbase = (long long)m_clamped * p.ldd * 2;
+  const long long dbytes = m_end > m_begin ? (long long)(m_end - m_begin) * p.ldd * 2 : 0;
+  const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
+  const uint32_t b_first = (uint32_t)m_clamped / thw;
+  const long long xbase = (long long)b_first * p.x_bstride * 2;
+  const long long xrem = p.x_total_bytes - xbase;
+  const uint32_t xnrec = xrem > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)xrem;
+  const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.dy + dbase), (short)0,
+                                                     (int)(dbytes > 0x7FFFFFF0LL ? 0x7FFFFFF0LL : dbytes), 0x00020000);
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + xbase), (short)0, (int)xnrec,
+                                                     0x00020000);
+
+  f32x4 acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (m_end - m_begin + R - 1) / R;
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+
+  auto issue = [&](int st) {
+    bf16_t* sd = ring + (st % STAGES) * STAGE_ELEMS;
+    bf16_t* sx = sd + R * TN_;
+    const int2* tb = rtab + (st % NTAB) * R;
+    const int mb = m_begin + st * R;
+#pragma unroll
+    for (int i = 0; i < D_INST; ++i) {
+      const int row = i * 4 * DRPI + d_lrow;
+      const int m = mb + row;
+      const bool v = (m < m_end) & n_ok;
+      const uint32_t off = v ? (uint32_t)(m - m_clamped) * (uint32_t)p.ldd * 2u + (uint32_t)n_lane * 2u : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(drs, (lds_ptr_t)(sd + (i * 4 * DRPI + wave * DRPI) * TN_), 16, off,
+                                               0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < X_INST; ++i) {
+      const int row = i * 4 * XRPI + x_lrow;
+      const int2 e = tb[row];
+      const int ti = (e.y & 1023) - 64 + dt, hi = ((e.y >> 10) & 1023) - 64 + dh, wi = (e.y >> 20) - 64 + dw;
+      const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+                     ((unsigned)wi < (unsigned)p.W);
+      const uint32_t off = v ? (uint32_t)((e.x + tapoff) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(sx + (i * 4 * XRPI + wave * XRPI) * TK_), 16, off,
+                                               0, 0, 0);
+    }
+  };
+
+  if (nsteps > 0) {
+#pragma unroll
+    for (int st = 0; st < STAGES; ++st)
+      if (st < nsteps) wgrad_row_table(rtab + (st % NTAB) * R, p, m_begin + st * R, m_end, b_first, tid);
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < STAGES - 1; ++st)
+      if (st < nsteps) issue(st);
+  }
+  for (int s = 0; s < nsteps; ++s) {
+    const int ahead = min(nsteps - 1, s + STAGES - 2) - s;
+    wait_vmcnt_le(ahead * NDMA);
+    __builtin_amdgcn_s_barrier();
+    if (s + STAGES - 1 < nsteps) issue(s + STAGES - 1);
+    if (s + STAGES < nsteps)
+      wgrad_row_table(rtab + ((s + STAGES) % NTAB) * R, p, m_begin + (s + STAGES) * R, m_end, b_first, tid);
+    const bf16_t* d = ring + (s % STAGES) * STAGE_ELEMS;
+    const bf16_t* x = d + R * TN_;
+#pragma unroll
+    for (int ks = 0; ks < R / 32; ++ks) {
+      bf16x8 af[TI], bfr[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = tr_frag_sw(d, TN_, DCPR, ks * 32, wr * WN + i * 16, g, q, pp);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = tr_frag_sw(x, TK_, XCPR, ks * 32, wc * WK + j * 16, g, q, pp);
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float* out = p.slab + (long long)split * p.Npad * p.Kpad;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wr * WN + i * 16 + (lane >> 4) * 4 + r;
+        const int k = k0 + wc * WK + j * 16 + (lane & 15);
+        out[(long long)n * p.Kpad + k] = acc[i][j][r];
+      }
+}
+
 // Sum the split slabs (coalesced along k) and scatter to the PyTorch weight layout
 // [n][c_param][tap].
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw, int splits,
@@ -1098,11 +1261,32 @@ static int launch_wgrad(WgradParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+template <int TN_, int TK_, int STAGES>
+static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
+  const size_t lds = (size_t)STAGES * WG_R * (TN_ + TK_) * 2 + (STAGES + 1) * WG_R * sizeof(int2);
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_v3_kernel<TN_, TK_, STAGES>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int nblocks = p.n_tiles * p.k_tiles * p.splits;
+  hipLaunchKernelGGL((conv_wgrad_v3_kernel<TN_, TK_, STAGES>), dim3(nblocks), dim3(256), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+template <int TN_, int TK_>
+static int launch_wgrad_impl(WgradParams& p, int impl, hipStream_t stream) {
+  if (impl == 4) return launch_wgrad_v3<TN_, TK_, 2>(p, stream);
+  if (impl == 3) return launch_wgrad_v3<TN_, TK_, 3>(p, stream);
+  return launch_wgrad<TN_, TK_, false>(p, stream);
+}
+
 MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u8, float* slab, float* dw,
                                  int B, int T, int H, int W, int Cin, int Cin_param, int Cout,
                                  int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
                                  int Kpad, int Npad, int tn, int tk, int splits, int accumulate, int wo_override,
-                                 hipStream_t stream) {
+                                 int impl, hipStream_t stream) {
   WgradParams p;
   p.dy = (const bf16_t*)dy; p.x = x; p.slab = slab;
   p.T = T; p.H = H; p.W = W; p.Cin = Cin;
@@ -1131,10 +1315,10 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
     else if (tn == 64 && tk == 128) rc = launch_wgrad<64, 128, true>(p, stream);
     else rc = (int)hipErrorInvalidValue;
   } else {
-    if (tn == 64 && tk == 64) rc = launch_wgrad<64, 64, false>(p, stream);
-    else if (tn == 64 && tk == 128) rc = launch_wgrad<64, 128, false>(p, stream);
-    else if (tn == 128 && tk == 64) rc = launch_wgrad<128, 64, false>(p, stream);
-    else if (tn == 128 && tk == 128) rc = launch_wgrad<128, 128, false>(p, stream);
+    if (tn == 64 && tk == 64) rc = launch_wgrad_impl<64, 64>(p, impl, stream);
+    else if (tn == 64 && tk == 128) rc = launch_wgrad_impl<64, 128>(p, impl, stream);
+    else if (tn == 128 && tk == 64) rc = launch_wgrad_impl<128, 64>(p, impl, stream);
+    else if (tn == 128 && tk == 128) rc = launch_wgrad_impl<128, 128>(p, impl, stream);
     else rc = (int)hipErrorInvalidValue;
   }
   if (rc) return rc;

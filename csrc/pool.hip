@@ -264,15 +264,60 @@ struct BnAcc {
 
 // Gather backward: output windows covering input i along one dim are o = (i+pad)/S - j,
 // j < ceil(K/S), valid when 0 <= o < n_out and the in-window offset i+pad-o*S < K.
+template <int KT, int KH, int KW, int ST, int SH, int SW>
+__device__ __forceinline__ void pool_bwd_one(const PoolParams& p, const PoolDivs& d, const bf16_t* __restrict__ dy,
+                                             const uint8_t* __restrict__ arg, uint32_t pos, int c0, float* acc) {
+  constexpr int NT = (KT + ST - 1) / ST, NH = (KH + SH - 1) / SH, NW = (KW + SW - 1) / SW;
+  uint32_t q = fdiv(pos, d.fW);
+  const int wi = (int)(pos - q * p.W);
+  uint32_t q2 = fdiv(q, d.fH);
+  const int hi = (int)(q - q2 * p.H);
+  const uint32_t b = fdiv(q2, d.fT);
+  const int ti = (int)(q2 - b * p.T);
+  const size_t obase = (size_t)b * p.To * p.Ho * p.Wo * p.C + c0;
+  uint4 g[NT * NH * NW];
+  uint2 a[NT * NH * NW];
+  uint32_t tap[NT * NH * NW];
+  bool ok[NT * NH * NW];
+#pragma unroll
+  for (int jt = 0; jt < NT; ++jt)
+#pragma unroll
+    for (int jh = 0; jh < NH; ++jh)
+#pragma unroll
+      for (int jw = 0; jw < NW; ++jw) {
+        const int u = (jt * NH + jh) * NW + jw;
+        const int to = (ti + p.pt) / ST - jt, ho = (hi + p.ph) / SH - jh, wo = (wi + p.pw) / SW - jw;
+        const int dt = ti + p.pt - to * ST, dh = hi + p.ph - ho * SH, dw = wi + p.pw - wo * SW;
+        ok[u] = (to >= 0) & (to < p.To) & (dt < KT) & (ho >= 0) & (ho < p.Ho) & (dh < KH) & (wo >= 0) &
+                (wo < p.Wo) & (dw < KW);
+        tap[u] = (uint32_t)((dt * KH + dh) * KW + dw);
+        const size_t o = ok[u] ? obase + ((size_t)(to * p.Ho + ho) * p.Wo + wo) * p.C : obase;
+        g[u] = *(const uint4*)(dy + o);
+        a[u] = *(const uint2*)(arg + o);
+      }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
+#pragma unroll
+  for (int u = 0; u < NT * NH * NW; ++u) {
+    float gf[8];
+    unpack8(g[u], gf);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t ak = ((k < 4 ? a[u].x : a[u].y) >> (8 * (k & 3))) & 0xff;
+      acc[k] += (ok[u] & (ak == tap[u])) ? gf[k] : 0.f;
+    }
+  }
+}
+
 // Thread = fixed 8-channel chunk cc = tid % cpr of rpi = 256/cpr input positions per step; block
-// blockIdx.x walks positions [pos_begin, pos_end).
+// blockIdx.x walks positions [pos_begin, pos_end), two positions per thread per iteration so
+// both gathers' loads are in flight together.
 template <int KT, int KH, int KW, int ST, int SH, int SW>
 __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ dy,
                                                      const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                      uint32_t npos, uint32_t pos_per_block,
                                                      const bf16_t* __restrict__ bn_y, int bn_ld,
                                                      const float* __restrict__ bn_ss, float* __restrict__ part) {
-  constexpr int NT = (KT + ST - 1) / ST, NH = (KH + SH - 1) / SH, NW = (KW + SW - 1) / SW;
   __shared__ float red[16 * 256];
   const int cpr = p.C >> 3, rpi = 256 / cpr;
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
@@ -283,53 +328,23 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
   acc_bn.zero();
   const uint32_t pos_begin = blockIdx.x * pos_per_block;
   const uint32_t pos_end = min(npos, pos_begin + pos_per_block);
-  for (uint32_t pos = pos_begin + rr; active && pos < pos_end; pos += rpi) {
-    uint32_t q = fdiv(pos, d.fW);
-    const int wi = (int)(pos - q * p.W);
-    uint32_t q2 = fdiv(q, d.fH);
-    const int hi = (int)(q - q2 * p.H);
-    const uint32_t b = fdiv(q2, d.fT);
-    const int ti = (int)(q2 - b * p.T);
-    const size_t obase = (size_t)b * p.To * p.Ho * p.Wo * p.C + c0;
-    uint4 g[NT * NH * NW];
-    uint2 a[NT * NH * NW];
-    uint32_t tap[NT * NH * NW];
-    bool ok[NT * NH * NW];
-#pragma unroll
-    for (int jt = 0; jt < NT; ++jt)
-#pragma unroll
-      for (int jh = 0; jh < NH; ++jh)
-#pragma unroll
-        for (int jw = 0; jw < NW; ++jw) {
-          const int u = (jt * NH + jh) * NW + jw;
-          const int to = (ti + p.pt) / ST - jt, ho = (hi + p.ph) / SH - jh, wo = (wi + p.pw) / SW - jw;
-          const int dt = ti + p.pt - to * ST, dh = hi + p.ph - ho * SH, dw = wi + p.pw - wo * SW;
-          ok[u] = (to >= 0) & (to < p.To) & (dt < KT) & (ho >= 0) & (ho < p.Ho) & (dh < KH) & (wo >= 0) &
-                  (wo < p.Wo) & (dw < KW);
-          tap[u] = (uint32_t)((dt * KH + dh) * KW + dw);
-          const size_t o = ok[u] ? obase + ((size_t)(to * p.Ho + ho) * p.Wo + wo) * p.C : obase;
-          g[u] = *(const uint4*)(dy + o);
-          a[u] = *(const uint2*)(arg + o);
-        }
-    float acc[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-#pragma unroll
-    for (int u = 0; u < NT * NH * NW; ++u) {
-      float gf[8];
-      unpack8(g[u], gf);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t ak = ((k < 4 ? a[u].x : a[u].y) >> (8 * (k & 3))) & 0xff;
-        acc[k] += (ok[u] & (ak == tap[u])) ? gf[k] : 0.f;
-      }
-    }
-    const uint4 dv = pack8(acc);
-    *(uint4*)(dx + (size_t)pos * p.C + c0) = dv;
+  for (uint32_t pos = pos_begin + rr; active && pos < pos_end; pos += 2 * rpi) {
+    const uint32_t pos2 = pos + rpi;
+    const bool two = pos2 < pos_end;
+    float a0[8], a1[8];
+    pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, pos, c0, a0);
+    pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, two ? pos2 : pos, c0, a1);
+    const uint4 v0 = pack8(a0), v1 = pack8(a1);
+    *(uint4*)(dx + (size_t)pos * p.C + c0) = v0;
+    if (two) *(uint4*)(dx + (size_t)pos2 * p.C + c0) = v1;
     if (bn) {
       float dr[8];
-      unpack8(dv, dr);
+      unpack8(v0, dr);
       acc_bn.add(dr, bn_y + (size_t)pos * bn_ld + c0, bn_ss, p.C, c0);
+      if (two) {
+        unpack8(v1, dr);
+        acc_bn.add(dr, bn_y + (size_t)pos2 * bn_ld + c0, bn_ss, p.C, c0);
+      }
     }
   }
   if (bn) acc_bn.commit(red, part, p.C, cpr, rpi, cc, rr, active);

@@ -66,6 +66,7 @@ class ConvPlan:
     wo_override: int = 0  # asymmetric w padding (paired-width stem): explicit output width
     impl: int = 0         # forward kernel variant (csrc/conv.hip launch_v3_impl); 0 = not tuned yet
     d_impl: int = 0       # dgrad kernel variant
+    w_impl: int = 0       # wgrad kernel variant (2: register-staged, 3/4: LDS-DMA ring, 3/2 stages)
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -232,9 +233,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tenso
     pt, ph, pw = plan.p
     slab = torch.empty((plan.w_splits, plan.w_Npad, plan.w_Kpad), dtype=F32, device=dy.device)
     dw = torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
-    call("milnce_conv_wgrad", ptr(dy), plan.Cout, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
-         plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-         plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, plan.wo_override, stream())
+    ldd = plan.Cout
+
+    def launch(impl):
+        call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
+             plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
+             plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, plan.wo_override, impl, stream())
+
+    if plan.w_impl == 0:
+        plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
+    launch(plan.w_impl)
     return dw
 
 

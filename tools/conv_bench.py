@@ -50,7 +50,7 @@ def main():
     print(f"{'shape (B,T,H,W,Cin)->Cout k s':58s} {'GFLOP':>7s} {'fwd ms':>7s} {'TF/s':>6s} {'dgr ms':>7s} "
           f"{'TF/s':>6s} {'wgr ms':>7s} {'TF/s':>6s}")
     for key, plan in sorted(hip_ops._PLANS.items(), key=lambda kv: -kv[1].M * kv[1].Cout * kv[1].Ktot):
-        plan.impl = plan.d_impl = 0  # re-tune on these operands
+        plan.impl = plan.d_impl = plan.w_impl = 0  # re-tune on these operands
         xs, ws, s, p, _wo = key
         u8 = plan.Cin % 8 != 0
         x = (torch.randint(0, 255, xs, dtype=torch.uint8, device="cuda") if u8
@@ -72,7 +72,7 @@ def main():
         flops_tot += fl
         desc = f"{xs}->{plan.Cout} k{plan.k} s{plan.s[1]}"
         print(f"{desc:58s} {fl / 1e9:7.1f} {t_f:7.3f} {fl / t_f / 1e9:6.0f} {t_d:7.3f} {fl / t_d / 1e9:6.0f} "
-              f"{t_w:7.3f} {fl / t_w / 1e9:6.0f}  impl f{plan.impl} d{plan.d_impl}", flush=True)
+              f"{t_w:7.3f} {fl / t_w / 1e9:6.0f}  impl f{plan.impl} d{plan.d_impl} w{plan.w_impl}", flush=True)
     print(f"TOTAL fwd {tot['fwd']:.2f} ms  dgrad {tot['dgrad']:.2f} ms  wgrad {tot['wgrad']:.2f} ms  "
           f"(fwd FLOP {flops_tot / 1e12:.2f} T -> {flops_tot / tot['fwd'] / 1e9:.0f} TF/s)")
 
