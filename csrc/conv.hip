@@ -32,7 +32,7 @@ struct ConvParams {
   int num_m_tiles, num_n_tiles, grid_m;
   float in_scale;
   long long x_total_bytes;
-  FastDiv fWo, fHo, fTo, fCin;
+  FastDiv fWo, fHo, fTo, fCin, fKW, fKH;
   // epilogue statistics: 0 none; 1 BN forward sums of this conv's output (stats);
   // 2 BN backward partials of the PRODUCER of this dgrad's output: the output is that
   //   layer's dz, bn_y/bn_ss its raw conv output and [mean, invstd, scale, shift];
@@ -520,13 +520,17 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
     auto issue = [&](int kt) {
       bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
       bf16_t* sb = sa + BM * BK;
+      // (tap, c) of this lane's chunk by arithmetic: an LDS table read here would make the
+      // compiler drain every LDS-DMA in flight (it cannot prove the read does not alias them)
       const int k = kt * BK + src_chunk * 8;
       const int tap = (int)fdiv((uint32_t)k, p.fCin);
       const int c = k - tap * p.Cin;
       const bool kval = tap < taps;
-      const int2 te = tab[min(tap, taps - 1)];
-      const int dt = te.y & 0xff, dh = (te.y >> 8) & 0xff, dw = te.y >> 16;
-      const uint32_t koff = (uint32_t)((te.x + c) * 2);
+      const int tq = (int)fdiv((uint32_t)tap, p.fKW);
+      const int dw = tap - tq * p.KW;
+      const int dt = (int)fdiv((uint32_t)tq, p.fKH);
+      const int dh = tq - dt * p.KH;
+      const uint32_t koff = (uint32_t)((((dt * p.H + dh) * p.W + dw) * p.Cin + c) * 2);
 #pragma unroll
       for (int i = 0; i < A_INST; ++i) {
         const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
@@ -926,8 +930,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 // (no staging VGPRs, no ds_write pass). The images are unpadded with a 16-B chunk XOR of
 // 2*(row & 7), which keeps the ds_read_b64_tr_b16 fragment reads conflict-free (the eight rows a
 // 32-lane group touches land on distinct chunk pairs); each lane DMAs the source chunk that
-// belongs in its lane-linear slot. Row tables (one row decomposition per stage) are computed
-// STAGES steps ahead in a (STAGES+1)-deep table ring.
+// belongs in its lane-linear slot.
 __device__ __forceinline__ int wg_swz(int row, int chunk, int cpr) {
   return chunk ^ ((2 * (row & 7)) & (cpr - 1));
 }
@@ -954,12 +957,10 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
   constexpr int WN = TN_ / 2, WK = TK_ / 2;
   constexpr int TI = WN / 16, TJ = WK / 16;
   constexpr int STAGE_ELEMS = R * (TN_ + TK_);
-  constexpr int NTAB = STAGES + 1;
   static_assert(D_INST >= 1 && X_INST >= 1, "tile too small for the DMA mapping");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* ring = (bf16_t*)smem;                               // stage: dY [R][TN] then X [R][TK]
-  int2* rtab = (int2*)(smem + STAGES * STAGE_ELEMS * 2);      // [NTAB][R]
+  bf16_t* ring = (bf16_t*)smem;  // stage: dY [R][TN] then X [R][TK]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1014,7 +1015,6 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
   auto issue = [&](int st) {
     bf16_t* sd = ring + (st % STAGES) * STAGE_ELEMS;
     bf16_t* sx = sd + R * TN_;
-    const int2* tb = rtab + (st % NTAB) * R;
     const int mb = m_begin + st * R;
 #pragma unroll
     for (int i = 0; i < D_INST; ++i) {
@@ -1027,22 +1027,26 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
     }
 #pragma unroll
     for (int i = 0; i < X_INST; ++i) {
-      const int row = i * 4 * XRPI + x_lrow;
-      const int2 e = tb[row];
-      const int ti = (e.y & 1023) - 64 + dt, hi = ((e.y >> 10) & 1023) - 64 + dh, wi = (e.y >> 20) - 64 + dw;
-      const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+      // row decomposition by arithmetic (no LDS reads while LDS-DMA is in flight, see fwd v3)
+      const int m = mb + i * 4 * XRPI + x_lrow;
+      const uint32_t q0 = fdiv((uint32_t)m, p.fWo);
+      const int wo = m - q0 * p.Wo;
+      const uint32_t q1 = fdiv(q0, p.fHo);
+      const int ho = q0 - q1 * p.Ho;
+      const uint32_t bb = fdiv(q1, p.fTo);
+      const int to = q1 - bb * p.To;
+      const int ti = to * p.st - p.pt + dt, hi = ho * p.sh - p.ph + dh, wi = wo * p.sw - p.pw + dw;
+      const bool v = kval & (m < m_end) & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                      ((unsigned)wi < (unsigned)p.W);
-      const uint32_t off = v ? (uint32_t)((e.x + tapoff) * 2) : 0x80000000u;
+      const uint32_t off = v ? (uint32_t)(((long long)(bb - b_first) * p.x_bstride +
+                                           ((long long)(ti * p.H + hi) * p.W + wi) * p.Cin + c) * 2)
+                             : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lds_ptr_t)(sx + (i * 4 * XRPI + wave * XRPI) * TK_), 16, off,
                                                0, 0, 0);
     }
   };
 
   if (nsteps > 0) {
-#pragma unroll
-    for (int st = 0; st < STAGES; ++st)
-      if (st < nsteps) wgrad_row_table(rtab + (st % NTAB) * R, p, m_begin + st * R, m_end, b_first, tid);
-    __syncthreads();
 #pragma unroll
     for (int st = 0; st < STAGES - 1; ++st)
       if (st < nsteps) issue(st);
@@ -1052,8 +1056,6 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
     wait_vmcnt_le(ahead * NDMA);
     __builtin_amdgcn_s_barrier();
     if (s + STAGES - 1 < nsteps) issue(s + STAGES - 1);
-    if (s + STAGES < nsteps)
-      wgrad_row_table(rtab + ((s + STAGES) % NTAB) * R, p, m_begin + (s + STAGES) * R, m_end, b_first, tid);
     const bf16_t* d = ring + (s % STAGES) * STAGE_ELEMS;
     const bf16_t* x = d + R * TN_;
 #pragma unroll
@@ -1232,6 +1234,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.in_scale = x_u8 ? (1.0f / 255.0f) : 1.0f;
   p.fWo = make_fastdiv(p.Wo); p.fHo = make_fastdiv(p.Ho); p.fTo = make_fastdiv(p.To);
   p.fCin = make_fastdiv(Cin);
+  p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
   if (x_u8) {
     if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, true>(p, impl, stream);
@@ -1263,7 +1266,7 @@ static int launch_wgrad(WgradParams& p, hipStream_t stream) {
 
 template <int TN_, int TK_, int STAGES>
 static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)STAGES * WG_R * (TN_ + TK_) * 2 + (STAGES + 1) * WG_R * sizeof(int2);
+  const size_t lds = (size_t)STAGES * WG_R * (TN_ + TK_) * 2;
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_v3_kernel<TN_, TK_, STAGES>,

@@ -19,7 +19,7 @@ def main(argv=None):
 
     args = get_args(argv=argv)
     ctx = pdist.init_distributed(args.dist_backend, args.device)
-    return eval_hmdb(args, ctx.device)
+    return eval_hmdb(args, ctx.device, ctx=ctx)
 
 
 if __name__ == "__main__":

@@ -19,7 +19,7 @@ def main(argv=None):
 
     args = get_args(argv=argv)
     ctx = pdist.init_distributed(args.dist_backend, args.device)
-    return eval_retrieval(args, ctx.device, "msrvtt")
+    return eval_retrieval(args, ctx.device, "msrvtt", ctx=ctx)
 
 
 if __name__ == "__main__":

@@ -14,18 +14,25 @@ import torch
 
 
 @torch.no_grad()
-def extract_features(model, batches: Iterable[dict], device):
+def extract_features(model, batches: Iterable[dict], device, rank: int = 0, world: int = 1):
+    """mixed_5c features of every window; with world > 1 each rank embeds its shard of the
+    batches and the results are all-gathered in stream order (eval/sharding.py)."""
+    from .sharding import map_sharded
+
     model.eval()
-    feats, labels, splits = [], [], [[], [], []]
-    for data in batches:
+
+    def one(data):
         video = data["video"].to(device)
         b, nc = video.shape[0], video.shape[1]
         f = model(video.reshape((b * nc,) + tuple(video.shape[2:])), None, mode="video", mixed5c=True)
-        feats.append(f.float().view(b, nc, -1).cpu().numpy())
-        labels.extend(list(data["label"]))
-        for k in range(3):
-            splits[k].append(np.asarray(data[f"split{k + 1}"]))
-    return np.concatenate(feats, 0), np.asarray(labels), [np.concatenate(s) for s in splits]
+        return (f.float().view(b, nc, -1).cpu().numpy(), list(data["label"]),
+                [np.asarray(data[f"split{k + 1}"]) for k in range(3)])
+
+    res = map_sharded(one, batches, rank, world)
+    feats = np.concatenate([r[0] for r in res], 0)
+    labels = np.asarray([lab for r in res for lab in r[1]])
+    splits = [np.concatenate([r[2][k] for r in res]) for k in range(3)]
+    return feats, labels, splits
 
 
 def linear_probe(feats: np.ndarray, labels: Sequence, splits: List[np.ndarray], C: float = 100.0,

@@ -53,8 +53,15 @@ def _use_real(csv: str, root: str) -> bool:
     return bool(csv) and os.path.isfile(csv) and os.path.isdir(root) and ffmpeg_available()
 
 
-def eval_hmdb(args, device, model: Optional[S3D] = None) -> dict:
+def _rank_world(ctx):
+    return (ctx.rank, ctx.world_size) if ctx is not None else (0, 1)
+
+
+def eval_hmdb(args, device, model: Optional[S3D] = None, ctx=None) -> dict:
+    """HMDB linear probe; with a multi-rank ``ctx`` the feature extraction is sharded over the
+    ranks (one process per GPU) and rank 0 reports."""
     model = model or load_eval_model(args, device)
+    rank, world = _rank_world(ctx)
     csv = getattr(args, "eval_csv", "") or os.path.join("csv", "hmdb51.csv")
     if _use_real(csv, args.eval_video_root):
         ds = HMDBDataset(csv, args.eval_video_root, args.num_windows_test, args.num_frames, args.video_size)
@@ -62,16 +69,17 @@ def eval_hmdb(args, device, model: Optional[S3D] = None) -> dict:
     else:
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,
                                    args.num_frames, args.video_size, device=device).batches(args.batch_size_val)
-    feats, labels, splits = extract_features(model, batches, device)
-    res = linear_probe(feats, labels, splits, C=100.0)
+    feats, labels, splits = extract_features(model, batches, device, rank, world)
+    res = linear_probe(feats, labels, splits, C=100.0) if rank == 0 else {}
     for k in (1, 2, 3):
         if f"split{k}" in res:
             print("Top 1 accuracy split {} and C {} : {}".format(k, 100.0, res[f"split{k}"]), flush=True)
     return res
 
 
-def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None) -> dict:
+def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None, ctx=None) -> dict:
     model = model or load_eval_model(args, device)
+    rank, world = _rank_world(ctx)
     csv = getattr(args, "eval_csv", "") or os.path.join(
         "csv", "msrvtt_test.csv" if kind == "msrvtt" else "validation_youcook.csv")
     tok = Tokenizer(args.token_to_word_path, max_words=30)
@@ -82,8 +90,9 @@ def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None) -> dict
     else:
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,
                                    args.num_frames, args.video_size, device=device).batches(args.batch_size_val)
-    m = evaluate_retrieval(model, batches, device)
-    print(format_metrics(m), flush=True)
+    m = evaluate_retrieval(model, batches, device, rank, world)
+    if rank == 0:
+        print(format_metrics(m), flush=True)
     return m
 
 

@@ -202,3 +202,42 @@ def test_phase_timers_cpu():
             sum(range(1000))
     s = t.summary()
     assert set(s) == {"forward"} and s["forward"] >= 0.0
+
+
+def _worker_eval(rank, world, port, outdir):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticEvalSet
+    from mil_nce_howto100m_amd.eval import embed_retrieval, extract_features
+    from mil_nce_howto100m_amd.train.engine import build_model, seed_everything
+    args = _args()
+    seed_everything(5, 0)
+    model = build_model(args, ctx.device)
+    ev = SyntheticEvalSet(10, 2, 4, 32, vocab_size=500)
+    f, lab, spl = extract_features(model, ev.batches(3), ctx.device, ctx.rank, ctx.world_size)
+    t, v = embed_retrieval(model, ev.batches(3), ctx.device, ctx.rank, ctx.world_size)
+    _put(outdir, rank, (f, lab, spl, t, v))
+    dist.destroy_process_group()
+
+
+def test_sharded_eval_matches_single_process():
+    """One process per GPU replaces nn.DataParallel in the evals: 2-rank sharded features and
+    embeddings == the single-process ones, in the same order, on every rank."""
+    import numpy as np
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticEvalSet
+    from mil_nce_howto100m_amd.eval import embed_retrieval, extract_features
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    from mil_nce_howto100m_amd.train.engine import build_model, seed_everything
+    world = 2
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_eval, args=(world, _port(), out), nprocs=world)
+        res = _collect(out, world)
+    pdist.set_context(pdist.DistContext())
+    seed_everything(5, 0)
+    model = build_model(_args(), torch.device("cpu"))
+    ev = SyntheticEvalSet(10, 2, 4, 32, vocab_size=500)
+    f, lab, spl = extract_features(model, ev.batches(3), "cpu")
+    t, v = embed_retrieval(model, ev.batches(3), "cpu")
+    for rf, rlab, rspl, rt, rv in res:
+        assert np.allclose(rf, f, atol=1e-5) and list(rlab) == list(lab)
+        assert all(np.array_equal(a, b) for a, b in zip(rspl, spl))
+        assert np.allclose(rt, t, atol=1e-5) and np.allclose(rv, v, atol=1e-5)
