@@ -187,7 +187,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
                                                                int C, double count, const float* __restrict__ gamma,
                                                                const float* __restrict__ ss,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                               float* __restrict__ coef) {
+                                                               float* __restrict__ coef, int accumulate, int batch_stats) {
   __shared__ double red[2][32][33];
   const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
@@ -218,11 +218,15 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __re
   if (rg != 0 || c >= C) return;
   s1 = 0.0; s2 = 0.0;
   for (int k = 0; k < 32; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
-  dbeta[c] = (float)s1;
-  dgamma[c] = (float)s2;
+  // accumulate: dgamma/dbeta are the parameters' gradient buffers (written in place, += across
+  // gradient-accumulation passes); otherwise fresh outputs
+  dbeta[c] = accumulate ? dbeta[c] + (float)s1 : (float)s1;
+  dgamma[c] = accumulate ? dgamma[c] + (float)s2 : (float)s2;
   coef[c] = gamma[c] * ss[C + c];
-  coef[C + c] = (float)(s1 / count);
-  coef[2 * C + c] = (float)(s2 / count);
+  // batch statistics (train mode): the mean/var depend on x, giving the two correction terms;
+  // running statistics (eval mode): BN is a fixed affine map, dy = gamma * invstd * dz * mask
+  coef[C + c] = batch_stats ? (float)(s1 / count) : 0.f;
+  coef[2 * C + c] = batch_stats ? (float)(s2 / count) : 0.f;
 }
 
 // dy = coef0 * (dz*mask - coef1 - xhat*coef2). Each thread owns one 8-channel chunk (its
@@ -287,7 +291,8 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
 // have_part = 0: reduce them here (ps = C).
 MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
                              const float* gamma, float* part, int nparts, int ps, int have_part, float* dgamma,
-                             float* dbeta, float* coef, void* dy, int lddy, hipStream_t stream) {
+                             float* dbeta, float* coef, void* dy, int lddy, int accumulate, int batch_stats,
+                             hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   if (!have_part) {
     const int rows_per_block = (int)((M + nparts - 1) / nparts);
@@ -296,7 +301,7 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
     ps = C;
   }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(1024), 0, stream, part, nparts, ps, C,
-                     (double)M, gamma, ss, dgamma, dbeta, coef);
+                     (double)M, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   const int rpi = 256 / (C / 8);
   long long nblk = (M + 16LL * rpi - 1) / (16LL * rpi);  // >= 16 rows per thread
   if (nblk > 8192) nblk = 8192;

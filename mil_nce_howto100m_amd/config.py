@@ -98,7 +98,8 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--synthetic_eval_videos", type=int, default=96, help="videos in the synthetic eval set")
     g.add_argument("--stop_epoch", type=int, default=0,
                    help="end this run after this epoch (simulated interruption for resume tests)")
-    g.add_argument("--hip_graph", type=int, default=0, help="capture the train step in a HIP graph")
+    g.add_argument("--hip_graph", type=int, default=1,
+                   help="replay evaluation forwards from captured HIP graphs (launch-bound at small batch)")
     g.add_argument("--grad_cache_chunks", type=int, default=0,
                    help="GradCache-style step in this many micro-batches per GPU: exact global-negative "
                         "MIL-NCE with bounded activation memory (BASELINE config 5); 0/1: off")

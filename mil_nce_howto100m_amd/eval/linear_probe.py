@@ -17,14 +17,17 @@ import torch
 def extract_features(model, batches: Iterable[dict], device, rank: int = 0, world: int = 1):
     """mixed_5c features of every window; with world > 1 each rank embeds its shard of the
     batches and the results are all-gathered in stream order (eval/sharding.py)."""
+    from ..utils.hipgraph import GraphedCallable
     from .sharding import map_sharded
 
     model.eval()
+    fwd = GraphedCallable(lambda v: model(v, None, mode="video", mixed5c=True)) if _graphs_ok(device) else \
+        (lambda v: model(v, None, mode="video", mixed5c=True))
 
     def one(data):
         video = data["video"].to(device)
         b, nc = video.shape[0], video.shape[1]
-        f = model(video.reshape((b * nc,) + tuple(video.shape[2:])), None, mode="video", mixed5c=True)
+        f = fwd(video.reshape((b * nc,) + tuple(video.shape[2:])))
         return (f.float().view(b, nc, -1).cpu().numpy(), list(data["label"]),
                 [np.asarray(data[f"split{k + 1}"]) for k in range(3)])
 
@@ -33,6 +36,16 @@ def extract_features(model, batches: Iterable[dict], device, rank: int = 0, worl
     labels = np.asarray([lab for r in res for lab in r[1]])
     splits = [np.concatenate([r[2][k] for r in res]) for k in range(3)]
     return feats, labels, splits
+
+
+def _graphs_ok(device) -> bool:
+    """HIP-graph replay for the eval forward: GPU with the HIP kernels active (env
+    MILNCE_EVAL_GRAPHS=0 disables)."""
+    import os
+    from .. import ops
+    dev = torch.device(device)
+    return (dev.type == "cuda" and os.environ.get("MILNCE_EVAL_GRAPHS", "1") != "0"
+            and ops.use_hip(torch.empty(0, device=dev)))
 
 
 def linear_probe(feats: np.ndarray, labels: Sequence, splits: List[np.ndarray], C: float = 100.0,

@@ -18,16 +18,19 @@ from .metrics import compute_metrics
 
 @torch.no_grad()
 def embed_retrieval(model, batches: Iterable[dict], device, rank: int = 0, world: int = 1) -> tuple:
+    from ..utils.hipgraph import GraphedCallable
+    from .linear_probe import _graphs_ok
     from .sharding import map_sharded
 
     model.eval()
+    fwd = GraphedCallable(lambda v, t: model(v, t)) if _graphs_ok(device) else (lambda v, t: model(v, t))
 
     def one(data):
         text = data["text"].to(device)
         video = data["video"].to(device)
         b, nc = video.shape[0], video.shape[1]
         video = video.reshape((b * nc,) + tuple(video.shape[2:]))
-        v, t = model(video, text)
+        v, t = fwd(video, text)
         v = v.float().view(b, nc, -1).mean(dim=1)
         return t.float().cpu().numpy(), v.cpu().numpy()
 

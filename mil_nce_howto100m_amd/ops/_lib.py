@@ -25,7 +25,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
-    "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, P],
+    "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, I, I, P],
     "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P],
     "milnce_gate_bwd_reduce": [I, P, P, P, P, I, I, P, P],
     "milnce_gate_bwd_apply": [I, P, P, P, P, P, I, I, P, P, P, P, I, P],

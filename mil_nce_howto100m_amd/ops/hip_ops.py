@@ -15,7 +15,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import aten
+from . import aten, grad_sink
 from ._lib import call, lib, ptr, stream
 
 BF16 = torch.bfloat16
@@ -138,22 +138,30 @@ _DEFAULT_IMPL = int(os.environ.get("MILNCE_CONV_IMPL", "2"))
 
 def _tune(launch, impls=_IMPLS) -> int:
     """Time each kernel variant on the real operands (outputs are simply overwritten) and keep
-    the fastest; run once per conv shape and direction, then cached in the plan."""
+    the fastest; run once per conv shape and direction, then cached in the plan. Each variant
+    is timed over >= ~0.5 ms of repetitions, and the default wins unless another is >= 3 %
+    faster, so the choice is stable from run to run."""
     if not _AUTOTUNE:
         return _DEFAULT_IMPL
-    best, best_t = _DEFAULT_IMPL, float("inf")
     s = torch.cuda.current_stream()
-    for impl in impls:
-        launch(impl)  # warm (first launch sets kernel attributes)
+
+    def timed(impl, reps):
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(s)
-        for _ in range(2):
+        for _ in range(reps):
             launch(impl)
         b.record(s)
         b.synchronize()
-        t = a.elapsed_time(b)
-        if t < best_t:
-            best, best_t = impl, t
+        return a.elapsed_time(b) / reps
+
+    times = {}
+    for impl in impls:
+        launch(impl)  # warm (first launch sets kernel attributes)
+        t0 = timed(impl, 1)
+        times[impl] = timed(impl, max(2, min(50, int(0.5 / max(t0, 1e-3)))))
+    best = min(times, key=times.get)
+    if _DEFAULT_IMPL in times and times[best] > 0.97 * times[_DEFAULT_IMPL]:
+        best = _DEFAULT_IMPL
     return best
 
 
@@ -227,21 +235,48 @@ def take_bn_partials(dz: torch.Tensor):
     return part
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan) -> torch.Tensor:
+# -----------------------------------------------------------------------------------------
+# Direct gradient writes. Parameters whose .grad is a view into the data-parallel flat buffer
+# (parallel/ddp.py marks them ``_milnce_flat_grad``) get their weight / BN gradients written
+# (accumulated) in place by the producing kernel instead of being returned to autograd, which
+# would launch one AccumulateGrad add per parameter; the bucketer is then told the gradient
+# is ready through the sink it registered.
+def _direct_grad(param: torch.Tensor) -> Optional[torch.Tensor]:
+    if not param.is_leaf or not getattr(param, "_milnce_flat_grad", False):
+        return None
+    g = param.grad
+    if g is not None and getattr(param, "_milnce_flat_grad", False) and g.dtype == F32 and g.is_contiguous():
+        return g
+    return None
+
+
+def _grad_done(param: torch.Tensor) -> None:
+    grad_sink.notify(param)
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """dW of the conv; with ``out`` the result is accumulated into it (a parameter's grad)."""
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
     slab = torch.empty((plan.w_splits, plan.w_Npad, plan.w_Kpad), dtype=F32, device=dy.device)
-    dw = torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
+    acc = int(out is not None)
+    dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
 
     def launch(impl):
         call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
              plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-             plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, 0, plan.wo_override, impl, stream())
+             plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, acc, plan.wo_override, impl, stream())
 
     if plan.w_impl == 0:
-        plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
+        if acc:  # tune on a scratch output: the real one accumulates
+            real, acc_real = dw, acc
+            dw, acc = torch.empty_like(real), 0
+            plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
+            dw, acc = real, acc_real
+        else:
+            plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
     launch(plan.w_impl)
     return dw
 
@@ -270,6 +305,8 @@ class _ConvBNReLU(torch.autograd.Function):
         call("milnce_bn_relu_apply", ptr(y), C, ptr(z), C, ptr(ss), C, plan.B, plan.To * plan.Ho * plan.Wo,
              ptr(gsum), stream())
         ctx.save_for_backward(x, weight, y, ss, gamma)
+        ctx.beta = beta  # parameter handle only (its gradient buffer may be written in place)
+        ctx.training = bool(training)
         ctx.plan = plan
         ctx.x_bn = getattr(x, "_milnce_bn", None)  # (y, ss, ld) of the BN layer that produced x
         z._milnce_bn = (y, ss, C)
@@ -293,16 +330,30 @@ class _ConvBNReLU(torch.autograd.Function):
             part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
             ps = C
         coef = torch.empty((3 * C,), dtype=F32, device=dev)
-        dgamma = torch.empty((C,), dtype=F32, device=dev)
-        dbeta = torch.empty((C,), dtype=F32, device=dev)
+        beta = ctx.beta
+        g_direct, b_direct = _direct_grad(gamma), _direct_grad(beta)
+        direct_bn = g_direct is not None and b_direct is not None
+        dgamma = g_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
+        dbeta = b_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
         dy = torch.empty_like(y)
         call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
-             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, stream())
+             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, int(direct_bn),
+             int(ctx.training), stream())
+        if direct_bn:
+            _grad_done(gamma)
+            _grad_done(beta)
+            dgamma = dbeta = None
         dx = None
         if ctx.needs_input_grad[0]:
             wd = _pack(weight, plan, 1)
             dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
-        dw = conv_wgrad(dy, x, plan) if ctx.needs_input_grad[1] else None
+        dw = None
+        if ctx.needs_input_grad[1]:
+            w_direct = _direct_grad(weight)
+            dw = conv_wgrad(dy, x, plan, out=w_direct)
+            if w_direct is not None:
+                _grad_done(weight)
+                dw = None
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
 
 
@@ -405,6 +456,8 @@ class _Conv1x1GroupBNReLU(torch.autograd.Function):
                 gsum = g
             off += c
         ctx.save_for_backward(x, wcat, y, *sss, *[b[0] for b in bns])
+        ctx.betas = [b[1] for b in bns]
+        ctx.training = bool(training)
         ctx.plan, ctx.widths, ctx.n = plan, widths, n
         ctx.x_bn = getattr(x, "_milnce_bn", None)
         if gsum is not None:
@@ -438,11 +491,17 @@ class _Conv1x1GroupBNReLU(torch.autograd.Function):
                 part = torch.empty((nparts * 2 * c,), dtype=F32, device=dev)
                 ps = c
             coef = torch.empty((3 * c,), dtype=F32, device=dev)
-            dgamma = torch.empty((c,), dtype=F32, device=dev)
-            dbeta = torch.empty((c,), dtype=F32, device=dev)
+            g_direct, b_direct = _direct_grad(gammas[i]), _direct_grad(ctx.betas[i])
+            direct_bn = g_direct is not None and b_direct is not None
+            dgamma = g_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
+            dbeta = b_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
             call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
                  ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
-                 ptr(dY[:, off:]), ctot, stream())
+                 ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
+            if direct_bn:
+                _grad_done(gammas[i])
+                _grad_done(ctx.betas[i])
+                dgamma = dbeta = None
             dgs.append(dgamma)
             dbs.append(dbeta)
             off += c

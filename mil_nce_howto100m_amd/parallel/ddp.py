@@ -5,7 +5,8 @@ sized design:
 
 * every trainable parameter's ``.grad`` is a view into ONE flat fp32 buffer laid out in
   (approximate) backward order, so a bucket is a contiguous slice and one RCCL call;
-* ``register_post_accumulate_grad_hook`` marks parameters ready; when a bucket's last
+* ``register_post_accumulate_grad_hook`` (or, for gradients a HIP kernel accumulated in place,
+  the ``ops.grad_sink`` notification) marks parameters ready; when a bucket's last
   gradient lands its all-reduce is issued asynchronously (RCCL runs on its own HIP stream,
   ordered after the compute stream by an event), overlapping with the rest of backward;
 * bucket size defaults to 8 MiB: the 45 MB fp32 gradient becomes ~6 collectives. On
@@ -53,6 +54,7 @@ class GradBucketer:
             self.bucket_of[id(p)] = len(self.buckets)
             cur_count += 1
             p.grad = self.flat[off:off + n].view_as(p)
+            p._milnce_flat_grad = True  # HIP kernels may accumulate into p.grad in place
             off += n
         self.buckets.append([cur_start, off])
         self.bucket_size.append(cur_count)
@@ -63,6 +65,9 @@ class GradBucketer:
         if world_size > 1:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        # kernels that write a gradient in place (no AccumulateGrad) report through this sink
+        from ..ops import grad_sink
+        grad_sink.set_sink(self._on_grad if world_size > 1 else None)
 
     # ---------------------------------------------------------------------------------
     def views_intact(self) -> bool:

@@ -53,6 +53,10 @@ def _use_real(csv: str, root: str) -> bool:
     return bool(csv) and os.path.isfile(csv) and os.path.isdir(root) and ffmpeg_available()
 
 
+def _graph_env(args) -> None:
+    os.environ["MILNCE_EVAL_GRAPHS"] = "1" if getattr(args, "hip_graph", 1) else "0"
+
+
 def _rank_world(ctx):
     return (ctx.rank, ctx.world_size) if ctx is not None else (0, 1)
 
@@ -62,6 +66,7 @@ def eval_hmdb(args, device, model: Optional[S3D] = None, ctx=None) -> dict:
     ranks (one process per GPU) and rank 0 reports."""
     model = model or load_eval_model(args, device)
     rank, world = _rank_world(ctx)
+    _graph_env(args)
     csv = getattr(args, "eval_csv", "") or os.path.join("csv", "hmdb51.csv")
     if _use_real(csv, args.eval_video_root):
         ds = HMDBDataset(csv, args.eval_video_root, args.num_windows_test, args.num_frames, args.video_size)
@@ -80,6 +85,7 @@ def eval_hmdb(args, device, model: Optional[S3D] = None, ctx=None) -> dict:
 def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None, ctx=None) -> dict:
     model = model or load_eval_model(args, device)
     rank, world = _rank_world(ctx)
+    _graph_env(args)
     csv = getattr(args, "eval_csv", "") or os.path.join(
         "csv", "msrvtt_test.csv" if kind == "msrvtt" else "validation_youcook.csv")
     tok = Tokenizer(args.token_to_word_path, max_words=30)

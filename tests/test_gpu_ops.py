@@ -132,6 +132,36 @@ def test_conv_bn_relu_train(cin, cout, k, p, gsum):
     assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
 
 
+def test_conv_bn_relu_eval_mode_backward():
+    """Running-statistics BN (eval mode) is a fixed affine map: no batch-mean correction terms."""
+    torch.manual_seed(6)
+    h = hip()
+    x = torch.randn(2, 4, 6, 6, 64, device=DEV).to(torch.bfloat16)
+    conv = nn.Conv3d(64, 96, (1, 3, 3), 1, (0, 1, 1), bias=False).to(DEV)
+    bn = nn.BatchNorm3d(96).to(DEV)
+    with torch.no_grad():
+        bn.running_mean.uniform_(-0.5, 0.5)
+        bn.running_var.uniform_(0.5, 2.0)
+        bn.weight.uniform_(0.5, 1.5)
+    bn_ref = nn.BatchNorm3d(96).to(DEV)
+    bn_ref.load_state_dict(bn.state_dict())
+    bn.eval()
+    bn_ref.eval()
+    xh = x.clone().requires_grad_(True)
+    z = h.conv_bn_relu(xh, conv.weight, bn, (1, 1, 1), (0, 1, 1), False)
+    wref = conv.weight.detach().to(torch.bfloat16).float().requires_grad_(True)
+    xr = x.float().requires_grad_(True)
+    zr = aten.conv_bn_relu(xr, wref, bn_ref, (1, 1, 1), (0, 1, 1), False)
+    assert rel_err(z, zr) < 2e-2
+    dz = torch.randn_like(zr)
+    z.backward(dz.to(torch.bfloat16))
+    zr.backward(dz)
+    assert rel_err(xh.grad, xr.grad) < 3e-2
+    assert rel_err(conv.weight.grad, wref.grad) < 3e-2
+    assert rel_err(bn.weight.grad, bn_ref.weight.grad) < 3e-2
+    assert rel_err(bn.bias.grad, bn_ref.bias.grad) < 3e-2
+
+
 @pytest.mark.parametrize("widths", [(64, 96, 16), (160, 112, 24)])
 def test_conv1x1_group_matches_separate_units(widths):
     """Fused Inception 1x1x1 branches (one GEMM, per-branch BN) vs an fp32 reference per branch."""
