@@ -88,6 +88,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
   }
   if (active) {
     const long long base = (long long)b * rows_per_b;
+#pragma unroll 4
     for (int r = r_begin + rr; r < r_end; r += rpi) {
       const long long row = base + r;
       uint4 v = *(const uint4*)(y + row * ldy + c0);
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
     a2[k] = 0.f;
   }
   if (active) {
+#pragma unroll 4
     for (long long r = r_begin + rr; r < r_end; r += rpi) {
       float g[8], v[8];
       unpack8(*(const uint4*)(dz + r * ldz + c0), g);
@@ -248,6 +250,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
   const long long r_begin = (long long)blockIdx.x * rows_per_block;
   const long long r_end = min(M, r_begin + rows_per_block);
+#pragma unroll 4
   for (long long r = r_begin + rr; r < r_end; r += rpi) {
     float g[8], v[8], o[8];
     unpack8(*(const uint4*)(dz + r * ldz + c0), g);

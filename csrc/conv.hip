@@ -416,13 +416,17 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
-template <int BN, int BK, int STAGES, int EPI>
-__global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
-  constexpr int BM = 128;
+// NWM waves along M (each wave a 64 x BN/2 sub-tile, 2 waves along N): BM = 64*NWM rows,
+// 128*NWM threads. NWM = 4 (256 x BN tiles, 8 waves) re-reads each operand byte fewer times.
+template <int BN, int BK, int STAGES, int EPI, int NWM>
+__global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p) {
+  constexpr int BM = 64 * NWM;
+  constexpr int NT = 128 * NWM;            // threads
+  constexpr int NWAVES = 2 * NWM;
   constexpr int CPR = BK / 8;              // 16-B chunks per tile row
   constexpr int RPI = 64 / CPR;            // rows per DMA instruction (1 KiB)
-  constexpr int A_INST = BM / RPI / 4;     // DMA instructions per wave per stage (A)
-  constexpr int B_INST = BN / RPI / 4;     // (B)
+  constexpr int A_INST = BM / RPI / NWAVES;  // DMA instructions per wave per stage (A)
+  constexpr int B_INST = BN / RPI / NWAVES;  // (B)
   constexpr int NDMA = A_INST + B_INST;
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: LDS-DMA bases go to M0
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave >> 1, wc = wave & 1;  // wr in [0, NWM)
   const int nblocks = p.num_n_tiles * p.grid_m;
   const int logical = xcd_remap(blockIdx.x, nblocks);
   const int n_tile = logical % p.num_n_tiles;
@@ -461,7 +465,7 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
 
   build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
   if constexpr (EPI == 2) {
-    for (int t = tid; t < 4 * BN; t += 256) {
+    for (int t = tid; t < 4 * BN; t += NT) {
       const int q = t / BN, c = n0 + (t - q * BN);
       ssl[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
     }
@@ -489,7 +493,7 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
     uint32_t rowoff[A_INST];
 #pragma unroll
     for (int i = 0; i < A_INST; ++i) {
-      const int m = m0 + i * 4 * RPI + lrow;
+      const int m = m0 + i * NWAVES * RPI + lrow;
       if (m < p.M) {
         uint32_t q = fdiv((uint32_t)m, p.fWo);
         const int wo = m - q * p.Wo;
@@ -537,14 +541,14 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
         const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                        ((unsigned)wi < (unsigned)p.W);
         const uint32_t off = v ? rowoff[i] + koff : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * 4 * RPI + wave * RPI) * BK), 16, off,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * BK), 16, off,
                                                  0, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < B_INST; ++i) {
-        const int n = n0 + i * 4 * RPI + lrow;
+        const int n = n0 + i * NWAVES * RPI + lrow;
         const uint32_t off = (uint32_t)(((long long)n * p.Kpad + kt * BK + src_chunk * 8) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * 4 * RPI + wave * RPI) * BK), 16, off,
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, off,
                                                  0, 0, 0);
       }
     };
@@ -611,8 +615,8 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
     __syncthreads();
     constexpr int OCPR = BN / 8;
 #pragma unroll
-    for (int it = 0; it < BM * OCPR / 256; ++it) {
-      const int cid = tid + it * 256;
+    for (int it = 0; it < BM * OCPR / NT; ++it) {
+      const int cid = tid + it * NT;
       const int row = cid / OCPR, cc = cid % OCPR;
       const int m = m0 + row, n = n0 + cc * 8;
       const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
@@ -638,16 +642,16 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
   if constexpr (EPI == 2) {
     constexpr int OCPR = BN / 8;
     __syncthreads();
-    float* red = (float*)smem;  // [2][8][256]
+    float* red = (float*)smem;  // [2][8][NT]
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { red[k * 256 + tid] = e_s[k]; red[(8 + k) * 256 + tid] = e_q[k]; }
+    for (int k = 0; k < 8; ++k) { red[k * NT + tid] = e_s[k]; red[(8 + k) * NT + tid] = e_q[k]; }
     __syncthreads();
     if (tid < OCPR) {
       const int npad = p.num_n_tiles * BN;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float s1 = 0.f, s2 = 0.f;
-        for (int j = tid; j < 256; j += OCPR) { s1 += red[k * 256 + j]; s2 += red[(8 + k) * 256 + j]; }
+        for (int j = tid; j < NT; j += OCPR) { s1 += red[k * NT + j]; s2 += red[(8 + k) * NT + j]; }
         const int col = n0 + tid * 8 + k;
         p.stats[(long long)m_slot * 2 * npad + col] = s1;
         p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
@@ -669,15 +673,15 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
         st_q[j][r] = q;
       }
     __syncthreads();
-    float* red = (float*)smem;  // [2 (wc)][2 (s,q)][WN]
-    if (wr == 1 && (lane & 15) == 0) {
+    float* red = (float*)smem;  // [NWM (wr)][2 (wc)][2 (s,q)][WN]
+    if ((lane & 15) == 0) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = j * 16 + (lane >> 4) * 4 + r;
-          red[(wc * 2 + 0) * WN + c] = st_s[j][r];
-          red[(wc * 2 + 1) * WN + c] = st_q[j][r];
+          red[((wr * 2 + wc) * 2 + 0) * WN + c] = st_s[j][r];
+          red[((wr * 2 + wc) * 2 + 1) * WN + c] = st_q[j][r];
         }
     }
     __syncthreads();
@@ -689,8 +693,14 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v3_kernel(ConvParams p) {
         for (int r = 0; r < 4; ++r) {
           const int c = j * 16 + (lane >> 4) * 4 + r;
           const int col = n0 + wc * WN + c;
-          p.stats[(long long)m_slot * 2 * npad + col] = st_s[j][r] + red[(wc * 2 + 0) * WN + c];
-          p.stats[(long long)m_slot * 2 * npad + npad + col] = st_q[j][r] + red[(wc * 2 + 1) * WN + c];
+          float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int w2 = 0; w2 < NWM; ++w2) {
+            s1 += red[((w2 * 2 + wc) * 2 + 0) * WN + c];
+            s2 += red[((w2 * 2 + wc) * 2 + 1) * WN + c];
+          }
+          p.stats[(long long)m_slot * 2 * npad + col] = s1;
+          p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
         }
     }
   }
@@ -806,8 +816,10 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16_t* img, int ld, int k0, int
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <int TN_, int TK_, bool U8>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
+// DEEP: two register staging sets, so the loads for stage s + 2 are issued before stage s is
+// computed and have ~two compute phases to land (the default has one).
+template <int TN_, int TK_, bool U8, bool DEEP = false>
+__global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
   constexpr int R = WG_R;
   constexpr int VEC = U8 ? 4 : 8;
   constexpr int ESZ = U8 ? 1 : 2;
@@ -821,10 +833,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ds = (bf16_t*)smem;               // [2][R][LDN]
   bf16_t* Xs = Ds + 2 * R * LDN;            // [2][R][LDK]
-  int2* rtab = (int2*)(Xs + 2 * R * LDK);   // [2][R] row tables
+  int2* rtab = (int2*)(Xs + 2 * R * LDK);   // [2 or 4][R] row tables
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave >> 1, wc = wave & 1;  // wr in [0, NWM)
   const int ntiles = p.n_tiles * p.k_tiles;
   const int nblocks = ntiles * p.splits;
   // split-major order: an XCD's contiguous logical range covers every tile of a few m-splits,
@@ -876,22 +888,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
 
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
   const int nsteps = (m_end - m_begin + R - 1) / R;
-  if (nsteps > 0) {
-    wgrad_row_table(rtab, p, m_begin, m_end, b_first, tid);
-    wgrad_row_table(rtab + R, p, m_begin + R, m_end, b_first, tid);
-    __syncthreads();
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
-                                                    n0, d_ccol, kval, dt, dh, dw, tapoff);
-    wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
-  }
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int buf = s & 1;
-    const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
-    wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sn & 1) * R, m_begin + sn * R,
-                                                    m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
-    // row table of stage s + 2 into the slot stage s used (its last reader was iteration s - 1)
-    if (s + 2 < nsteps) wgrad_row_table(rtab + buf * R, p, m_begin + (s + 2) * R, m_end, b_first, tid);
+  auto compute = [&](int buf) {
     const bf16_t* d = Ds + buf * R * LDN;
     const bf16_t* x = Xs + buf * R * LDK;
 #pragma unroll
@@ -907,9 +904,70 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradParams p) {
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds + (buf ^ 1) * R * LDN, Xs + (buf ^ 1) * R * LDK,
-                                                     tid, d_ccol, x_ccol, p.in_scale);
+  };
+  if constexpr (!DEEP) {
+    if (nsteps > 0) {
+      wgrad_row_table(rtab, p, m_begin, m_end, b_first, tid);
+      wgrad_row_table(rtab + R, p, m_begin + R, m_end, b_first, tid);
+      __syncthreads();
+      wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
+                                                      n0, d_ccol, kval, dt, dh, dw, tapoff);
+      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+    }
     __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+      const int buf = s & 1;
+      const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
+      wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sn & 1) * R, m_begin + sn * R,
+                                                      m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+      // row table of stage s + 2 into the slot stage s used (its last reader was iteration s - 1)
+      if (s + 2 < nsteps) wgrad_row_table(rtab + buf * R, p, m_begin + (s + 2) * R, m_end, b_first, tid);
+      compute(buf);
+      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds + (buf ^ 1) * R * LDN, Xs + (buf ^ 1) * R * LDK,
+                                                       tid, d_ccol, x_ccol, p.in_scale);
+      __syncthreads();
+    }
+  } else {
+    // register sets: stage x lives in set x & 1; row tables in a 4-slot ring (slot x & 3)
+    uint4 dreg2[DCH];
+    XReg xreg2[XCH];
+    if (nsteps > 0) {
+      for (int st = 0; st < 3; ++st) wgrad_row_table(rtab + (st & 3) * R, p, m_begin + st * R, m_end, b_first, tid);
+      __syncthreads();
+      wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
+                                                      n0, d_ccol, kval, dt, dh, dw, tapoff);
+      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+      wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg2, xreg2, drs, xrs, p, rtab + R, m_begin + R, m_end,
+                                                      m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+    }
+    __syncthreads();
+    for (int s = 0; s < nsteps; s += 2) {
+      // even step s: stage s in LDS buf 0 / set 0 free; stage s+1 in flight in set 1
+      {
+        const int sl = min(s + 2, nsteps - 1);
+        wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sl & 3) * R, m_begin + sl * R,
+                                                        m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+        if (s + 3 < nsteps)
+          wgrad_row_table(rtab + ((s + 3) & 3) * R, p, m_begin + (s + 3) * R, m_end, b_first, tid);
+        compute(0);
+        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg2, xreg2, Ds + R * LDN, Xs + R * LDK, tid, d_ccol,
+                                                         x_ccol, p.in_scale);
+        __syncthreads();
+      }
+      if (s + 1 >= nsteps) break;
+      // odd step s+1: stage s+1 in LDS buf 1 / set 1 free; stage s+2 in flight in set 0
+      {
+        const int sl = min(s + 3, nsteps - 1);
+        wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg2, xreg2, drs, xrs, p, rtab + (sl & 3) * R,
+                                                        m_begin + sl * R, m_end, m_clamped, tid, n0, d_ccol, kval, dt,
+                                                        dh, dw, tapoff);
+        if (s + 4 < nsteps)
+          wgrad_row_table(rtab + ((s + 4) & 3) * R, p, m_begin + (s + 4) * R, m_end, b_first, tid);
+        compute(1);
+        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+        __syncthreads();
+      }
+    }
   }
   // C[i = n][j = k]: row (n) = 4*(lane>>4) + r, col (k) = lane & 15
   float* out = p.slab + (long long)split * p.Npad * p.Kpad;
@@ -1156,34 +1214,42 @@ static int launch_fwd_epi(ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int BN, int BK, int STAGES, int EPI>
+template <int BN, int BK, int STAGES, int EPI, int NWM = 2>
 static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
-  constexpr size_t ring = (size_t)STAGES * (128 + BN) * BK * 2;
-  constexpr size_t epi = (size_t)128 * (BN + 8) * 2;
+  constexpr int BM = 64 * NWM;
+  constexpr size_t ring = (size_t)STAGES * (BM + BN) * BK * 2;
+  constexpr size_t epi = (size_t)BM * (BN + 8) * 2;
   const size_t lds = (ring > epi ? ring : epi) + 8 * 160 + 16 * BN;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v3_kernel<BN, BK, STAGES, EPI>,
+    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  const int nblocks = p.num_n_tiles * p.grid_m;
-  hipLaunchKernelGGL((conv_fwd_v3_kernel<BN, BK, STAGES, EPI>), dim3(nblocks), dim3(256), lds, stream, p);
+  ConvParams q = p;
+  q.num_m_tiles = (p.M + BM - 1) / BM;
+  const int nblocks = q.num_n_tiles * q.grid_m;
+  hipLaunchKernelGGL((conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>), dim3(nblocks), dim3(128 * NWM), lds, stream, q);
   return (int)hipGetLastError();
 }
 
 // Kernel variants (the host autotunes per conv shape, ops/hip_ops.py):
 //   2: register-staged double buffer; 3: LDS-DMA ring, BK as planned, 3 stages;
 //   4: LDS-DMA ring, 2 stages (2 blocks/CU at BN 128); 5: LDS-DMA ring, BK 32, 4 stages.
-template <int BN, int BK, int S>
+template <int BN, int BK, int S, int NWM = 2>
 static int launch_v3_epi(ConvParams& p, hipStream_t stream) {
-  if (p.bn_mode == 0) return launch_fwd_v3<BN, BK, S, 0>(p, stream);
-  if (p.bn_mode == 1) return launch_fwd_v3<BN, BK, S, 1>(p, stream);
-  return launch_fwd_v3<BN, BK, S, 2>(p, stream);
+  if (p.bn_mode == 0) return launch_fwd_v3<BN, BK, S, 0, NWM>(p, stream);
+  if (p.bn_mode == 1) return launch_fwd_v3<BN, BK, S, 1, NWM>(p, stream);
+  return launch_fwd_v3<BN, BK, S, 2, NWM>(p, stream);
 }
 
+//   6: 256-row tiles (8 waves), BK as planned, 3 stages; 7: same, 2 stages.
 template <int BN, int BK>
 static int launch_v3_impl(ConvParams& p, int impl, hipStream_t stream) {
+  if constexpr (BN * BK >= 64 * 64) {  // >= one 1-KiB DMA piece of B per wave with 8 waves
+    if (impl == 7) return launch_v3_epi<BN, BK, 2, 4>(p, stream);
+    if (impl == 6) return launch_v3_epi<BN, BK, 3, 4>(p, stream);
+  }
   if (impl == 5) return launch_v3_epi<BN, 32, 4>(p, stream);
   if (impl == 4) return launch_v3_epi<BN, BK, 2>(p, stream);
   return launch_v3_epi<BN, BK, 3>(p, stream);
@@ -1250,17 +1316,17 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   return (int)hipErrorInvalidValue;
 }
 
-template <int TN_, int TK_, bool U8>
+template <int TN_, int TK_, bool U8, bool DEEP = false>
 static int launch_wgrad(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2 + 2 * WG_R * sizeof(int2);
+  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2 + 4 * WG_R * sizeof(int2);
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_kernel<TN_, TK_, U8>,
+    HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_kernel<TN_, TK_, U8, DEEP>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   const int nblocks = p.n_tiles * p.k_tiles * p.splits;
-  hipLaunchKernelGGL((conv_wgrad_kernel<TN_, TK_, U8>), dim3(nblocks), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_kernel<TN_, TK_, U8, DEEP>), dim3(nblocks), dim3(256), lds, stream, p);
   return (int)hipGetLastError();
 }
 
@@ -1280,6 +1346,7 @@ static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
 
 template <int TN_, int TK_>
 static int launch_wgrad_impl(WgradParams& p, int impl, hipStream_t stream) {
+  if (impl == 5) return launch_wgrad<TN_, TK_, false, true>(p, stream);
   if (impl == 4) return launch_wgrad_v3<TN_, TK_, 2>(p, stream);
   if (impl == 3) return launch_wgrad_v3<TN_, TK_, 3>(p, stream);
   return launch_wgrad<TN_, TK_, false>(p, stream);

@@ -71,6 +71,7 @@ __global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float
   const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
   const bf16_t* zs = t.z[s] + (size_t)b * thw * C + cl;
   bf16_t* o = out + (size_t)b * thw * Ctot + c;
+#pragma unroll 4
   for (int r = r_begin + rr; r < r_end; r += rpi) {
     float f[8];
     unpack8(*(const uint4*)(zs + (size_t)r * C), f);
@@ -166,6 +167,7 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
   const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
   if (active) {
     const size_t row0 = (size_t)b * thw;
+#pragma unroll 4
     for (int r = r_begin + rr; r < r_end; r += rpi) {
       const size_t row = row0 + r;
       float d[8];

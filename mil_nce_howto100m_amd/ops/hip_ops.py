@@ -131,7 +131,8 @@ def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
     return out
 
 
-_IMPLS = (2, 3, 4, 5)
+_IMPLS = (2, 3, 4, 5, 6, 7)
+_W_IMPLS = (2, 3, 4, 5)  # wgrad: register-staged, LDS-DMA 3/2 stages, register-staged 2-deep
 _AUTOTUNE = os.environ.get("MILNCE_CONV_AUTOTUNE", "1") != "0"
 _DEFAULT_IMPL = int(os.environ.get("MILNCE_CONV_IMPL", "2"))
 
@@ -273,10 +274,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         if acc:  # tune on a scratch output: the real one accumulates
             real, acc_real = dw, acc
             dw, acc = torch.empty_like(real), 0
-            plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
+            plan.w_impl = _tune(launch, _W_IMPLS) if x.dtype != torch.uint8 else 2
             dw, acc = real, acc_real
         else:
-            plan.w_impl = _tune(launch, (2, 3, 4)) if x.dtype != torch.uint8 else 2
+            plan.w_impl = _tune(launch, _W_IMPLS) if x.dtype != torch.uint8 else 2
     launch(plan.w_impl)
     return dw
 
