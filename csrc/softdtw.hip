@@ -5,7 +5,8 @@
 // computed on anti-diagonal pass p = (i-1) + (j-1); the three predecessors are the lane's own
 // previous value (R[i][j-1]) and the previous-row lane's values from passes p-1 (R[i-1][j]) and
 // p-2 (R[i-1][j-1]), exchanged through a 3-deep LDS ring, so only the final R goes to global
-// memory (it is saved for the backward). Up to 1024 rows per pair (16 waves).
+// memory (it is saved for the backward). Up to 1024 lanes per pair; longer sequences put several
+// rows on each lane (up to ~6.6k rows, the LDS ring's limit).
 // The distance matrix of pair p is read in place from a (possibly shared) matrix:
 //     D_p[i][j] = D[(p / pair_div) * s_i + (p % pair_div) * s_j + i * ld + j]
 // so the b^2 all-pairs losses (loss.py:93-134) use ONE [b*n, b*m] GEMM output instead of the
@@ -25,13 +26,15 @@ struct PairIndex {
   }
 };
 
+// RPL rows per lane (row i = lane + 1 + k * blockDim.x): rows handled by one lane lie on the same
+// anti-diagonal pass but are >= blockDim apart, so their predecessors always come from another
+// lane through the ring; sequences up to ~6.6k (LDS ring 3 x (N+2) doubles) run on the GPU.
+template <int RPL>
 __global__ void softdtw_fwd_kernel(const float* __restrict__ D, PairIndex pi, int N, int M, float gamma_f, float bw,
                                    double* __restrict__ R, float* __restrict__ out) {
   extern __shared__ double ring[];  // [3][N+1]
   const double gamma = gamma_f;
   const int b = blockIdx.x;
-  const int i = threadIdx.x + 1;  // 1-based row
-  const bool row_ok = i <= N;
   const float* Dp = D + pi.base(b);
   double* Rp = R + (long long)b * (N + 2) * (M + 2);
   const double inv_g = 1.0 / gamma;
@@ -43,36 +46,43 @@ __global__ void softdtw_fwd_kernel(const float* __restrict__ D, PairIndex pi, in
   // ring slot for "row 0": R[0][j] = 0 if j == 0 else inf ; row i>0 at j<=0: inf
   for (int k = threadIdx.x; k < 3 * S; k += blockDim.x) ring[k] = INFINITY;
   __syncthreads();
-  double own_prev = INFINITY;  // R[i][j-1]
+  double own_prev[RPL];  // R[i][j-1]
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) own_prev[r] = INFINITY;
   const int passes = N + M - 1;
   for (int p = 0; p < passes; ++p) {
-    const int j = p - i + 2;
-    double val = INFINITY;
-    if (row_ok && j >= 1 && j <= M) {
-      // R[i-1][j] from pass p-1, R[i-1][j-1] from pass p-2 (row 0 handled analytically)
-      double up, diag;
-      if (i == 1) {
-        up = INFINITY;                  // R[0][j], j >= 1
-        diag = (j == 1) ? 0.0 : INFINITY;  // R[0][j-1]
-      } else {
-        up = ring[((p + 2) % 3) * S + (i - 1)];
-        diag = ring[((p + 1) % 3) * S + (i - 1)];
-        if (j == 1) diag = INFINITY;     // R[i-1][0]
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = threadIdx.x + 1 + r * blockDim.x;  // 1-based row
+      const bool row_ok = i <= N;
+      const int j = p - i + 2;
+      double val = INFINITY;
+      if (row_ok && j >= 1 && j <= M) {
+        // R[i-1][j] from pass p-1, R[i-1][j-1] from pass p-2 (row 0 handled analytically)
+        double up, diag;
+        if (i == 1) {
+          up = INFINITY;                     // R[0][j], j >= 1
+          diag = (j == 1) ? 0.0 : INFINITY;  // R[0][j-1]
+        } else {
+          up = ring[((p + 2) % 3) * S + (i - 1)];
+          diag = ring[((p + 1) % 3) * S + (i - 1)];
+          if (j == 1) diag = INFINITY;  // R[i-1][0]
+        }
+        const double left = own_prev[r];  // R[i][j-1] (inf at j == 1)
+        if (bw > 0.f && fabsf((float)(i - j)) > bw) {
+          val = INFINITY;
+        } else {
+          const double r0 = -diag * inv_g, r1 = -up * inv_g, r2 = -left * inv_g;
+          const double rmax = fmax(fmax(r0, r1), r2);
+          const double rsum = exp(r0 - rmax) + exp(r1 - rmax) + exp(r2 - rmax);
+          const double softmin = -gamma * (log(rsum) + rmax);
+          val = (double)Dp[(long long)(i - 1) * pi.ld + (j - 1)] + softmin;
+        }
+        Rp[(long long)i * (M + 2) + j] = val;
+        own_prev[r] = val;
       }
-      const double left = own_prev;      // R[i][j-1] (inf at j == 1)
-      if (bw > 0.f && fabsf((float)(i - j)) > bw) {
-        val = INFINITY;
-      } else {
-        const double r0 = -diag * inv_g, r1 = -up * inv_g, r2 = -left * inv_g;
-        const double rmax = fmax(fmax(r0, r1), r2);
-        const double rsum = exp(r0 - rmax) + exp(r1 - rmax) + exp(r2 - rmax);
-        const double softmin = -gamma * (log(rsum) + rmax);
-        val = (double)Dp[(long long)(i - 1) * pi.ld + (j - 1)] + softmin;
-      }
-      Rp[(long long)i * (M + 2) + j] = val;
-      own_prev = val;
+      if (row_ok) ring[(p % 3) * S + i] = val;
     }
-    if (row_ok) ring[(p % 3) * S + i] = val;
     __syncthreads();
   }
   if (threadIdx.x == 0) out[b] = (float)Rp[(long long)N * (M + 2) + M];
@@ -88,14 +98,13 @@ __device__ __forceinline__ double rv(const double* Rp, int i, int j, int N, int 
   return isinf(v) ? -INFINITY : v;
 }
 
+template <int RPL>
 __global__ void softdtw_bwd_kernel(const float* __restrict__ D, const double* __restrict__ R, PairIndex pi, int N,
                                    int M, float gamma_f, float bw, const float* __restrict__ gout,
                                    float* __restrict__ G) {
   extern __shared__ double ring[];  // [3][N+2]
   const double gamma = gamma_f;
   const int b = blockIdx.x;
-  const int i = threadIdx.x + 1;
-  const bool row_ok = i <= N;
   const float* Dp = D + pi.base(b);
   const double* Rp = R + (long long)b * (N + 2) * (M + 2);
   float* Gp = G + (long long)b * N * M;
@@ -104,64 +113,95 @@ __global__ void softdtw_bwd_kernel(const float* __restrict__ D, const double* __
   const int S = N + 2;
   for (int k = threadIdx.x; k < 3 * S; k += blockDim.x) ring[k] = 0.0;
   __syncthreads();
-  double own_prev = 0.0;  // E[i][j+1]
+  double own_prev[RPL];  // E[i][j+1]
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) own_prev[r] = 0.0;
   const int passes = N + M - 1;
   for (int q = 0; q < passes; ++q) {
     const int p = passes - 1 - q;  // anti-diagonal index, descending
-    const int j = p - i + 2;
-    double e = 0.0;
-    if (row_ok && j >= 1 && j <= M) {
-      if (!(bw > 0.f && fabsf((float)(i - j)) > bw)) {
-        const double r = rv(Rp, i, j, N, M);
-        const double d_down = (i + 1 <= N) ? (double)Dp[(long long)i * pi.ld + (j - 1)] : 0.0;
-        const double d_right = (j + 1 <= M) ? (double)Dp[(long long)(i - 1) * pi.ld + j] : 0.0;
-        const double d_diag = (i + 1 <= N && j + 1 <= M) ? (double)Dp[(long long)i * pi.ld + j] : 0.0;
-        const double a = exp((rv(Rp, i + 1, j, N, M) - r - d_down) * inv_g);
-        const double bb = exp((rv(Rp, i, j + 1, N, M) - r - d_right) * inv_g);
-        const double c = exp((rv(Rp, i + 1, j + 1, N, M) - r - d_diag) * inv_g);
-        // E[i+1][j] from pass p+1 (row below), E[i+1][j+1] from pass p+2; E[N+1][M+1] = 1
-        double e_down, e_diag;
-        if (i == N) {
-          e_down = 0.0;
-          e_diag = (j == M) ? 1.0 : 0.0;
-        } else {
-          e_down = ring[((q + 2) % 3) * S + (i + 1)];
-          e_diag = (j == M) ? 0.0 : ring[((q + 1) % 3) * S + (i + 1)];
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = threadIdx.x + 1 + r * blockDim.x;
+      const bool row_ok = i <= N;
+      const int j = p - i + 2;
+      double e = 0.0;
+      if (row_ok && j >= 1 && j <= M) {
+        if (!(bw > 0.f && fabsf((float)(i - j)) > bw)) {
+          const double rr = rv(Rp, i, j, N, M);
+          const double d_down = (i + 1 <= N) ? (double)Dp[(long long)i * pi.ld + (j - 1)] : 0.0;
+          const double d_right = (j + 1 <= M) ? (double)Dp[(long long)(i - 1) * pi.ld + j] : 0.0;
+          const double d_diag = (i + 1 <= N && j + 1 <= M) ? (double)Dp[(long long)i * pi.ld + j] : 0.0;
+          const double a = exp((rv(Rp, i + 1, j, N, M) - rr - d_down) * inv_g);
+          const double bb = exp((rv(Rp, i, j + 1, N, M) - rr - d_right) * inv_g);
+          const double c = exp((rv(Rp, i + 1, j + 1, N, M) - rr - d_diag) * inv_g);
+          // E[i+1][j] from pass p+1 (row below), E[i+1][j+1] from pass p+2; E[N+1][M+1] = 1
+          double e_down, e_diag;
+          if (i == N) {
+            e_down = 0.0;
+            e_diag = (j == M) ? 1.0 : 0.0;
+          } else {
+            e_down = ring[((q + 2) % 3) * S + (i + 1)];
+            e_diag = (j == M) ? 0.0 : ring[((q + 1) % 3) * S + (i + 1)];
+          }
+          const double e_right = (j == M) ? 0.0 : own_prev[r];
+          e = e_down * a + e_right * bb + e_diag * c;
         }
-        const double e_right = (j == M) ? 0.0 : own_prev;
-        e = e_down * a + e_right * bb + e_diag * c;
+        Gp[(long long)(i - 1) * M + (j - 1)] = (float)(e * g);
+        own_prev[r] = e;
       }
-      Gp[(long long)(i - 1) * M + (j - 1)] = (float)(e * g);
-      own_prev = e;
+      if (row_ok) ring[(q % 3) * S + i] = e;
     }
-    if (row_ok) ring[(q % 3) * S + i] = e;
     __syncthreads();
   }
 }
 
 static int block_for(int n) {
   int t = ((n + 63) / 64) * 64;
-  return t < 64 ? 64 : t;
+  t = t < 64 ? 64 : t;
+  return t > 1024 ? 1024 : t;
 }
+
+static int rows_per_lane(int n) {
+  const int r = (n + 1023) / 1024;
+  return r <= 1 ? 1 : r <= 2 ? 2 : r <= 4 ? 4 : r <= 8 ? 8 : -1;
+}
+
+constexpr int kSdtwMaxN = 6600;  // LDS ring: 3 x (N + 2) doubles <= 160 KiB
 
 MILNCE_API int milnce_softdtw_fwd(const float* D, int B, int N, int M, int ld, int pair_div, long long s_i,
                                   long long s_j, float gamma, float bandwidth, double* R, float* out,
                                   hipStream_t stream) {
-  if (N > 1024) return (int)hipErrorInvalidValue;
+  if (N > kSdtwMaxN) return (int)hipErrorInvalidValue;
   PairIndex pi{pair_div, ld, s_i, s_j};
-  hipLaunchKernelGGL(softdtw_fwd_kernel, dim3(B), dim3(block_for(N)), 3 * (N + 1) * sizeof(double), stream, D, pi, N,
-                     M, gamma, bandwidth, R, out);
-  return (int)hipGetLastError();
+  const size_t lds = 3 * (N + 1) * sizeof(double);
+  const int rpl = rows_per_lane(N);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) HIP_RET(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipLaunchKernelGGL(kern, dim3(B), dim3(block_for(N)), lds, stream, D, pi, N, M, gamma, bandwidth, R, out);
+    return (int)hipGetLastError();
+  };
+  if (rpl == 1) return go(softdtw_fwd_kernel<1>);
+  if (rpl == 2) return go(softdtw_fwd_kernel<2>);
+  if (rpl == 4) return go(softdtw_fwd_kernel<4>);
+  return go(softdtw_fwd_kernel<8>);
 }
 
 MILNCE_API int milnce_softdtw_bwd(const float* D, const double* R, int B, int N, int M, int ld, int pair_div,
                                   long long s_i, long long s_j, float gamma, float bandwidth, const float* gout,
                                   float* G, hipStream_t stream) {
-  if (N > 1024) return (int)hipErrorInvalidValue;
+  if (N > kSdtwMaxN) return (int)hipErrorInvalidValue;
   PairIndex pi{pair_div, ld, s_i, s_j};
-  hipLaunchKernelGGL(softdtw_bwd_kernel, dim3(B), dim3(block_for(N)), 3 * (N + 2) * sizeof(double), stream, D, R, pi,
-                     N, M, gamma, bandwidth, gout, G);
-  return (int)hipGetLastError();
+  const size_t lds = 3 * (N + 2) * sizeof(double);
+  const int rpl = rows_per_lane(N);
+  auto go = [&](auto kern) {
+    if (lds > 64 * 1024) HIP_RET(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    hipLaunchKernelGGL(kern, dim3(B), dim3(block_for(N)), lds, stream, D, R, pi, N, M, gamma, bandwidth, gout, G);
+    return (int)hipGetLastError();
+  };
+  if (rpl == 1) return go(softdtw_bwd_kernel<1>);
+  if (rpl == 2) return go(softdtw_bwd_kernel<2>);
+  if (rpl == 4) return go(softdtw_bwd_kernel<4>);
+  return go(softdtw_bwd_kernel<8>);
 }
 
 // ---------------------------------------------------------------------------------------

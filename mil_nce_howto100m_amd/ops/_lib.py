@@ -72,11 +72,25 @@ def lib():
     return l
 
 
+# MILNCE_DEBUG_SYNC=1: synchronise after every native call so an asynchronous kernel fault is
+# reported at the op that caused it (the analogue of HIP_LAUNCH_BLOCKING for this library), and
+# native calls are counted so the failure names the call index.
+_DEBUG_SYNC = os.environ.get("MILNCE_DEBUG_SYNC", "0") == "1"
+_calls = 0
+
+
 def call(name: str, *args) -> None:
+    global _calls
     fn = getattr(lib(), name)
     rc = fn(*args)
     if rc != 0:
         raise NativeLibraryError(f"{name} failed with hipError {rc}")
+    if _DEBUG_SYNC:
+        _calls += 1
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # the fault surfaced at this op
+            raise NativeLibraryError(f"{name} (native call #{_calls}) faulted asynchronously: {e}") from e
 
 
 def ptr(t) -> int:

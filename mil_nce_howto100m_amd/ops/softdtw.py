@@ -169,16 +169,23 @@ class _SoftDTWHIP(torch.autograd.Function):
         return G, None, None, None
 
 
+GPU_MAX_N = 6600  # csrc/softdtw.hip kSdtwMaxN: the LDS ring holds 3 x (N + 2) doubles
+
+
 def softdtw_from_dist(D: torch.Tensor, gamma: float, bandwidth: float = 0.0) -> torch.Tensor:
-    """Batched soft-DTW value of distance matrices D [B, N, M] -> [B]."""
+    """Batched soft-DTW value of distance matrices D [B, N, M] -> [B]. Longer-than-LDS sequences
+    run on the CPU implementation (the reference falls back to CPU above 1024,
+    ``soft_dtw_cuda.py:318``; the HIP kernel goes to ~6.6k rows)."""
     if use_hip(D):
-        return _SoftDTWHIP.apply(D, gamma, bandwidth, 0)
+        if D.shape[-2] <= GPU_MAX_N:
+            return _SoftDTWHIP.apply(D, gamma, bandwidth, 0)
+        return _SoftDTWCPU.apply(D.cpu(), gamma, bandwidth).to(D.device)
     return _SoftDTWCPU.apply(D, gamma, bandwidth)
 
 
 def softdtw_pairwise_from_dist(Dbig: torch.Tensor, b: int, gamma: float, bandwidth: float = 0.0) -> torch.Tensor:
     """All b*b pairs from one [b*n, b*m] distance matrix -> [b, b], out[i, j] = sdtw(block(i, j))."""
-    if use_hip(Dbig):
+    if use_hip(Dbig) and Dbig.shape[0] // b <= GPU_MAX_N:
         return _SoftDTWHIP.apply(Dbig, gamma, bandwidth, b).view(b, b)
     n, m = Dbig.shape[0] // b, Dbig.shape[1] // b
     D = Dbig.view(b, n, b, m).permute(0, 2, 1, 3).reshape(b * b, n, m)

@@ -241,3 +241,26 @@ def test_sharded_eval_matches_single_process():
         assert np.allclose(rf, f, atol=1e-5) and list(rlab) == list(lab)
         assert all(np.array_equal(a, b) for a, b in zip(rspl, spl))
         assert np.allclose(rt, t, atol=1e-5) and np.allclose(rv, v, atol=1e-5)
+
+
+def test_bench_contract_two_ranks_cpu():
+    """bench.py under torch.distributed.run (the driver's N>1 launch, gloo on CPU here): exactly
+    one JSON line from rank 0 with the whole-job aggregate and the documented keys."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--num_frames", "4", "--size", "32", "--batch_per_gpu", "2", "--blocks", "mixed_3b"]
+    out = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in r, k
+    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["config"]["global_batch"] == 4 and r["config"]["parallelism"] == "dp2"
+    assert abs(r["value"] - 4 * 1000.0 / r["ms_per_step"]) / r["value"] < 1e-2

@@ -366,7 +366,8 @@ def test_paired_width_stem(S):
 
 
 @pytest.mark.parametrize("dist", ["cosine", "negative_dot", None])
-@pytest.mark.parametrize("B,N,M,bw", [(4, 8, 8, 0.0), (3, 17, 15, 0.0), (2, 70, 66, 0.0), (2, 12, 12, 3.0)])
+@pytest.mark.parametrize("B,N,M,bw", [(4, 8, 8, 0.0), (3, 17, 15, 0.0), (2, 70, 66, 0.0), (2, 12, 12, 3.0),
+                                      (1, 1500, 40, 0.0)])
 def test_softdtw_vs_cpu_oracle(dist, B, N, M, bw):
     from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
     torch.manual_seed(7)
