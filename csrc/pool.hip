@@ -168,10 +168,13 @@ struct PoolDivs {
   FastDiv fcpr, fWo, fHo, fTo, fW, fH, fT;
 };
 
-template <int KT, int KH, int KW, int ST, int SH, int SW>
+// BN: x is the raw conv output of a train-mode BN layer and z = relu(x * scale + shift) is
+// pooled without being materialised (ss = [mean, invstd, scale, shift] per channel); padded
+// cells stay zero candidates, as for the z the unfused pool would read.
+template <int KT, int KH, int KW, int ST, int SH, int SW, bool BN = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ x,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
-                                                     uint32_t nout_chunks) {
+                                                     uint32_t nout_chunks, const float* __restrict__ ss = nullptr) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nout_chunks; i += gridDim.x * blockDim.x) {
     uint32_t r = fdiv(i, d.fcpr);
     const int c0 = (int)(i - r * d.fcpr.d) * 8;
@@ -199,14 +202,25 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
           const size_t off = in[t] ? ((size_t)(ti * p.H + hi) * p.W + wi) * p.C : 0;
           v[t] = *(const uint4*)(xb + off);
         }
-    float best[8];
+    float best[8], sc[8], sh[8];
     uint32_t bi[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { best[k] = -INFINITY; bi[k] = 0; }
+    for (int k = 0; k < 8; ++k) {
+      best[k] = -INFINITY;
+      bi[k] = 0;
+      if constexpr (BN) {
+        sc[k] = ss[2 * p.C + c0 + k];
+        sh[k] = ss[3 * p.C + c0 + k];
+      }
+    }
 #pragma unroll
     for (int t = 0; t < KT * KH * KW; ++t) {
       float f[8];
       unpack8(v[t], f);
+      if constexpr (BN) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float val = in[t] ? f[k] : (cand[t] ? 0.f : -INFINITY);
@@ -496,9 +510,23 @@ static bool is_s1_333(const PoolParams& p) {
          p.pw == 1 && !p.zero_pad && p.To == p.T && p.Ho == p.H && p.Wo == p.W;
 }
 
-static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s) {
+static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s,
+                             const float* bn_ss = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
+  if (bn_ss != nullptr) {
+    long long g = (n + 255) / 256;
+    const int grid = (int)(g > 65536 ? 65536 : g);
+#define X(a, b, c, e, f, h)                                                                                      \
+    if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                            \
+      hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true>), dim3(grid), dim3(256), 0, s, p, d,             \
+                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss);                       \
+      return true;                                                                                               \
+    }
+    MILNCE_POOL_SHAPES(X)
+#undef X
+    return false;
+  }
   if (is_s1_333(p)) {
     const long long rows = n / p.W / (p.C / 8);  // n = B*T*H*W*cpr
     const long long thr = rows * (p.C / 8);
@@ -571,6 +599,19 @@ MILNCE_API int milnce_maxpool_fwd(const void* x, void* y, void* arg, int B, int 
   if (pool_fwd_special(p, x, y, arg, n, stream)) return (int)hipGetLastError();
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, stream, p, (const bf16_t*)x,
                      (bf16_t*)y, (uint8_t*)arg, n);
+  return (int)hipGetLastError();
+}
+
+// Train-mode BN + ReLU + max pool in one pass over the raw conv output (specialised window
+// shapes only; returns hipErrorInvalidValue otherwise).
+MILNCE_API int milnce_bn_relu_maxpool_fwd(const void* x, const float* ss, void* y, void* arg, int B, int T, int H,
+                                          int W, int C, int To, int Ho, int Wo, int kt, int kh, int kw, int st,
+                                          int sh, int sw, int pt0, int pt1, int ph0, int ph1, int pw0, int pw1,
+                                          int zero_pad, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
+  const long long n = (long long)B * To * Ho * Wo * (C / 8);
+  if (!pool_fwd_special(p, x, y, arg, n, stream, ss)) return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

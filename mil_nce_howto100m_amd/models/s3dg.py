@@ -224,12 +224,15 @@ class S3D(nn.Module):
             net = ops.space_to_depth(net)
             net = self.conv1(net)
         elif net.is_cuda and ops.use_hip(net):
-            net = ops.stem_conv_bn_relu(net, self.conv1.conv1.weight, self.conv1.bn1, self.training)
+            # stem + BN + ReLU + maxpool_2a in one op: the full-resolution ReLU output is never stored
+            net = ops.stem_conv_bn_relu_pool(net, self.conv1.conv1.weight, self.conv1.bn1, self.training,
+                                             *self.maxpool_2a)
         else:
             net = self.conv1(net)
         if self.space_to_depth:
             net = net[:, 1:, 1:, 1:, :].contiguous()
-        net = ops.maxpool_tf_same(net, *self.maxpool_2a)
+        if not (net.is_cuda and ops.use_hip(net) and not self.space_to_depth):
+            net = ops.maxpool_tf_same(net, *self.maxpool_2a)
         net = self.conv_2b(net)
         net, gsum = self.conv_2c(net, want_gsum=True)
         net = self.gating(net, gsum)

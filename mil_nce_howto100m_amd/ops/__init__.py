@@ -55,6 +55,11 @@ def stem_conv_bn_relu(x, weight, bn, training: bool):
     return _hip().stem_conv_bn_relu(x, weight, bn, training)
 
 
+def stem_conv_bn_relu_pool(x, weight, bn, training: bool, pool_k, pool_s):
+    """Stem unit + maxpool_2a in one fused op (GPU)."""
+    return _hip().stem_conv_bn_relu_pool(x, weight, bn, training, pool_k, pool_s)
+
+
 def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = False):
     """Several 1x1x1 conv -> BN -> ReLU units on the same input (one fused GEMM on GPU).
     Returns the list of outputs and the gating sum of the first (None on the ATen path)."""

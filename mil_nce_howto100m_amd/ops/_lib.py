@@ -33,6 +33,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_avgpool_bwd": [P, I, I, I, P, P],
     "milnce_maxpool_fwd": [P, P, P] + [I] * 21 + [P],
     "milnce_maxpool_bwd": [P, P, P] + [I] * 21 + [P, I, P, P, I, P],
+    "milnce_bn_relu_maxpool_fwd": [P, P, P, P] + [I] * 21 + [P],
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],

@@ -287,22 +287,74 @@ def _bn_nparts(M: int) -> int:
     return int(max(1, min(2048, max(min(1024, _ceil(M, 64)), _ceil(M, 2048)))))
 
 
+def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
+                   wo_override=0):
+    """conv (statistics epilogue) + BN finalize: returns (plan, raw conv output y, ss)."""
+    plan = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
+    dev = x.device
+    wp = _pack(weight, plan, 0)
+    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+    y = conv_forward_raw(x, wp, plan, stats)
+    C = plan.Cout
+    ss = torch.empty((4 * C,), dtype=F32, device=dev)
+    call("milnce_bn_finalize", ptr(stats), plan.grid_m, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
+         ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(momentum), float(eps), int(training),
+         ptr(ss), stream())
+    return plan, y, ss
+
+
+def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
+    """Backward of conv -> BN -> ReLU from dz (grad of the ReLU output): BN backward (fused
+    partials when the producer of dz attached them), dgrad, wgrad; BN and weight gradients are
+    accumulated in place into flat-buffer grads when possible."""
+    plan: ConvPlan = ctx.plan
+    dz = dz.contiguous()
+    C = plan.Cout
+    dev = dz.device
+    fused = take_bn_partials(dz)
+    if fused is not None:
+        part, nparts, ps = fused
+    else:
+        nparts = _bn_nparts(plan.M)
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
+        ps = C
+    coef = torch.empty((3 * C,), dtype=F32, device=dev)
+    beta = ctx.beta
+    g_direct, b_direct = _direct_grad(gamma), _direct_grad(beta)
+    direct_bn = g_direct is not None and b_direct is not None
+    dgamma = g_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
+    dbeta = b_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
+    dy = torch.empty_like(y)
+    call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
+         int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, int(direct_bn),
+         int(ctx.training), stream())
+    if direct_bn:
+        _grad_done(gamma)
+        _grad_done(beta)
+        dgamma = dbeta = None
+    dx = None
+    if ctx.needs_input_grad[0]:
+        wd = _pack(weight, plan, 1)
+        dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
+    dw = None
+    if ctx.needs_input_grad[1]:
+        w_direct = _direct_grad(weight)
+        dw = conv_wgrad(dy, x, plan, out=w_direct)
+        if w_direct is not None:
+            _grad_done(weight)
+            dw = None
+    return dx, dw, dgamma, dbeta
+
+
 class _ConvBNReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
                 want_gsum, wo_override=0):
-        plan = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
-        dev = x.device
-        wp = _pack(weight, plan, 0)
-        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
-        y = conv_forward_raw(x, wp, plan, stats)
+        plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
+                                     training, wo_override)
         C = plan.Cout
-        ss = torch.empty((4 * C,), dtype=F32, device=dev)
-        call("milnce_bn_finalize", ptr(stats), plan.grid_m, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
-             ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(momentum), float(eps), int(training),
-             ptr(ss), stream())
         z = torch.empty_like(y)
-        gsum = torch.zeros((plan.B, C), dtype=F32, device=dev) if want_gsum else None
+        gsum = torch.zeros((plan.B, C), dtype=F32, device=x.device) if want_gsum else None
         call("milnce_bn_relu_apply", ptr(y), C, ptr(z), C, ptr(ss), C, plan.B, plan.To * plan.Ho * plan.Wo,
              ptr(gsum), stream())
         ctx.save_for_backward(x, weight, y, ss, gamma)
@@ -319,43 +371,51 @@ class _ConvBNReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, *unused):
         x, weight, y, ss, gamma = ctx.saved_tensors
-        plan: ConvPlan = ctx.plan
-        dz = dz.contiguous()
-        C = plan.Cout
-        dev = dz.device
-        fused = take_bn_partials(dz)
-        if fused is not None:
-            part, nparts, ps = fused
-        else:
-            nparts = _bn_nparts(plan.M)
-            part = torch.empty((nparts * 2 * C,), dtype=F32, device=dev)
-            ps = C
-        coef = torch.empty((3 * C,), dtype=F32, device=dev)
-        beta = ctx.beta
-        g_direct, b_direct = _direct_grad(gamma), _direct_grad(beta)
-        direct_bn = g_direct is not None and b_direct is not None
-        dgamma = g_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
-        dbeta = b_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
-        dy = torch.empty_like(y)
-        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
-             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, int(direct_bn),
-             int(ctx.training), stream())
-        if direct_bn:
-            _grad_done(gamma)
-            _grad_done(beta)
-            dgamma = dbeta = None
-        dx = None
-        if ctx.needs_input_grad[0]:
-            wd = _pack(weight, plan, 1)
-            dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
-        dw = None
-        if ctx.needs_input_grad[1]:
-            w_direct = _direct_grad(weight)
-            dw = conv_wgrad(dy, x, plan, out=w_direct)
-            if w_direct is not None:
-                _grad_done(weight)
-                dw = None
+        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
+
+
+class _ConvBNReLUPool(torch.autograd.Function):
+    """conv -> BN -> ReLU -> TF-SAME max pool (the stem and maxpool_2a, ``s3dg.py:226-228``)
+    with the BN+ReLU applied inside the pool's loads: the full-resolution ReLU output is never
+    written. Backward: pool backward (dz at full resolution, with the BN-backward partial
+    sums), then the conv-BN backward."""
+
+    @staticmethod
+    def forward(ctx, x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
+                wo_override, pool_k, pool_s):
+        plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
+                                     training, wo_override)
+        B, T, H, W, C = plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout
+        pads = aten.tf_same_pad(pool_k, pool_s)
+        To = _pool_out(T, pool_k[0], pool_s[0], *pads[0])
+        Ho = _pool_out(H, pool_k[1], pool_s[1], *pads[1])
+        Wo = _pool_out(W, pool_k[2], pool_s[2], *pads[2])
+        out = torch.empty((B, To, Ho, Wo, C), dtype=BF16, device=x.device)
+        arg = torch.empty((B, To, Ho, Wo, C), dtype=torch.uint8, device=x.device)
+        geo = [B, T, H, W, C, To, Ho, Wo, *pool_k, *pool_s, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
+               pads[2][0], pads[2][1], 1]
+        call("milnce_bn_relu_maxpool_fwd", ptr(y), ptr(ss), ptr(out), ptr(arg), *geo, stream())
+        ctx.save_for_backward(x, weight, y, ss, gamma, arg)
+        ctx.beta = beta
+        ctx.training = bool(training)
+        ctx.plan, ctx.geo = plan, geo
+        ctx.x_bn = getattr(x, "_milnce_bn", None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, weight, y, ss, gamma, arg = ctx.saved_tensors
+        geo = ctx.geo
+        B, T, H, W, C = geo[:5]
+        dz = torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
+        nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
+        call("milnce_maxpool_bwd", ptr(dout.contiguous()), ptr(arg), ptr(dz), *geo, ptr(y), C, ptr(ss), ptr(part),
+             nparts, stream())
+        attach_bn_partials(dz, part, nparts, C)
+        dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
 
 
 def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
@@ -396,6 +456,23 @@ def _stem_pair_map(device) -> Tuple[torch.Tensor, torch.Tensor]:
     hit = (idx.reshape(-1).to(device), mask.reshape(-1).to(device))
     _STEM_MAP[device] = hit
     return hit
+
+
+def stem_conv_bn_relu_pool(x, weight, bn, training: bool, pool_k, pool_s):
+    """The stem unit followed by its TF-SAME max pool (maxpool_2a), fused: see
+    ``_ConvBNReLUPool`` and ``stem_conv_bn_relu``."""
+    B, T, H, W, C = x.shape
+    if C != 4 or W % 2 or tuple(weight.shape) != (64, 3, 3, 7, 7) or x.dtype != BF16:
+        raise ValueError(f"stem expects bf16 [B,T,H,W even,4] and a (64,3,3,7,7) weight, got {tuple(x.shape)}")
+    idx, mask = _stem_pair_map(x.device)
+    cout = weight.shape[0]
+    w2 = (weight.reshape(cout, -1).index_select(1, idx) * mask).view(cout, 8, 3, 7, 4)
+    x2 = x.contiguous().view(B, T, H, W // 2, 8)
+    wo = (W + 2 * 3 - 7) // 2 + 1
+    momentum = bn.momentum if bn.momentum is not None else 0.1
+    return _ConvBNReLUPool.apply(x2, w2, bn.weight, bn.bias, bn.running_mean, bn.running_var,
+                                 bn.num_batches_tracked, (2, 2, 1), (1, 3, 2), momentum, bn.eps, bool(training), wo,
+                                 tuple(pool_k), tuple(pool_s))
 
 
 def stem_conv_bn_relu(x, weight, bn, training: bool):

@@ -365,6 +365,30 @@ def test_paired_width_stem(S):
     assert torch.allclose(bn.running_mean, bn_ref.running_mean, rtol=2e-2, atol=2e-3)
 
 
+def test_stem_bn_relu_pool_fused_matches_unfused():
+    """stem -> BN -> ReLU -> maxpool_2a with BN+ReLU applied inside the pool == the two ops."""
+    torch.manual_seed(9)
+    h = hip()
+    u8 = torch.randint(0, 256, (2, 6, 24, 24, 4), dtype=torch.uint8, device=DEV)
+    u8[..., 3] = 0
+    x = h.prepare_stem_input(u8, native=True)
+    conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
+    bns = [nn.BatchNorm3d(64).to(DEV) for _ in range(2)]
+    bns[1].load_state_dict(bns[0].state_dict())
+    w1 = conv.weight.detach().clone().requires_grad_(True)
+    w2 = conv.weight.detach().clone().requires_grad_(True)
+    out_f = h.stem_conv_bn_relu_pool(x, w1, bns[0], True, (1, 3, 3), (1, 2, 2))
+    out_u = h.maxpool3d(h.stem_conv_bn_relu(x, w2, bns[1], True), (1, 3, 3), (1, 2, 2), True)
+    assert torch.equal(out_f, out_u)
+    g = torch.randn_like(out_f.float()).to(torch.bfloat16)
+    out_f.backward(g)
+    out_u.backward(g)
+    assert rel_err(w1.grad, w2.grad) < 1e-3
+    assert rel_err(bns[0].weight.grad, bns[1].weight.grad) < 1e-3
+    assert rel_err(bns[0].bias.grad, bns[1].bias.grad) < 1e-3
+    assert torch.equal(bns[0].running_mean, bns[1].running_mean)
+
+
 @pytest.mark.parametrize("dist", ["cosine", "negative_dot", None])
 @pytest.mark.parametrize("B,N,M,bw", [(4, 8, 8, 0.0), (3, 17, 15, 0.0), (2, 70, 66, 0.0), (2, 12, 12, 3.0),
                                       (1, 1500, 40, 0.0)])
