@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
       unpack8(v[t], f);
       if constexpr (BN) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
+        for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f)));  // = the stored z
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
