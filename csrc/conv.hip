@@ -403,15 +403,28 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
 // source chunk that belongs in its slot. Wave w's j-th DMA of a tile covers rows
 // j*4*RPI + w*RPI + lane/CPR, so the swizzle term -- and hence the lane's k chunk and its
 // (tap, channel) -- is the same for all of the lane's rows: one tap lookup per stage.
-__device__ __forceinline__ void wait_vmcnt_le(int n) {
-  // n is one of a few compile-time values at every call site (see the callers)
-  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if (n <= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if (n <= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if (n <= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if (n <= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else if (n <= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+// Workgroup barrier for the LDS-DMA rings. __builtin_amdgcn_s_barrier() is not a memory barrier
+// for the compiler (LDS reads could be hoisted above it, i.e. before other waves' DMA pieces
+// for the stage have landed), and __syncthreads() would add a vmcnt(0) that drains the ring.
+// One asm statement with a memory clobber orders both: this wave's LDS reads of the previous
+// stage are complete (lgkmcnt(0)) and no LDS access moves across the barrier.
+__device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Wait until at most N vector-memory operations (here: LDS-DMA pieces) of this wave are
+// outstanding. N must be exact (rounding up would let a piece of the stage about to be read
+// still be in flight), so it is a template constant; wait_stages picks N = ahead * NDMA.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NDMA, int MAXAHEAD>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  static_assert(MAXAHEAD <= 2, "ring depth");
+  if (ahead <= 0) wait_vmcnt<0>();
+  else if (ahead == 1 || MAXAHEAD < 2) wait_vmcnt<NDMA>();
+  else wait_vmcnt<(MAXAHEAD >= 2 ? 2 * NDMA : 0)>();
 }
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -428,7 +441,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   constexpr int A_INST = BM / RPI / NWAVES;  // DMA instructions per wave per stage (A)
   constexpr int B_INST = BN / RPI / NWAVES;  // (B)
   constexpr int NDMA = A_INST + B_INST;
-  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int WM = BM / NWM, WN = BN / 2;  // wave tile: 64 rows x BN/2
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int KSTEPS = BK / 32;
   constexpr int LDE = BN + 8;
@@ -560,8 +573,8 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
     for (int kt = 0; kt < nk; ++kt) {
       // stage kt must have landed: later stages (issued: min(nk-1, kt+STAGES-2) - kt of them) may stay in flight
       const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
-      wait_vmcnt_le(ahead * NDMA);
-      __builtin_amdgcn_s_barrier();
+      wait_stages<NDMA, STAGES - 2>(ahead);
+      ring_barrier();
       if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
       const bf16_t* a = ring + (kt % STAGES) * STAGE_ELEMS;
       const bf16_t* bsh = a + BM * BK;
@@ -1111,8 +1124,8 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
   }
   for (int s = 0; s < nsteps; ++s) {
     const int ahead = min(nsteps - 1, s + STAGES - 2) - s;
-    wait_vmcnt_le(ahead * NDMA);
-    __builtin_amdgcn_s_barrier();
+    wait_stages<NDMA, STAGES - 2>(ahead);
+    ring_barrier();
     if (s + STAGES - 1 < nsteps) issue(s + STAGES - 1);
     const bf16_t* d = ring + (s % STAGES) * STAGE_ELEMS;
     const bf16_t* x = d + R * TN_;

@@ -18,6 +18,7 @@ followed by a ``k x 1 x 1`` conv, both Cin->Cout dense (``s3dg.py:74-99``), not 
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -25,6 +26,9 @@ import torch.nn as nn
 
 from .. import ops
 from .text import SentenceEmbedding
+
+
+_FUSE_STEM_POOL = os.environ.get("MILNCE_FUSE_STEM_POOL", "1") != "0"
 
 
 def _triple(v) -> Tuple[int, int, int]:
@@ -220,18 +224,22 @@ class S3D(nn.Module):
 
     def forward_video(self, inputs, mixed5c=False):
         net = self.prepare_video(inputs)
+        pooled = False
         if self.space_to_depth:
             net = ops.space_to_depth(net)
             net = self.conv1(net)
-        elif net.is_cuda and ops.use_hip(net):
+        elif net.is_cuda and ops.use_hip(net) and _FUSE_STEM_POOL:
             # stem + BN + ReLU + maxpool_2a in one op: the full-resolution ReLU output is never stored
             net = ops.stem_conv_bn_relu_pool(net, self.conv1.conv1.weight, self.conv1.bn1, self.training,
                                              *self.maxpool_2a)
+            pooled = True
+        elif net.is_cuda and ops.use_hip(net):
+            net = ops.stem_conv_bn_relu(net, self.conv1.conv1.weight, self.conv1.bn1, self.training)
         else:
             net = self.conv1(net)
         if self.space_to_depth:
             net = net[:, 1:, 1:, 1:, :].contiguous()
-        if not (net.is_cuda and ops.use_hip(net) and not self.space_to_depth):
+        if not pooled:
             net = ops.maxpool_tf_same(net, *self.maxpool_2a)
         net = self.conv_2b(net)
         net, gsum = self.conv_2c(net, want_gsum=True)

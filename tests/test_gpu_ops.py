@@ -75,6 +75,49 @@ def test_conv_fwd_dgrad_wgrad(case):
     assert rel_err(dw, wr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 192, (3, 1, 1), (1, 0, 0)),
+                                          (256, 288, (1, 1, 1), (0, 0, 0))])
+def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
+    """Every forward / dgrad / wgrad kernel variant the autotuner may pick computes the same sums
+    in the same order: outputs must be bitwise identical, on a problem large enough (8 clips of
+    8x50x50) that an LDS-ring race or a pipeline hazard would show up. Run twice for determinism."""
+    torch.manual_seed(12)
+    h = hip()
+    x = torch.randn(8, 8, 50, 50, cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(cout, cin, *k, device=DEV) * 0.05
+    plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), p)
+    wp = h._pack(w, plan, 0)
+    wd = h._pack(w, plan, 1)
+    dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
+    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device=DEV)
+    outs = {}
+    for impl in h._IMPLS:
+        plan.impl = plan.d_impl = impl
+        for rep in range(2):
+            y = h.conv_forward_raw(x, wp, plan, stats)
+            st = stats.clone()
+            dx = h.conv_dgrad(dy, wd, plan)
+            outs[(impl, rep)] = (y, st, dx)
+    ref = outs[(2, 0)]
+    npad = plan.Npad
+    ref_sums = ref[1].view(-1, 2, npad).double().sum(0)
+    for key, val in outs.items():
+        assert torch.equal(val[0], ref[0]), ("y", key)
+        assert torch.equal(val[2], ref[2]), ("dx", key)
+        # BN statistics partials: per-block rows depend on the tile height (256-row variants 6/7
+        # group rows differently), their column sums must agree
+        sums = val[1].view(-1, 2, npad).double().sum(0)
+        assert torch.allclose(sums, ref_sums, rtol=1e-5, atol=1e-3), ("stats", key)
+    dws = []
+    for impl in h._W_IMPLS:
+        plan.w_impl = impl
+        for rep in range(2):
+            dws.append(h.conv_wgrad(dy, x, plan))
+    for d in dws[1:]:
+        assert torch.equal(d, dws[0])
+    plan.impl = plan.d_impl = plan.w_impl = 0
+
+
 def test_stem_uint8():
     torch.manual_seed(0)
     h = hip()
