@@ -117,3 +117,24 @@ def test_hip_graph_eval_forward_matches_eager():
                 f(v)
             torch.cuda.synchronize()
             print(f"{'graph' if f is g else 'eager'}: {(time.perf_counter() - t0) * 100:.2f} ms/forward")
+
+
+def test_full_model_loss_matches_aten_at_batch_32():
+    """Whole S3D-G + text tower + MIL-NCE at a batch large enough to exercise every autotuned
+    kernel variant / persistent-tile path: the HIP loss equals the ATen (MIOpen) bf16 loss."""
+    from mil_nce_howto100m_amd import ops
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    from mil_nce_howto100m_amd.models import S3D
+    torch.manual_seed(3)
+    m = S3D(512, vocab_size=2000).cuda().train()
+    m_aten = copy.deepcopy(m)
+    data = SyntheticClips(32, 8, 112, 2, 20, 2000, device=torch.device("cuda"))
+    b = data.batch(0)
+    text = b["text"].reshape(-1, b["text"].shape[-1])
+    with torch.no_grad():
+        v, t = m(b["video"], text)
+        loss = float(ops.milnce_loss(v.float(), t.float()))
+        with ops.force_aten():
+            va, ta = m_aten(b["video"], text)
+            loss_a = float(ops.milnce_loss(va.float(), ta.float()))
+    assert abs(loss - loss_a) < 0.02 * abs(loss_a), (loss, loss_a)
