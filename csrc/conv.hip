@@ -485,14 +485,10 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   }
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long long)p.num_n_tiles * BN * p.Kpad * 2),
                                                      0x00020000);
-  float st_s[TN][4], st_q[TN][4];
+  // per-thread partial sums of its fixed output chunk column: EPI 1 (sum y, sum y^2) / EPI 2
   float e_s[8], e_q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { st_s[j][r] = 0.f; st_q[j][r] = 0.f; }
 
   for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
     const int m0 = m_tile * BM;
@@ -605,19 +601,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wr * WM + i * 16 + (lane & 15);
-      const bool rv = (m0 + row) < p.M;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const f32x4 v = acc[j][i];
-        if constexpr (EPI == 1) {
-          if (rv) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              st_s[j][r] += v[r];
-              st_q[j][r] += v[r] * v[r];
-            }
-          }
-        }
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
@@ -626,33 +612,49 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
       }
     }
     __syncthreads();
+    // store: thread = fixed 16-B chunk column cc of RPP rows per pass (BN/8 need not divide the
+    // block size; the EPI 2 partials then accumulate per fixed channel chunk)
     constexpr int OCPR = BN / 8;
+    constexpr int RPP = NT / OCPR;  // rows per pass
+    const int cc = tid % OCPR;
+    if (tid < RPP * OCPR) {
+#pragma unroll 4
+      for (int row = tid / OCPR; row < BM; row += RPP) {
+        const int m = m0 + row, n = n0 + cc * 8;
+        const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
+        const bool ok = (m < p.M) & (n < p.Cout);
+        if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
+        if constexpr (EPI == 1) {
+          // BN statistics of the values actually stored (bf16), as a bf16 BN layer would see them
+          if (ok) {
+            float d8[8];
+            unpack8(dv, d8);
 #pragma unroll
-    for (int it = 0; it < BM * OCPR / NT; ++it) {
-      const int cid = tid + it * NT;
-      const int row = cid / OCPR, cc = cid % OCPR;
-      const int m = m0 + row, n = n0 + cc * 8;
-      const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
-      const bool ok = (m < p.M) & (n < p.Cout);
-      if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
-      if constexpr (EPI == 2) {
-        if (ok) {
-          float d8[8], y8[8];
-          unpack8(dv, d8);
-          unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
+            for (int k = 0; k < 8; ++k) {
+              e_s[k] += d8[k];
+              e_q[k] += d8[k] * d8[k];
+            }
+          }
+        }
+        if constexpr (EPI == 2) {
+          if (ok) {
+            float d8[8], y8[8];
+            unpack8(dv, d8);
+            unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int cl = cc * 8 + k;
-            const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
-            e_s[k] += gm;
-            e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
+            for (int k = 0; k < 8; ++k) {
+              const int cl = cc * 8 + k;
+              const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
+              e_s[k] += gm;
+              e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
+            }
           }
         }
       }
     }
   }
 
-  if constexpr (EPI == 2) {
+  if constexpr (EPI != 0) {
     constexpr int OCPR = BN / 8;
     __syncthreads();
     float* red = (float*)smem;  // [2][8][NT]
@@ -661,60 +663,15 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
     __syncthreads();
     if (tid < OCPR) {
       const int npad = p.num_n_tiles * BN;
+      constexpr int ACT = (NT / OCPR) * OCPR;  // threads that stored (the rest hold zeros)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float s1 = 0.f, s2 = 0.f;
-        for (int j = tid; j < NT; j += OCPR) { s1 += red[k * NT + j]; s2 += red[(8 + k) * NT + j]; }
+        for (int j = tid; j < ACT; j += OCPR) { s1 += red[k * NT + j]; s2 += red[(8 + k) * NT + j]; }
         const int col = n0 + tid * 8 + k;
         p.stats[(long long)m_slot * 2 * npad + col] = s1;
         p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
       }
-    }
-  }
-  if constexpr (EPI == 1) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = st_s[j][r], q = st_q[j][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          s += __shfl_xor(s, o, 64);
-          q += __shfl_xor(q, o, 64);
-        }
-        st_s[j][r] = s;
-        st_q[j][r] = q;
-      }
-    __syncthreads();
-    float* red = (float*)smem;  // [NWM (wr)][2 (wc)][2 (s,q)][WN]
-    if ((lane & 15) == 0) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = j * 16 + (lane >> 4) * 4 + r;
-          red[((wr * 2 + wc) * 2 + 0) * WN + c] = st_s[j][r];
-          red[((wr * 2 + wc) * 2 + 1) * WN + c] = st_q[j][r];
-        }
-    }
-    __syncthreads();
-    if (wr == 0 && (lane & 15) == 0) {
-      const int npad = p.num_n_tiles * BN;
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = j * 16 + (lane >> 4) * 4 + r;
-          const int col = n0 + wc * WN + c;
-          float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-          for (int w2 = 0; w2 < NWM; ++w2) {
-            s1 += red[((w2 * 2 + wc) * 2 + 0) * WN + c];
-            s2 += red[((w2 * 2 + wc) * 2 + 1) * WN + c];
-          }
-          p.stats[(long long)m_slot * 2 * npad + col] = s1;
-          p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
-        }
     }
   }
 }
@@ -1315,6 +1272,14 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.fCin = make_fastdiv(Cin);
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
+  if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
+    // wide / odd N tiles: LDS-DMA ring variants only, BK 64
+    if (bk != 64) return (int)hipErrorInvalidValue;
+    const int im = impl == 3 ? 3 : 4;
+    if (bn == 96) return launch_v3_impl<96, 64>(p, im, stream);
+    if (bn == 160) return launch_v3_impl<160, 64>(p, im, stream);
+    return launch_v3_impl<192, 64>(p, im, stream);
+  }
   if (x_u8) {
     if (bn == 64 && bk == 32) return launch_fwd<128, 64, 32, true>(p, impl, stream);
     if (bn == 64 && bk == 64) return launch_fwd<128, 64, 64, true>(p, impl, stream);

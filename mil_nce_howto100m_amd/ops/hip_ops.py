@@ -73,9 +73,21 @@ _PLANS: Dict[tuple, ConvPlan] = {}
 _NUM_CU = 256
 
 
+_WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (csrc/conv.hip)
+
+
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
-    bn = 128 if N > 64 else 64
-    bk = 64 if K >= 128 else 32
+    """N tile from {64, 96, 128, 160, 192}: least padded work, discounted for the lower operand
+    reuse of narrow tiles (ties: the wider), e.g. 192 -> one 192 tile instead of two 128 tiles
+    (25 % padding), 320 -> two 160s, 448 -> three 160s, 832 -> seven 128s."""
+    eff = {192: 1.0, 160: 1.0, 128: 1.0, 96: 0.9, 64: 0.8}
+    best = None
+    for cand in (192, 160, 128, 96, 64):
+        cost = _ceil(N, cand) * cand / eff[cand]
+        if best is None or cost < best[1] - 1e-9:
+            best = (cand, cost)
+    bn = best[0]
+    bk = 64 if (K >= 128 or bn in _WIDE_BN) else 32
     npad = _ceil(N, bn) * bn
     kpad = _ceil(K, bk) * bk
     m_tiles = _ceil(M, 128)
@@ -178,7 +190,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
              plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, impl, stream())
 
     if plan.impl == 0:
-        plan.impl = _tune(launch) if x.dtype != torch.uint8 else 2
+        plan.impl = (_tune(launch, (3, 4) if plan.bn in _WIDE_BN else _IMPLS) if x.dtype != torch.uint8 else 2)
     launch(plan.impl)
     return y
 
@@ -203,7 +215,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl = _tune(launch)
+        plan.d_impl = _tune(launch, (3, 4) if plan.d_bn in _WIDE_BN else _IMPLS)
     launch(plan.d_impl)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)

@@ -98,7 +98,7 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
             st = stats.clone()
             dx = h.conv_dgrad(dy, wd, plan)
             outs[(impl, rep)] = (y, st, dx)
-    ref = outs[(2, 0)]
+    ref = outs[(4, 0)]
     npad = plan.Npad
     ref_sums = ref[1].view(-1, 2, npad).double().sum(0)
     for key, val in outs.items():
@@ -107,7 +107,8 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
         # BN statistics partials: per-block rows depend on the tile height (256-row variants 6/7
         # group rows differently), their column sums must agree
         sums = val[1].view(-1, 2, npad).double().sum(0)
-        assert torch.allclose(sums, ref_sums, rtol=1e-5, atol=1e-3), ("stats", key)
+        # (the LDS-DMA variants sum the stored bf16 outputs, the register-staged one the fp32 ones)
+        assert torch.allclose(sums, ref_sums, rtol=5e-3, atol=5e-2), ("stats", key)
     dws = []
     for impl in h._W_IMPLS:
         plan.w_impl = impl
