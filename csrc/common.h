@@ -84,6 +84,11 @@ __device__ __forceinline__ int xcd_remap(int id, int nblocks) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS ops (lgkmcnt(0)) and
+// s_barrier, with a compiler memory clobber. Unlike __syncthreads() it does not drain
+// outstanding global loads (vmcnt), so register prefetches stay in flight across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 #define HIP_RET(expr)                           \
   do {                                          \
     hipError_t _e = (expr);                     \

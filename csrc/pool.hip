@@ -494,6 +494,305 @@ __global__ __launch_bounds__(256) void maxpool_s1_bwd_slide(PoolParams p, PoolDi
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stride-1 3x3x3 pool as three separable 1-D max stages on an LDS plane sweep.
+//
+//   m1 = max_dw x(w+dw-1),  m2 = max_dh m1(h+dh-1),  y = max_dt m2(t+dt-1)   (-inf padding)
+//
+// each stage keeping its FIRST maximum. The routing y -> m2 (dt*) -> m1 (dh*) -> x (dw*) picks the
+// lexicographically first (dt, dh, dw) among the window's maxima, i.e. exactly ATen's first
+// maximum in (t, h, w) scan order, and the three 2-bit stage codes of a grid position share
+// one byte: code = dw* of m1 | dh* of m2 << 2 | dt* of y << 4 (all at that position).
+// Forward: ~3 compares per element and stage instead of 27; backward: three 1-D 3-candidate
+// gathers instead of testing 27 candidate windows per input element.
+//
+// Layout: one workgroup owns clip b and a chunk of G 8-channel groups over the WHOLE (t, h)
+// plane (thread = (row r = t*H + h, group g)) and sweeps along w; the w stage runs in
+// registers (sliding window), the h and t stages exchange one column through LDS. Every
+// element is fetched from memory once, all memory ops are buffer ops on per-clip descriptors
+// with out-of-range offsets for idle lanes (branch-free, so counted vmcnt waits keep the
+// prefetches in flight across the LDS-only barriers), and the workgroup owns complete
+// (clip, channel) planes, so plane sums need no atomics. Requires T*H*G <= 512.
+struct S1Geo {
+  int rows, G, nchunk, b, chunk, r, g, t, h;
+  bool active;
+  uint32_t e0;  // element offset (in the clip) of this thread's column 0, or out of range
+};
+
+__device__ __forceinline__ S1Geo s1_geo(const PoolParams& p, int G, int nchunk) {
+  S1Geo s;
+  s.rows = p.T * p.H;
+  s.G = G;
+  s.nchunk = nchunk;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the chunks of a clip share cache lines: one L2
+  s.b = bid / nchunk;
+  s.chunk = bid - s.b * nchunk;
+  s.r = threadIdx.x / G;
+  s.g = threadIdx.x - s.r * G;
+  const int cg = s.chunk * G + s.g;
+  s.active = s.r < s.rows && cg < (p.C >> 3);
+  s.t = s.r / p.H;
+  s.h = s.r - s.t * p.H;
+  s.e0 = s.active ? (uint32_t)(s.r * p.W * p.C + cg * 8) : 0x40000000u;
+  return s;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const void* base, int nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);
+}
+
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 0));
+}
+__device__ __forceinline__ uint2 bld8(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
+  return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, byte_off, 0, 0));
+}
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off, uint4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, v), rs,
+                                         byte_off, 0, 0);
+}
+__device__ __forceinline__ void bst8(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off, uint2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, v), rs,
+                                        byte_off, 0, 0);
+}
+
+// first maximum over three candidates (invalid ones skipped), per channel: value and code 0..2
+__device__ __forceinline__ void max3(const float* a, bool va, const float* b, bool vb, const float* c, bool vc,
+                                     float* out, uint32_t* code) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float m = va ? a[k] : -INFINITY;
+    uint32_t cd = 0;
+    if (vb && b[k] > m) { m = b[k]; cd = 1; }
+    if (vc && c[k] > m) { m = c[k]; cd = 2; }
+    out[k] = m;
+    code[k] = cd;
+  }
+}
+
+__global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, int nchunk, const bf16_t* __restrict__ x,
+                                                          bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
+  extern __shared__ uint4 s1_lds[];  // m1 [rows+1][G], m2 [rows+1][G] (bf16 x 8); row `rows`: idle lanes
+  const S1Geo s = s1_geo(p, G, nchunk);
+  uint4* m1s = s1_lds;
+  uint4* m2s = s1_lds + (s.rows + 1) * G;
+  const size_t clip = (size_t)s.b * s.rows * p.W * p.C;
+  const int nbytes = s.rows * p.W * p.C * 2;
+  const auto xr = clip_rsrc(x + clip, nbytes);
+  const auto yr = clip_rsrc(y + clip, nbytes);
+  const auto ar = clip_rsrc(arg + clip, nbytes / 2);
+  const uint32_t oob = 0x40000000u, ecol = (uint32_t)p.C;
+  const int me = (s.active ? s.r : s.rows) * G + s.g;  // idle lanes own a dummy row
+  // neighbour slots (clamped for idle lanes / edges; validity flags decide)
+  const bool vhm = s.active && s.h > 0, vhp = s.active && s.h + 1 < p.H;
+  const bool vtm = s.active && s.t > 0, vtp = s.active && s.t + 1 < p.T;
+  const int ihm = vhm ? me - G : me, ihp = vhp ? me + G : me;
+  const int itm = vtm ? me - p.H * G : me, itp = vtp ? me + p.H * G : me;
+  auto col = [&](int w) { return (w >= 0 && w < p.W) ? (s.e0 + (uint32_t)w * ecol) : oob; };
+  uint4 xp = make_uint4(0, 0, 0, 0), xc = bld16(xr, col(0) * 2), xn = bld16(xr, col(1) * 2);
+  for (int w = 0; w < p.W; ++w) {
+    const uint4 xnn = bld16(xr, col(w + 2) * 2);  // prefetch
+    float fa[8], fb[8], fc[8], m1[8], m2[8], o[8];
+    uint32_t cw[8], ch[8], ct[8];
+    unpack8(xp, fa);
+    unpack8(xc, fb);
+    unpack8(xn, fc);
+    max3(fa, w > 0, fb, true, fc, w + 1 < p.W, m1, cw);
+    m1s[me] = pack8(m1);  // exact: maxima of bf16 values
+    lds_barrier();
+    unpack8(m1s[ihm], fa);
+    unpack8(m1s[ihp], fc);
+    max3(fa, vhm, m1, true, fc, vhp, m2, ch);
+    m2s[me] = pack8(m2);
+    lds_barrier();
+    unpack8(m2s[itm], fa);
+    unpack8(m2s[itp], fc);
+    max3(fa, vtm, m2, true, fc, vtp, o, ct);
+    const uint32_t off = col(s.active ? w : -1);
+    bst16(yr, off * 2, pack8(o));
+    uint32_t cb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cb[k] = cw[k] | (ch[k] << 2) | (ct[k] << 4);
+    uint2 a;
+    a.x = cb[0] | (cb[1] << 8) | (cb[2] << 16) | (cb[3] << 24);
+    a.y = cb[4] | (cb[5] << 8) | (cb[6] << 16) | (cb[7] << 24);
+    bst8(ar, off, a);
+    xp = xc;
+    xc = xn;
+    xn = xnn;
+  }
+}
+
+// Backward of the separable sweep, output column wo per step:
+//   t stage  dm2(r) = sum_dt [ct(r_o) == dt] dy(r_o),  r_o = r - (dt-1)*H   (LDS exchange of dy, codes)
+//   h stage  dm1(r) = sum_dh [ch(r_o) == dh] dm2(r_o), r_o = r - (dh-1)     (LDS exchange of dm2, fp32)
+//   w stage  dx(w)  = sum_dw [cw(w_o) == dw] dm1(w_o), w_o = w - dw + 1     (registers, 3 columns)
+// dx column wo-1 is final at step wo. Fused epilogue (both optional, 0-record descriptors
+// otherwise): acc_in  dx += acc_in (the other gradient of the pool input: the Inception 1x1
+// GEMM's dX); x, gs  gs[b, c] = sum_thw dx * x (the SelfGating reduction of the block that
+// produced x, from the final bf16 dx), written directly (the workgroup owns the plane).
+__global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, int nchunk,
+                                                          const bf16_t* __restrict__ dy,
+                                                          const uint8_t* __restrict__ arg,
+                                                          const bf16_t* __restrict__ acc_in,
+                                                          const bf16_t* __restrict__ x, float* __restrict__ gs,
+                                                          bf16_t* __restrict__ dx) {
+  extern __shared__ uint4 s1_lds[];  // dy [2][rows+1][G] bf16x8 | dm2 [rows+1][G] f32x8 | codes [2][rows+1][G]
+  const S1Geo s = s1_geo(p, G, nchunk);
+  const int n = (s.rows + 1) * G;
+  uint4* dys = s1_lds;                   // 2 * n
+  float4* m2s = (float4*)(s1_lds + 2 * n);  // 2 * n float4 (8 floats per slot)
+  uint2* cds = (uint2*)(s1_lds + 4 * n);    // 2 * n
+  const size_t clip = (size_t)s.b * s.rows * p.W * p.C;
+  const int nbytes = s.rows * p.W * p.C * 2;
+  const auto dyr = clip_rsrc(dy + clip, nbytes);
+  const auto agr = clip_rsrc(arg + clip, nbytes / 2);
+  const auto inr = clip_rsrc(acc_in != nullptr ? acc_in + clip : dy + clip, acc_in != nullptr ? nbytes : 0);
+  const auto xr = clip_rsrc(x != nullptr ? x + clip : dy + clip, gs != nullptr ? nbytes : 0);
+  const auto dxr = clip_rsrc(dx + clip, nbytes);
+  const uint32_t oob = 0x40000000u, ecol = (uint32_t)p.C;
+  const int me = (s.active ? s.r : s.rows) * G + s.g;  // idle lanes own a dummy row
+  const bool vhm = s.active && s.h > 0, vhp = s.active && s.h + 1 < p.H;
+  const bool vtm = s.active && s.t > 0, vtp = s.active && s.t + 1 < p.T;
+  const int ihm = vhm ? me - G : me, ihp = vhp ? me + G : me;
+  const int itm = vtm ? me - p.H * G : me, itp = vtp ? me + p.H * G : me;
+  auto col = [&](int w) { return (w >= 0 && w < p.W) ? (s.e0 + (uint32_t)w * ecol) : oob; };
+  auto code = [](const uint2& a, int k, int sh) {
+    return ((((k < 4 ? a.x : a.y) >> (8 * (k & 3))) >> sh) & 3u);
+  };
+  float sacc[8], dA[8], dB[8];  // dm1 of columns wo-2 (A), wo-1 (B)
+  uint2 cA = make_uint2(0, 0), cB = make_uint2(0, 0);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { sacc[k] = 0.f; dA[k] = 0.f; dB[k] = 0.f; }
+  uint4 gcur = bld16(dyr, col(0) * 2);
+  uint2 acur = bld8(agr, col(0));
+  for (int wo = 0; wo <= p.W; ++wo) {
+    // emit operands of column wo-1 first, then the next column's gradient and codes
+    const uint32_t ep = col(wo - 1);
+    const uint4 ein = bld16(inr, ep * 2), xin = bld16(xr, ep * 2);
+    const uint4 gnext = bld16(dyr, col(wo + 1) * 2);
+    const uint2 anext = bld8(agr, col(wo + 1));
+    float dC[8];  // dm1 of column wo
+    uint2 cC = acur;
+    if (wo < p.W) {
+      const int buf = (wo & 1) * n;
+      dys[buf + me] = gcur;
+      cds[buf + me] = acur;
+      lds_barrier();
+      // t stage: candidates are the outputs at t+1 (dt=0), t (dt=1), t-1 (dt=2)
+      float g0[8], g1[8], g2[8], m2[8];
+      const uint2 c0 = cds[buf + itp], c2 = cds[buf + itm];
+      unpack8(dys[buf + itp], g0);
+      unpack8(gcur, g1);
+      unpack8(dys[buf + itm], g2);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = code(acur, k, 4) == 1u ? g1[k] : 0.f;
+        v += (vtp && code(c0, k, 4) == 0u) ? g0[k] : 0.f;
+        v += (vtm && code(c2, k, 4) == 2u) ? g2[k] : 0.f;
+        m2[k] = v;
+      }
+      m2s[2 * me] = make_float4(m2[0], m2[1], m2[2], m2[3]);
+      m2s[2 * me + 1] = make_float4(m2[4], m2[5], m2[6], m2[7]);
+      lds_barrier();
+      // h stage: candidates are the m2 cells at h+1 (dh=0), h (dh=1), h-1 (dh=2)
+      const uint2 h0 = cds[buf + ihp], h2 = cds[buf + ihm];
+      const float4 p0a = m2s[2 * ihp], p0b = m2s[2 * ihp + 1], p2a = m2s[2 * ihm], p2b = m2s[2 * ihm + 1];
+      const float q0[8] = {p0a.x, p0a.y, p0a.z, p0a.w, p0b.x, p0b.y, p0b.z, p0b.w};
+      const float q2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = code(acur, k, 2) == 1u ? m2[k] : 0.f;
+        v += (vhp && code(h0, k, 2) == 0u) ? q0[k] : 0.f;
+        v += (vhm && code(h2, k, 2) == 2u) ? q2[k] : 0.f;
+        dC[k] = v;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dC[k] = 0.f;
+      cC = make_uint2(0, 0);
+    }
+    if (wo >= 1) {
+      // w stage for input column wo-1: dm1 cells at wo (dw=0), wo-1 (dw=1), wo-2 (dw=2)
+      float d[8], e[8], q[8], xv[8];
+      unpack8(ein, e);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = e[k];
+        v += code(cC, k, 0) == 0u ? dC[k] : 0.f;
+        v += code(cB, k, 0) == 1u ? dB[k] : 0.f;
+        v += code(cA, k, 0) == 2u ? dA[k] : 0.f;
+        d[k] = v;
+      }
+      const uint4 vout = pack8(d);
+      bst16(dxr, ep * 2, vout);
+      unpack8(vout, q);
+      unpack8(xin, xv);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sacc[k] += q[k] * xv[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { dA[k] = dB[k]; dB[k] = dC[k]; }
+    cA = cB;
+    cB = cC;
+    gcur = gnext;
+    acur = anext;
+  }
+  if (gs == nullptr) return;
+  __syncthreads();
+  float* red = (float*)s1_lds;  // G*8 floats
+  for (int i = threadIdx.x; i < G * 8; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  if (s.active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) atomicAdd(&red[s.g * 8 + k], sacc[k]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < G * 8; i += blockDim.x) {
+    const int c = s.chunk * G * 8 + i;
+    if (c < p.C) gs[(size_t)s.b * p.C + c] = red[i];
+  }
+}
+
+// G (8-channel groups per workgroup) for the plane sweeps: as many as fit `maxthr` threads
+// (all rows of the plane are always in one workgroup), at least 1.
+static int s1_groups(int rows, int C, int maxthr = 256, long long B = 0) {
+  const int cpr = C / 8;
+  int G = rows >= maxthr ? 1 : maxthr / rows;
+  if (G > cpr) G = cpr;
+  // keep >= 4 workgroups per CU (1024) when the batch allows: small planes (the 2x7x7 blocks)
+  // otherwise get too few, too long-lived workgroups
+  if (B > 0) {
+    const long long want_chunks = (1024 + B - 1) / B;
+    const int gmax = (int)((cpr + want_chunks - 1) / want_chunks);
+    if (G > gmax) G = gmax < 1 ? 1 : gmax;
+  }
+  // prefer a divisor of cpr (no idle lanes in the last chunk) if it keeps >= 3/4 of G
+  for (int d = G; d >= 1 && 4 * d >= 3 * G; --d)
+    if (cpr % d == 0) return d;
+  return G;
+}
+
+// LDS bytes of the separable sweeps: fwd m1 + m2 columns (16 B per slot each); bwd dy and
+// codes double-buffered plus the fp32 m2 column (2*16 + 2*8 + 32 = 80 B per slot).
+static size_t s1_fwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 32; }
+static size_t s1_bwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 80; }
+
+// Stride-1 pool implementation: 1 = LDS plane sweeps (default), 0 = global-memory sliding
+// kernels (A/B benchmarks only; milnce_set_pool_s1_impl).
+static int g_s1_impl = 1;
+static bool s1_use_lds(const PoolParams& p) { return g_s1_impl == 1 && p.T * p.H <= 512; }
+MILNCE_API int milnce_set_pool_s1_impl(int impl) {
+  const int old = g_s1_impl;
+  g_s1_impl = impl;
+  return old;
+}
+
+static int s1_threads(int rows, int G) {
+  const int n = rows * G;
+  return ((n + 63) / 64) * 64;
+}
+
 static PoolDivs make_divs(const PoolParams& p) {
   PoolDivs d;
   d.fcpr = make_fastdiv(p.C / 8);
@@ -527,6 +826,13 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
 #undef X
     return false;
   }
+  if (is_s1_333(p) && s1_use_lds(p)) {
+    const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
+    const int rows = p.T * p.H, G = s1_groups(rows, p.C, 512, B), nchunk = (p.C / 8 + G - 1) / G;
+    hipLaunchKernelGGL(maxpool_s1_fwd_sep, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)),
+                       s1_fwd_lds(rows, G), s, p, G, nchunk, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg);
+    return true;
+  }
   if (is_s1_333(p)) {
     const long long rows = n / p.W / (p.C / 8);  // n = B*T*H*W*cpr
     const long long thr = rows * (p.C / 8);
@@ -553,6 +859,14 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
                              hipStream_t s) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
+  if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
+    const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
+    const int rows = p.T * p.H, G = s1_groups(rows, p.C, 512, B), nchunk = (p.C / 8 + G - 1) / G;
+    hipLaunchKernelGGL(maxpool_s1_bwd_sep, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)),
+                       s1_bwd_lds(rows, G), s, p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg,
+                       (const bf16_t*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, (bf16_t*)dx);
+    return true;
+  }
   if (is_s1_333(p) && bn_y == nullptr) {
     const long long rows = n / p.W / (p.C / 8);
     const long long thr = rows * (p.C / 8);
@@ -627,5 +941,22 @@ MILNCE_API int milnce_maxpool_bwd(const void* dy, const void* arg, void* dx, int
   if (bn_y != nullptr && (256 % (C / 8) != 0 || bn_ld != C)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(nparts), dim3(256), 0, stream, p, (const bf16_t*)dy,
                      (const uint8_t*)arg, (bf16_t*)dx, n, (const bf16_t*)bn_y, bn_ss, part);
+  return (int)hipGetLastError();
+}
+
+// Inception branch-3 pool backward with the fused epilogue of maxpool_s1_bwd_lds:
+// dx = pool_bwd(dy) (+ acc_in), and (gs != null) gs[b, c] = sum_thw dx * x.
+MILNCE_API int milnce_maxpool_s1_bwd_fused(const void* dy, const void* arg, const void* acc_in, const void* x,
+                                           float* gs, void* dx, int B, int T, int H, int W, int C,
+                                           hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0);
+  const int rows = T * H;
+  // the separable code layout must match the forward that produced arg (milnce_maxpool_fwd)
+  if (!s1_use_lds(p) || (gs != nullptr && x == nullptr)) return (int)hipErrorInvalidValue;
+  const int G = s1_groups(rows, C, 512, B), nchunk = (C / 8 + G - 1) / G;
+  hipLaunchKernelGGL(maxpool_s1_bwd_sep, dim3((unsigned)((long long)B * nchunk)), dim3(s1_threads(rows, G)),
+                     s1_bwd_lds(rows, G), stream, p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg,
+                     (const bf16_t*)acc_in, (const bf16_t*)x, gs, (bf16_t*)dx);
   return (int)hipGetLastError();
 }

@@ -105,13 +105,14 @@ class InceptionBlock(nn.Module):
     def forward(self, x):
         g = self.gating
         # branches 0, 1a, 2a are 1x1x1 units on the same input: one fused GEMM on GPU
+        # (and the branch-3 pool reads it too: one fused op owning every read of x)
         units = (self.conv_b0, self.conv_b1_a, self.conv_b2_a)
-        (z0, z1, z2), s0 = ops.conv1x1_group_bn_relu(x, [u.conv1.weight for u in units], [u.bn1 for u in units],
-                                                     self.training, want_gsum0=g)
+        (z0, z1, z2), s0, pooled = ops.inception_head(x, [u.conv1.weight for u in units],
+                                                      [u.bn1 for u in units], self.training, want_gsum0=g)
         b0 = (z0, s0)
         b1 = self.conv_b1_b(z1, want_gsum=g)
         b2 = self.conv_b2_b(z2, want_gsum=g)
-        b3 = self.conv_b3_b(ops.maxpool_s1(x), want_gsum=g)
+        b3 = self.conv_b3_b(pooled, want_gsum=g)
         if not g:
             return torch.cat((z0, b1, b2, b3), dim=-1)
         gates = (self.gating_b0, self.gating_b1, self.gating_b2, self.gating_b3)

@@ -515,99 +515,110 @@ class _Conv1x1GroupBNReLU(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, n, training, want_gsum0, hyper, *args):
-        ws = args[:n]
-        bns = [args[n + 5 * i: n + 5 * i + 5] for i in range(n)]  # gamma, beta, rmean, rvar, nbt
-        widths = [int(w.shape[0]) for w in ws]
-        ctot = sum(widths)
-        wcat = torch.cat([w.detach() for w in ws], 0)
-        plan = conv_plan(x.shape, wcat.shape, (1, 1, 1), (0, 0, 0))
-        dev = x.device
-        wp = _pack(wcat, plan, 0)
-        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
-        y = conv_forward_raw(x, wp, plan, stats)
-        thw = plan.To * plan.Ho * plan.Wo
-        zs, sss, gsum = [], [], None
-        off = 0
-        y2 = y.view(-1, ctot)
-        for i, (c, (gamma, beta, rmean, rvar, nbt)) in enumerate(zip(widths, bns)):
-            ss = torch.empty((4 * c,), dtype=F32, device=dev)
-            st = stats[off:] if training else None
-            call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
-                 ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
-                 float(hyper[i][1]), int(training), ptr(ss), stream())
-            z = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev)
-            g = torch.zeros((plan.B, c), dtype=F32, device=dev) if (i == 0 and want_gsum0) else None
-            ysl = y2[:, off:off + c]
-            call("milnce_bn_relu_apply", ptr(ysl), ctot, ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g), stream())
-            z._milnce_bn = (ysl, ss, ctot)
-            zs.append(z)
-            sss.append(ss)
-            if g is not None:
-                gsum = g
-            off += c
-        ctx.save_for_backward(x, wcat, y, *sss, *[b[0] for b in bns])
-        ctx.betas = [b[1] for b in bns]
-        ctx.training = bool(training)
-        ctx.plan, ctx.widths, ctx.n = plan, widths, n
-        ctx.x_bn = getattr(x, "_milnce_bn", None)
-        if gsum is not None:
-            ctx.mark_non_differentiable(gsum)
-            return (*zs, gsum)
-        return tuple(zs)
+        return _group_forward(ctx, x, n, training, want_gsum0, hyper, args, ())
 
     @staticmethod
     def backward(ctx, *grads):
-        n, widths, plan = ctx.n, ctx.widths, ctx.plan
-        saved = ctx.saved_tensors
-        x, wcat, y = saved[:3]
-        sss = saved[3:3 + n]
-        gammas = saved[3 + n:3 + 2 * n]
-        ctot = sum(widths)
-        dev = y.device
-        dY = torch.empty((plan.M, ctot), dtype=BF16, device=dev)
-        y2 = y.view(-1, ctot)
-        dgs, dbs = [], []
-        off = 0
-        for i, c in enumerate(widths):
-            dz = grads[i]
-            if dz is None:
-                dz = torch.zeros((plan.M, c), dtype=BF16, device=dev)
-            dz = dz.contiguous()
-            fused = take_bn_partials(dz)
-            if fused is not None:
-                part, nparts, ps = fused
-            else:
-                nparts = _bn_nparts(plan.M)
-                part = torch.empty((nparts * 2 * c,), dtype=F32, device=dev)
-                ps = c
-            coef = torch.empty((3 * c,), dtype=F32, device=dev)
-            g_direct, b_direct = _direct_grad(gammas[i]), _direct_grad(ctx.betas[i])
-            direct_bn = g_direct is not None and b_direct is not None
-            dgamma = g_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
-            dbeta = b_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
-            call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
-                 ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
-                 ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
-            if direct_bn:
-                _grad_done(gammas[i])
-                _grad_done(ctx.betas[i])
-                dgamma = dbeta = None
-            dgs.append(dgamma)
-            dbs.append(dbeta)
-            off += c
-        dYv = dY.view(plan.B, plan.To, plan.Ho, plan.Wo, ctot)
-        dx = None
-        if ctx.needs_input_grad[0]:
-            dx = conv_dgrad(dYv, _pack(wcat, plan, 1), plan, ctx.x_bn)
-        dwcat = conv_wgrad(dYv, x, plan)
-        dws, off = [], 0
-        for c in widths:
-            dws.append(dwcat[off:off + c])
-            off += c
-        bn_grads = []
-        for dg, db in zip(dgs, dbs):
-            bn_grads += [dg, db, None, None, None]
-        return (dx, None, None, None, None, *dws, *bn_grads)
+        dx, rest = _group_backward(ctx, grads)
+        return (dx, *rest)
+
+
+def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
+    """Forward of the fused 1x1 group (see ``_Conv1x1GroupBNReLU``); ``extra_saved`` tensors are
+    appended to the saved tensors (read back by ``_group_backward`` callers)."""
+    ws = args[:n]
+    bns = [args[n + 5 * i: n + 5 * i + 5] for i in range(n)]  # gamma, beta, rmean, rvar, nbt
+    widths = [int(w.shape[0]) for w in ws]
+    ctot = sum(widths)
+    wcat = torch.cat([w.detach() for w in ws], 0)
+    plan = conv_plan(x.shape, wcat.shape, (1, 1, 1), (0, 0, 0))
+    dev = x.device
+    wp = _pack(wcat, plan, 0)
+    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+    y = conv_forward_raw(x, wp, plan, stats)
+    thw = plan.To * plan.Ho * plan.Wo
+    zs, sss, gsum = [], [], None
+    off = 0
+    y2 = y.view(-1, ctot)
+    for i, (c, (gamma, beta, rmean, rvar, nbt)) in enumerate(zip(widths, bns)):
+        ss = torch.empty((4 * c,), dtype=F32, device=dev)
+        st = stats[off:] if training else None
+        call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
+             ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
+             float(hyper[i][1]), int(training), ptr(ss), stream())
+        z = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev)
+        g = torch.zeros((plan.B, c), dtype=F32, device=dev) if (i == 0 and want_gsum0) else None
+        ysl = y2[:, off:off + c]
+        call("milnce_bn_relu_apply", ptr(ysl), ctot, ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g), stream())
+        z._milnce_bn = (ysl, ss, ctot)
+        zs.append(z)
+        sss.append(ss)
+        if g is not None:
+            gsum = g
+        off += c
+    ctx.save_for_backward(x, wcat, y, *sss, *[b[0] for b in bns], *extra_saved)
+    ctx.betas = [b[1] for b in bns]
+    ctx.training = bool(training)
+    ctx.plan, ctx.widths, ctx.n = plan, widths, n
+    ctx.x_bn = getattr(x, "_milnce_bn", None)
+    if gsum is not None:
+        ctx.mark_non_differentiable(gsum)
+        return (*zs, gsum)
+    return tuple(zs)
+
+def _group_backward(ctx, grads, saved=None):
+    """Backward of the fused 1x1 group: returns (dX of the GEMM, the remaining grads tuple)."""
+    n, widths, plan = ctx.n, ctx.widths, ctx.plan
+    saved = ctx.saved_tensors if saved is None else saved
+    x, wcat, y = saved[:3]
+    sss = saved[3:3 + n]
+    gammas = saved[3 + n:3 + 2 * n]
+    ctot = sum(widths)
+    dev = y.device
+    dY = torch.empty((plan.M, ctot), dtype=BF16, device=dev)
+    y2 = y.view(-1, ctot)
+    dgs, dbs = [], []
+    off = 0
+    for i, c in enumerate(widths):
+        dz = grads[i]
+        if dz is None:
+            dz = torch.zeros((plan.M, c), dtype=BF16, device=dev)
+        dz = dz.contiguous()
+        fused = take_bn_partials(dz)
+        if fused is not None:
+            part, nparts, ps = fused
+        else:
+            nparts = _bn_nparts(plan.M)
+            part = torch.empty((nparts * 2 * c,), dtype=F32, device=dev)
+            ps = c
+        coef = torch.empty((3 * c,), dtype=F32, device=dev)
+        g_direct, b_direct = _direct_grad(gammas[i]), _direct_grad(ctx.betas[i])
+        direct_bn = g_direct is not None and b_direct is not None
+        dgamma = g_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
+        dbeta = b_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
+        call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
+             ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
+             ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
+        if direct_bn:
+            _grad_done(gammas[i])
+            _grad_done(ctx.betas[i])
+            dgamma = dbeta = None
+        dgs.append(dgamma)
+        dbs.append(dbeta)
+        off += c
+    dYv = dY.view(plan.B, plan.To, plan.Ho, plan.Wo, ctot)
+    dx = None
+    if ctx.needs_input_grad[0]:
+        dx = conv_dgrad(dYv, _pack(wcat, plan, 1), plan, ctx.x_bn)
+    dwcat = conv_wgrad(dYv, x, plan)
+    dws, off = [], 0
+    for c in widths:
+        dws.append(dwcat[off:off + c])
+        off += c
+    bn_grads = []
+    for dg, db in zip(dgs, dbs):
+        bn_grads += [dg, db, None, None, None]
+    return dx, (None, None, None, None, *dws, *bn_grads)
 
 
 def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = False):
@@ -620,6 +631,73 @@ def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = Fa
         args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
     hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
     return _Conv1x1GroupBNReLU.apply(x, len(weights), bool(training), bool(want_gsum0), hyper, *args)
+
+
+class _InceptionHead(torch.autograd.Function):
+    """Everything an Inception block reads its input x with (``s3dg.py:13-21``): the fused 1x1
+    group GEMM of branches 0/1a/2a and the branch-3 max pool (3x3x3, stride 1, -inf padding).
+    Owning both consumers of x lets the backward produce dX in ONE pass: the pool backward
+    kernel gathers the pooled gradient, adds the GEMM's dX (no separate autograd add) and,
+    when x is a SelfGating output, also emits the previous gate's reduction
+    sum_thw dX * x (attached to dX; ``_GateConcat.backward`` then skips its reduce pass).
+    Returns (*branch outputs, [gating sum of branch 0], pooled x)."""
+
+    @staticmethod
+    def forward(ctx, x, n, training, want_gsum0, hyper, *args):
+        B, T, H, W, C = x.shape
+        pooled = torch.empty_like(x)
+        arg = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+        geo = [B, T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0]
+        call("milnce_maxpool_fwd", ptr(x), ptr(pooled), ptr(arg), *geo, stream())
+        outs = _group_forward(ctx, x, n, training, want_gsum0, hyper, args, (arg,))
+        ctx.x_gate = bool(getattr(x, "_milnce_gate", False))
+        return (*outs, pooled)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        saved = ctx.saved_tensors
+        arg = saved[-1]
+        x = saved[0]
+        dpooled = grads[-1]
+        dx1, rest = _group_backward(ctx, grads[:-1], saved[:-1])
+        B, T, H, W, C = x.shape
+        if dpooled is None or not ctx.needs_input_grad[0]:
+            return (dx1, *rest)
+        dx = torch.empty_like(x)
+        gs = torch.empty((B, C), dtype=F32, device=x.device) if ctx.x_gate else None
+        call("milnce_maxpool_s1_bwd_fused", ptr(dpooled.contiguous()), ptr(arg), ptr(dx1), ptr(x), ptr(gs),
+             ptr(dx), B, T, H, W, C, stream())
+        if gs is not None:
+            dx._milnce_gs = gs
+            dx._milnce_gsver = dx._version
+        return (dx, *rest)
+
+
+_FUSE_HEAD = os.environ.get("MILNCE_FUSE_INCEPTION_HEAD", "1") != "0"
+
+
+def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False):
+    """Fused 1x1 group + branch-3 pool on the Inception input; see ``_InceptionHead``."""
+    if x.dtype != BF16:
+        x = x.to(BF16)
+    x = x.contiguous()
+    B, T, H, W, C = x.shape
+    if not _FUSE_HEAD or T * H > 512 or C % 8:  # csrc/pool.hip milnce_maxpool_s1_bwd_fused limits
+        outs = conv1x1_group_bn_relu(x, weights, bns, training, want_gsum0)
+        return (*outs, maxpool3d(x, (3, 3, 3), (1, 1, 1), False))
+    args = list(weights)
+    for bn in bns:
+        args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
+    hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
+    return _InceptionHead.apply(x, len(weights), bool(training), bool(want_gsum0), hyper, *args)
+
+
+def take_gate_sums(dout: torch.Tensor):
+    """sum_thw dout * out per (clip, channel) if the producer of dout attached it."""
+    gs = getattr(dout, "_milnce_gs", None)
+    if gs is None or getattr(dout, "_milnce_gsver", -1) != dout._version:
+        return None
+    return gs
 
 
 # =========================================================================================
@@ -649,6 +727,7 @@ class _GateConcat(torch.autograd.Function):
         ctx.save_for_backward(*zs, *ws, g, mean)
         ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
         ctx.z_bn = [getattr(z, "_milnce_bn", None) for z in zs]
+        out._milnce_gate = True  # consumers may return sum_thw dout * out with the gradient
         return out
 
     @staticmethod
@@ -664,9 +743,14 @@ class _GateConcat(torch.autograd.Function):
         dev = dout.device
         dzs = [torch.empty_like(z) for z in zs]
         widths = _arr(ctypes.c_int, ctx.widths)
-        dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
-        call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zs]), ptr(dout),
-             ptr(g), B, ctx.thw, ptr(dpre), stream())
+        gs = take_gate_sums(dout)
+        if gs is not None:
+            # gs = sum dout * bf16(z * g) = g * sum dout * z  ->  dpre = gs * (1 - g)
+            dpre = gs * (1.0 - g)
+        else:
+            dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
+            call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zs]), ptr(dout),
+                 ptr(g), B, ctx.thw, ptr(dpre), stream())
         # per-branch fc backward: plain GEMMs on hipBLASLt
         dmean = torch.empty((B, ctot), dtype=F32, device=dev)
         dws, dbs = [], []

@@ -261,6 +261,63 @@ def test_maxpool(kernel, stride, tf):
     assert rel_err(xh.grad, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 16, 25, 9, 16), (3, 4, 13, 13, 56), (2, 2, 7, 7, 832), (1, 3, 1, 5, 8)])
+def test_maxpool_s1_lds_shapes(shape):
+    """LDS plane-sweep stride-1 pool: > 256 plane rows (1 group), partial channel chunks, W=5/H=1."""
+    torch.manual_seed(12)
+    h = hip()
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    x[0, 0, 0, :2, :8] = 1.0  # ties: first tap in (t, h, w) order wins
+    xh = x.clone().requires_grad_(True)
+    y = h.maxpool3d(xh, (3, 3, 3), (1, 1, 1), False)
+    xr = x.float().requires_grad_(True)
+    yr = aten.maxpool_s1(xr)
+    assert torch.equal(y.float(), yr)
+    dy = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    assert rel_err(xh.grad, xr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("T,HW,cin", [(4, 13, 192), (8, 25, 64)])
+def test_inception_head_fused_backward(T, HW, cin):
+    """gate -> fused Inception head (1x1 group GEMM + branch-3 pool; one-pass dX that adds the
+    GEMM's dX and attaches the gate reduction) vs the same graph through the unfused HIP ops
+    (separate pool / autograd add / gate reduce pass): same bf16 block output, so the same
+    pool arg-max; differences are rounding only."""
+    from mil_nce_howto100m_amd import ops
+    torch.manual_seed(13)
+    h = hip()
+    widths = (32, 48, 16)
+    B = 2
+    z = torch.rand(B, T, HW, HW, cin, device=DEV).to(torch.bfloat16)
+    fc = nn.Linear(cin, cin).to(DEV)
+    convs = [nn.Conv3d(cin, c, 1, bias=False).to(DEV) for c in widths]
+    ds = None
+    res = []
+    for fused in (True, False):
+        bns = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+        for m in [fc] + convs:
+            for p_ in m.parameters():
+                p_.grad = None
+        old = h._FUSE_HEAD
+        h._FUSE_HEAD = fused
+        try:
+            zh = z.clone().requires_grad_(True)
+            x = h.gate_concat([zh], [fc.weight], [fc.bias], [z.float().sum(dim=(1, 2, 3))])
+            zs0, s0, pooled = ops.inception_head(x, [c.weight for c in convs], bns, True, True)
+            outs = list(zs0) + [pooled]
+            if ds is None:
+                ds = [torch.randn_like(o.float()).to(torch.bfloat16) for o in outs]
+            torch.autograd.backward(outs, ds)
+        finally:
+            h._FUSE_HEAD = old
+        res.append([zh.grad.float(), fc.weight.grad.clone(), fc.bias.grad.clone()] +
+                   [c.weight.grad.clone() for c in convs] + [o.float() for o in outs])
+    for a, b in zip(*res):
+        assert rel_err(a, b) < 1e-2
+
+
 def test_gate_concat():
     torch.manual_seed(3)
     h = hip()
