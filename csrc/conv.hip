@@ -730,7 +730,7 @@ __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH]
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
     const int m = mb + row;
-    const int n = n0 + d_ccol * 8;
+    const int n = n0 + ((tid + i * 256) % DCPR) * 8;  // == d_ccol when DCPR divides 256
     const bool v = (m < m_end) & (n < p.Cout);
     const uint32_t off = v ? (uint32_t)(((long long)(m - m_base) * p.ldd + n) * 2) : 0x80000000u;
     dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
@@ -757,7 +757,7 @@ __device__ __forceinline__ void wgrad_store(const uint4 (&dreg)[DCH], const XReg
 #pragma unroll
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
-    *(uint4*)(d + row * LDN + d_ccol * 8) = dreg[i];
+    *(uint4*)(d + row * LDN + ((tid + i * 256) % DCPR) * 8) = dreg[i];
   }
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
@@ -1324,10 +1324,21 @@ static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
 
 template <int TN_, int TK_>
 static int launch_wgrad_impl(WgradParams& p, int impl, hipStream_t stream) {
-  if (impl == 5) return launch_wgrad<TN_, TK_, false, true>(p, stream);
-  if (impl == 4) return launch_wgrad_v3<TN_, TK_, 2>(p, stream);
-  if (impl == 3) return launch_wgrad_v3<TN_, TK_, 3>(p, stream);
-  return launch_wgrad<TN_, TK_, false>(p, stream);
+  if constexpr (TN_ % 64 != 0) {
+    // wide N tiles (96 / 192: Cout = 96, 192, 288, 384, ... without padding) exist only as the
+    // register-staged kernels (the LDS-DMA mapping needs TN / 8 to divide 64); the 2-deep
+    // variant of 192 x 128 would spill
+    if constexpr (!(TN_ == 192 && TK_ == 128)) {
+      if (impl == 5) return launch_wgrad<TN_, TK_, false, true>(p, stream);
+    }
+    if (impl == 2) return launch_wgrad<TN_, TK_, false>(p, stream);
+    return (int)hipErrorInvalidValue;
+  } else {
+    if (impl == 5) return launch_wgrad<TN_, TK_, false, true>(p, stream);
+    if (impl == 4) return launch_wgrad_v3<TN_, TK_, 2>(p, stream);
+    if (impl == 3) return launch_wgrad_v3<TN_, TK_, 3>(p, stream);
+    return launch_wgrad<TN_, TK_, false>(p, stream);
+  }
 }
 
 MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u8, float* slab, float* dw,
@@ -1367,6 +1378,10 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
     else if (tn == 64 && tk == 128) rc = launch_wgrad_impl<64, 128>(p, impl, stream);
     else if (tn == 128 && tk == 64) rc = launch_wgrad_impl<128, 64>(p, impl, stream);
     else if (tn == 128 && tk == 128) rc = launch_wgrad_impl<128, 128>(p, impl, stream);
+    else if (tn == 96 && tk == 64) rc = launch_wgrad_impl<96, 64>(p, impl, stream);
+    else if (tn == 96 && tk == 128) rc = launch_wgrad_impl<96, 128>(p, impl, stream);
+    else if (tn == 192 && tk == 64) rc = launch_wgrad_impl<192, 64>(p, impl, stream);
+    else if (tn == 192 && tk == 128) rc = launch_wgrad_impl<192, 128>(p, impl, stream);
     else rc = (int)hipErrorInvalidValue;
   }
   if (rc) return rc;

@@ -56,40 +56,62 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return ((x >> 16) ^ x) & 0x7fffffffu;
 }
 
+// One wave per (b, t, y) image row, 4 pixels (16 B) per lane: the label-dependent
+// constants are per row, index math is 32-bit, and the three channel waves use the hardware
+// sine (the torch reference in data/synthetic.py agrees to +-1 grey level).
 __global__ __launch_bounds__(256) void synth_video_kernel(const int* __restrict__ labels, const int* __restrict__ ids,
-                                                          int T, int S, uint32_t* __restrict__ out, long long npix) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < npix;
-       i += (long long)gridDim.x * blockDim.x) {
-    long long r = i;
-    const int x = r % S; r /= S;
-    const int y = r % S; r /= S;
-    const int t = r % T;
-    const int b = (int)(r / T);
+                                                          int T, int S, uint32_t* __restrict__ out, long long nrows) {
+  const int q = S >> 2;  // 4-pixel quads per row (S % 4 == 0)
+  for (long long row = blockIdx.x; row < nrows; row += gridDim.x) {
+    const int y = (int)(row % S);
+    const int bt = (int)(row / S);
+    const int t = bt % T, b = bt / T;
     const float lab = (float)labels[b];
     const float freq = 0.05f + 0.01f * fmodf(lab, 7.f);
     const float drift = 0.5f + 0.25f * fmodf(lab, 5.f);
-    const uint32_t h = mix32((uint32_t)ids[b] * 65537u + ((uint32_t)t * S + y) * S + x);
-    const float noise = (float)(h % 64u) - 32.f;
-    uint32_t px = 0;
+    const uint32_t id = (uint32_t)ids[b] * 65537u;
+    float color[3], ph[3];
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
-      const float color = 64.f + 48.f * fmodf(lab * 3.f + ch * 5.f, 4.f);
-      const float wave = sinf(freq * ((float)x + (float)y * (1.f + 0.1f * ch)) + drift * (float)t);
-      float v = color + 60.f * wave + noise;
-      v = fminf(fmaxf(v, 0.f), 255.f);
-      px |= ((uint32_t)v & 0xffu) << (8 * ch);
+      color[ch] = 64.f + 48.f * fmodf(lab * 3.f + ch * 5.f, 4.f);
+      ph[ch] = (float)y * (1.f + 0.1f * ch);
     }
-    out[i] = px;
+    uint32_t* orow = out + row * S;
+    for (int x0 = threadIdx.x * 4; x0 < S; x0 += blockDim.x * 4) {
+      uint32_t px[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int x = x0 + j;
+        const uint32_t h = mix32(id + ((uint32_t)t * S + y) * S + x);
+        const float noise = (float)(h % 64u) - 32.f;
+        uint32_t v4 = 0;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+          const float wave = __sinf(freq * ((float)x + ph[ch]) + drift * (float)t);
+          float v = color[ch] + 60.f * wave + noise;
+          v = fminf(fmaxf(v, 0.f), 255.f);
+          v4 |= ((uint32_t)v & 0xffu) << (8 * ch);
+        }
+        px[j] = v4;
+      }
+      if ((S & 3) == 0) {
+        *(uint4*)(orow + x0) = make_uint4(px[0], px[1], px[2], px[3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (x0 + j < S) orow[x0 + j] = px[j];
+      }
+    }
   }
 }
 
 MILNCE_API int milnce_synth_video(const int* labels, const int* ids, int B, int T, int S, void* out,
                                   hipStream_t stream) {
-  const long long npix = (long long)B * T * S * S;
-  long long grid = (npix + 255) / 256;
-  if (grid > 16384) grid = 16384;
-  hipLaunchKernelGGL(synth_video_kernel, dim3((int)grid), dim3(256), 0, stream, labels, ids, T, S,
-                     (uint32_t*)out, npix);
+  const long long nrows = (long long)B * T * S;
+  const long long grid = nrows < 65536 ? nrows : 65536;
+  // one wave per image row: a 200-pixel row is 50 quads
+  hipLaunchKernelGGL(synth_video_kernel, dim3((int)grid), dim3(64), 0, stream, labels, ids, T, S,
+                     (uint32_t*)out, nrows);
   return (int)hipGetLastError();
 }
 

@@ -149,7 +149,7 @@ _AUTOTUNE = os.environ.get("MILNCE_CONV_AUTOTUNE", "1") != "0"
 _DEFAULT_IMPL = int(os.environ.get("MILNCE_CONV_IMPL", "2"))
 
 
-def _tune(launch, impls=_IMPLS) -> int:
+def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
     """Time each kernel variant on the real operands (outputs are simply overwritten) and keep
     the fastest; run once per conv shape and direction, then cached in the plan. Each variant
     is timed over >= ~0.5 ms of repetitions, and the default wins unless another is >= 3 %
@@ -173,8 +173,9 @@ def _tune(launch, impls=_IMPLS) -> int:
         t0 = timed(impl, 1)
         times[impl] = timed(impl, max(2, min(50, int(0.5 / max(t0, 1e-3)))))
     best = min(times, key=times.get)
-    if _DEFAULT_IMPL in times and times[best] > 0.97 * times[_DEFAULT_IMPL]:
-        best = _DEFAULT_IMPL
+    default = _DEFAULT_IMPL if default is None else default
+    if default in times and times[best] > 0.97 * times[default]:
+        best = default
     return best
 
 
@@ -267,30 +268,62 @@ def _grad_done(param: torch.Tensor) -> None:
     grad_sink.notify(param)
 
 
+def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int) -> Tuple[int, int, int]:
+    """(Npad, Kpad, splits) of a wgrad tiling: split-K over m until >= 4 blocks per CU."""
+    npad = _ceil(Cout, tn) * tn
+    kpad = _ceil(Ktot, tk) * tk
+    tiles = (npad // tn) * (kpad // tk)
+    splits = max(1, min(_ceil(4 * _NUM_CU, tiles), _ceil(M, 32 * 8)))
+    return npad, kpad, splits
+
+
+def _wgrad_tiles(Cout: int) -> List[int]:
+    """N-tile candidates: 128 (64 for narrow layers) plus the wide register-staged tiles 96 / 192
+    where they pad Cout less (192 -> one 192 or two 96 tiles instead of two 128s)."""
+    if Cout <= 64:
+        return [64]
+    base = _ceil(Cout, 128) * 128
+    return [128] + [t for t in (96, 192) if _ceil(Cout, t) * t < base]
+
+
+_WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
+
+
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """dW of the conv; with ``out`` the result is accumulated into it (a parameter's grad)."""
+    """dW of the conv; with ``out`` the result is accumulated into it (a parameter's grad).
+    The first call of a plan tunes over (N tile, kernel variant) pairs on the real operands."""
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
-    slab = torch.empty((plan.w_splits, plan.w_Npad, plan.w_Kpad), dtype=F32, device=dy.device)
     acc = int(out is not None)
     dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
 
-    def launch(impl):
-        call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(dw),
+    def launch_with(tn, impl, target, accumulate):
+        npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk)
+        slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
+        call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
              plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-             plan.w_Kpad, plan.w_Npad, plan.w_tn, plan.w_tk, plan.w_splits, acc, plan.wo_override, impl, stream())
+             kpad, npad, tn, plan.w_tk, splits, accumulate, plan.wo_override, impl, stream())
 
     if plan.w_impl == 0:
-        if acc:  # tune on a scratch output: the real one accumulates
-            real, acc_real = dw, acc
-            dw, acc = torch.empty_like(real), 0
-            plan.w_impl = _tune(launch, _W_IMPLS) if x.dtype != torch.uint8 else 2
-            dw, acc = real, acc_real
+        if x.dtype == torch.uint8 or not _AUTOTUNE:
+            plan.w_impl = 2 if x.dtype == torch.uint8 else _DEFAULT_IMPL
         else:
-            plan.w_impl = _tune(launch, _W_IMPLS) if x.dtype != torch.uint8 else 2
-    launch(plan.w_impl)
+            scratch = torch.empty_like(dw)  # tune on a scratch output: the real one may accumulate
+            cands = []
+            for tn in _wgrad_tiles(plan.Cout):
+                for impl in _WIDE_W_IMPLS.get(tn, _W_IMPLS):
+                    cands.append((tn, impl))
+            code = {c: i + 1 for i, c in enumerate(cands)}
+            inv = {v: k for k, v in code.items()}
+            default = (plan.w_tn, _DEFAULT_IMPL)
+            best = _tune(lambda c: launch_with(*inv[c], scratch, 0), tuple(code.values()),
+                         default=code.get(default))
+            tn, impl = inv[best]
+            plan.w_tn, plan.w_impl = tn, impl
+            plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk)
+    launch_with(plan.w_tn, plan.w_impl, dw, acc)
     return dw
 
 

@@ -119,6 +119,31 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     plan.impl = plan.d_impl = plan.w_impl = 0
 
 
+@pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 176, (1, 1, 1), (0, 0, 0)),
+                                          (96, 288, (3, 1, 1), (1, 0, 0))])
+def test_wgrad_every_tile_and_variant(cin, cout, k, p):
+    """Every (N tile, kernel variant) the wgrad tuner may pick, incl. the wide 96/192 register-staged
+    tiles, against fp32 autograd."""
+    torch.manual_seed(21)
+    h = hip()
+    x = torch.randn(2, 4, 9, 9, cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(cout, cin, *k, device=DEV) * 0.05
+    plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), p)
+    dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
+    xr = x.float().requires_grad_(True)
+    wr = w.to(torch.bfloat16).float().requires_grad_(True)
+    F.conv3d(xr.permute(0, 4, 1, 2, 3), wr, None, 1, p).permute(0, 2, 3, 4, 1).backward(dy.float())
+    tiles = h._wgrad_tiles(cout)
+    assert len(tiles) > 1
+    for tn in tiles:
+        for impl in h._WIDE_W_IMPLS.get(tn, h._W_IMPLS):
+            plan.w_tn, plan.w_impl = tn, impl
+            plan.w_Npad, plan.w_Kpad, plan.w_splits = h._wgrad_geom(cout, plan.Ktot, plan.M, tn, plan.w_tk)
+            dw = h.conv_wgrad(dy, x, plan)
+            assert rel_err(dw, wr.grad) < 1e-2, (tn, impl)
+    plan.w_impl = 0
+
+
 def test_stem_uint8():
     torch.manual_seed(0)
     h = hip()
