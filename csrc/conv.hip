@@ -1140,6 +1140,185 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
 }
 
 // ---------------------------------------------------------------------------------------
+// Stem wgrad (paired-width stem: x2 [B, T, H, W2, 8] bf16, Cout 64, kernel (3, 7, 4), stride
+// (2, 2, 1), padding (1, 3, 2), Wo = W2) as a halo-tiled direct convolution gradient.
+//
+// The generic wgrad gathers the im2col rows of X from L2 for every tap (84 taps x 16 B per
+// output position) and re-reads dY once per K tile. Here a work item is HR = 2 output rows of
+// one (clip, to): its input halo (3 t x (2*HR+5) h x (W2+4) w-pairs, 45 KB at 200x200) and its
+// dY rows (HR*Wo x 64, 25.6 KB) are staged through registers into an LDS double buffer while the
+// previous item is computed, so every input byte is fetched ~3x instead of ~84x. The B operand of tap row
+// (dt, dh) is an overlapping-row image of the halo (row = output position, stride one w-pair,
+// 32 columns = 4 w-pairs x 8 channels) read with ds_read_b64_tr_b16; each wave owns 11 of the
+// 42 16-column K fragments for all 64 output channels (176 accumulators) and keeps them across
+// all of its items; one partial [64][672] per workgroup goes to the slab for wgrad_reduce.
+constexpr int STW_HR = 2;
+constexpr int STW_KF = 42;           // 672 / 16
+constexpr int STW_KFW = 11;          // K fragments per wave (11, 11, 11, 9)
+
+struct StemWgradParams {
+  const bf16_t* dy;  // [M, 64]
+  const bf16_t* x;   // [B, T, H, W2, 8]
+  float* slab;       // [gridDim][64][672]
+  int B, T, H, W2, To, Ho, Wo;
+  int nitems;        // B * To * (Ho / HR)
+  int halo_px;       // 3 * (2*HR+5) * (W2+4)
+  int dy_rows;       // HR * Wo rounded up to 32 (MFMA reduction chunks; tail rows are zero)
+  long long x_bytes, dy_bytes;
+};
+
+__device__ __forceinline__ bf16x8 tr_pair(const bf16_t* a0, const bf16_t* a1) {
+  s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a0);
+  s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)a1);
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+constexpr int STW_HREG = 13;  // halo pixels per thread (<= 3 * 9 * 116 at 224x224)
+constexpr int STW_DREG = 7;   // dY chunks per thread (<= 224 rows x 8 chunks)
+
+__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hrows = 2 * STW_HR + 5, wpx = p.W2 + 4;
+  const int buf_elems = (p.halo_px + p.dy_rows * 8) * 8;  // halo pixels, then dY rows (8 chunks each)
+  bf16_t* const buf0 = (bf16_t*)smem;
+  bf16_t* const buf1 = buf0 + buf_elems;
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const int hg_per = p.Ho / STW_HR;
+  const int real_rows = STW_HR * p.Wo;
+
+  // register staging (T14): the next item's halo and dY are loaded into VGPRs while the current
+  // item is computed from LDS, then written to the other buffer
+  uint4 hreg[STW_HREG], dreg[STW_DREG];
+  auto load = [&](int it) {
+    const int hg = it % hg_per, q = it / hg_per;
+    const int to = q % p.To, b = q / p.To;
+    const int t0 = 2 * to - 1, h0 = 2 * hg * STW_HR - 3;
+#pragma unroll
+    for (int i = 0; i < STW_HREG; ++i) {
+      const int f = tid + 256 * i;
+      const int tt = f / (hrows * wpx), rem = f - tt * (hrows * wpx);
+      const int hh = rem / wpx, wp = rem - hh * wpx;
+      const int ti = t0 + tt, hi = h0 + hh, wi = wp - 2;
+      const bool v = f < p.halo_px && tt < 3 && (unsigned)ti < (unsigned)p.T && (unsigned)hi < (unsigned)p.H &&
+                     (unsigned)wi < (unsigned)p.W2;
+      const uint32_t off = v ? (uint32_t)(((((long long)b * p.T + ti) * p.H + hi) * p.W2 + wi) * 16) : 0x80000000u;
+      hreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+    const long long m0 = ((long long)(b * p.To + to) * p.Ho + hg * STW_HR) * p.Wo;
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + m0 * 64), (short)0, real_rows * 128, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < STW_DREG; ++i) {
+      const int ch = tid + 256 * i;  // chunk = row * 8 + logical column chunk
+      const uint32_t off = ch < real_rows * 8 ? (uint32_t)(ch * 16) : 0x80000000u;
+      dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+    }
+  };
+  auto store = [&](bf16_t* base) {
+#pragma unroll
+    for (int i = 0; i < STW_HREG; ++i) {
+      const int f = tid + 256 * i;
+      if (f < p.halo_px) *(uint4*)(base + f * 8) = hreg[i];
+    }
+    bf16_t* D = base + p.halo_px * 8;
+#pragma unroll
+    for (int i = 0; i < STW_DREG; ++i) {
+      const int ch = tid + 256 * i;
+      const int row = ch >> 3, c = ch & 7;
+      if (row < p.dy_rows) *(uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8) = dreg[i];  // tail rows: zeros
+    }
+  };
+
+  f32x4 acc[4][STW_KFW];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < STW_KFW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  const int kf0 = wave * STW_KFW;
+  const int nchunks = p.dy_rows / 32;
+  // fragments of one 32-position chunk: 4 dY (A) fragments and this wave's 11 X (B) fragments;
+  // chunk c + 1's are read while chunk c's 44 MFMAs run (two register sets)
+  struct Frags {
+    bf16x8 a[4], b[STW_KFW];
+  };
+  auto read_frags = [&](const bf16_t* X, int c, Frags& f) {
+    const bf16_t* D = X + p.halo_px * 8;
+    const int p0 = c * 32;
+#pragma unroll
+    for (int nf = 0; nf < 4; ++nf) f.a[nf] = tr_frag_sw(D, 64, 8, p0, nf * 16, g, qq, pp);
+    int pb[2];  // this lane's two positions (rows of the transposed reads): halo pixel bases
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      int pos = p0 + 4 * g + qq + 16 * h;
+      pos = pos < real_rows ? pos : real_rows - 1;  // tail rows: dY is zero, read any finite pixel
+      const int hr = pos / p.Wo, wo = pos - hr * p.Wo;
+      pb[h] = (2 * hr) * wpx + wo;
+    }
+#pragma unroll
+    for (int j = 0; j < STW_KFW; ++j) {
+      const int kf = min(kf0 + j, STW_KF - 1);
+      const int tr = kf >> 1;  // (dt, dh) tap row
+      const int dt = tr / 7, dh = tr - 7 * (tr / 7);
+      const int poff = (dt * hrows + dh) * wpx + 2 * (kf & 1);
+      f.b[j] = tr_pair(X + (pb[0] + poff) * 8 + pp * 4, X + (pb[1] + poff) * 8 + pp * 4);
+    }
+  };
+  auto mfmas = [&](const Frags& f) {
+#pragma unroll
+    for (int j = 0; j < STW_KFW; ++j) {
+      if (kf0 + j < STW_KF) {
+#pragma unroll
+        for (int nf = 0; nf < 4; ++nf)
+          acc[nf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[nf], f.b[j], acc[nf][j], 0, 0, 0);
+      }
+    }
+  };
+  auto compute = [&](const bf16_t* X) {
+    Frags f0, f1;
+    read_frags(X, 0, f0);
+    int c = 0;
+    for (; c + 2 <= nchunks; c += 2) {
+      read_frags(X, c + 1, f1);
+      mfmas(f0);
+      if (c + 2 < nchunks) read_frags(X, c + 2, f0);
+      mfmas(f1);
+    }
+    if (c < nchunks) mfmas(f0);
+  };
+
+  int it = blockIdx.x;
+  if (it < p.nitems) {
+    load(it);
+    store(buf0);
+  }
+  __syncthreads();
+  for (int k = 0; it < p.nitems; it += gridDim.x, ++k) {
+    const bool more = it + (int)gridDim.x < p.nitems;
+    if (more) load(it + gridDim.x);
+    compute((k & 1) ? buf1 : buf0);
+    if (more) store((k & 1) ? buf0 : buf1);
+    __syncthreads();
+  }
+  // partial dW[n][k] of this workgroup: C[i = n][j = k], row n = 4*(lane>>4) + r, col k = lane & 15
+  float* out = p.slab + (long long)blockIdx.x * 64 * 672;
+#pragma unroll
+  for (int nf = 0; nf < 4; ++nf)
+#pragma unroll
+    for (int j = 0; j < STW_KFW; ++j) {
+      const int kf = kf0 + j;
+      if (kf < STW_KF) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          out[(long long)(nf * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] = acc[nf][j][r];
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Weight packing: fp32 [Cout][Cin_p][KT][KH][KW] -> bf16 [Npad][Kpad]
 //   mode 0 (forward): row n = cout, k = (tap, c)        with c < Cin (c >= Cin_p -> 0)
 //   mode 1 (dgrad)  : row n = cin,  k = (tap', cout)    with tap' = flipped tap
@@ -1399,5 +1578,42 @@ MILNCE_API int milnce_pack_weight(const float* w, void* out, int Cout, int Cin, 
   const int grid = (int)((total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(grid), dim3(256), 0, stream, w, (bf16_t*)out, Cout, Cin, Cin_p,
                      KT, KH, KW, Npad, Kpad, mode);
+  return (int)hipGetLastError();
+}
+
+// Stem wgrad (see stem_wgrad_kernel): dW2 [64][8][3][7][4] (accumulated if `accumulate`).
+// Returns hipErrorInvalidValue for geometries it does not cover (caller falls back).
+MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, float* slab, long long slab_floats, float* dw,
+                                 int B, int T, int H, int W2, int accumulate, hipStream_t stream) {
+  StemWgradParams p;
+  p.dy = (const bf16_t*)dy; p.x = (const bf16_t*)x2; p.slab = slab;
+  p.B = B; p.T = T; p.H = H; p.W2 = W2;
+  p.To = (T + 2 - 3) / 2 + 1;
+  p.Ho = (H + 6 - 7) / 2 + 1;
+  p.Wo = W2;
+  if (p.Ho % STW_HR) return (int)hipErrorInvalidValue;
+  p.nitems = B * p.To * (p.Ho / STW_HR);
+  p.halo_px = 3 * (2 * STW_HR + 5) * (W2 + 4);
+  if (p.halo_px > 256 * STW_HREG || STW_HR * p.Wo > 32 * STW_DREG) return (int)hipErrorInvalidValue;
+  p.dy_rows = (STW_HR * p.Wo + 31) / 32 * 32;
+  p.x_bytes = (long long)B * T * H * W2 * 16;
+  p.dy_bytes = (long long)B * p.To * p.Ho * p.Wo * 128;
+  if (p.x_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)2 * (p.halo_px + p.dy_rows * 8) * 16;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024));
+    attr_set = true;
+  }
+  int grid = 256;
+  if (grid > p.nitems) grid = p.nitems;
+  if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(256), lds, stream, p);
+  HIP_RET(hipGetLastError());
+  const long long total = 64LL * 672;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, slab, dw, grid,
+                     64, 672, 64, 8, 8, 84, accumulate);
   return (int)hipGetLastError();
 }

@@ -268,6 +268,15 @@ def _grad_done(param: torch.Tensor) -> None:
     grad_sink.notify(param)
 
 
+_STEM_WGRAD = os.environ.get("MILNCE_STEM_WGRAD", "1") != "0"
+
+
+def _is_paired_stem(plan: ConvPlan) -> bool:
+    """The paired-width stem conv (csrc/conv.hip stem_wgrad_kernel geometry)."""
+    return (plan.Cin == 8 and plan.Cin_p == 8 and plan.Cout == 64 and plan.k == (3, 7, 4) and
+            plan.s == (2, 2, 1) and plan.p == (1, 3, 2) and plan.Wo == plan.W)
+
+
 def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int) -> Tuple[int, int, int]:
     """(Npad, Kpad, splits) of a wgrad tiling: split-K over m until >= 4 blocks per CU."""
     npad = _ceil(Cout, tn) * tn
@@ -298,6 +307,12 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     acc = int(out is not None)
     dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
+    if _STEM_WGRAD and _is_paired_stem(plan) and x.dtype == BF16:
+        slab = torch.empty((256 * 64 * 672,), dtype=F32, device=dy.device)
+        rc = lib().milnce_stem_wgrad(ptr(dy), ptr(x), ptr(slab), slab.numel(), ptr(dw), plan.B, plan.T, plan.H,
+                                     plan.W, acc, stream())
+        if rc == 0:
+            return dw
 
     def launch_with(tn, impl, target, accumulate):
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk)
