@@ -1319,6 +1319,204 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Stem forward (same paired-width geometry) as a halo-tiled direct convolution with the whole
+// packed weight [64][672] resident in LDS (loaded once per workgroup, rows padded to 1376 B so
+// every ds_read_b128 lane group of the A-fragment reads hits 16 distinct 16-B bank windows). Work item = HR output rows of one (clip, to); its
+// halo is staged through registers (loaded one item ahead) into a single LDS buffer. Every
+// operand address is a per-lane constant plus a compile-time immediate (W2 is a template
+// parameter), so the 21-step K loop is ds_reads + MFMAs only. Waves split the 64 output
+// channels in halves and the item's positions in halves (2 x 7 tiles of 16x16). Epilogue:
+// bf16 stores of 4 channels per lane and BN partial statistics of the stored values, kept in
+// registers across items and reduced once: stats[block][2][64].
+constexpr int STF_LDW = 688;  // padded LDS row of the weight: 86 16-B chunks, conflict-free b128 groups
+
+struct StemFwdParams {
+  const bf16_t* x;   // [B, T, H, W2, 8]
+  const bf16_t* w;   // packed [64][Kpad] bf16
+  bf16_t* y;         // [M, 64]
+  float* stats;      // [gridDim][2][64]
+  int B, T, H, To, Ho, Kpad;
+  int nitems;
+  long long x_bytes;
+};
+
+template <int W2>
+__global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
+  constexpr int HR = STW_HR, WO = W2, WPX = W2 + 4, HROWS = 2 * HR + 5;
+  constexpr int HALO = 3 * HROWS * WPX;
+  constexpr int ROWS = HR * WO;                    // positions per item
+  constexpr int PF = (ROWS + 15) / 16;             // 16-position fragments
+  constexpr int PFW = (PF + 1) / 2;                // per wave (position half 0 takes the extra one)
+  constexpr int HREG = (HALO + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Ws = (bf16_t*)smem;                      // [64][STF_LDW]
+  bf16_t* X = Ws + 64 * STF_LDW;                   // [HALO][8]
+  float* red = (float*)(X + HALO * 8);             // [2][64] stats reduction
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nh = wave & 1, ph = wave >> 1;
+  const int l16 = lane & 15, lg = lane >> 4;
+  const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
+  const int hg_per = p.Ho / HR;
+
+  // weight -> LDS (once)
+  for (int c = tid; c < 64 * 84; c += 256) {
+    const int n = c / 84, k8 = c - n * 84;
+    *(uint4*)(Ws + n * STF_LDW + k8 * 8) = *(const uint4*)(p.w + (long long)n * p.Kpad + k8 * 8);
+  }
+  if (tid < 128) red[tid] = 0.f;
+
+  uint4 hreg[HREG];
+  // item-invariant part of this thread's halo pixels: (tt, hh, wp) packed, -1 past the halo
+  int hgeo[HREG];
+#pragma unroll
+  for (int i = 0; i < HREG; ++i) {
+    const int f = tid + 256 * i;
+    const int tt = f / (HROWS * WPX), rem = f - tt * (HROWS * WPX);
+    const int hh = rem / WPX, wp = rem - hh * WPX;
+    hgeo[i] = f < HALO ? (tt | (hh << 2) | (wp << 8)) : -1;
+  }
+  auto load = [&](int it) {
+    const int hg = it % hg_per, q = it / hg_per;
+    const int to = q % p.To, b = q / p.To;
+    const int t0 = 2 * to - 1, h0 = 2 * hg * HR - 3;
+    const int base = ((b * p.T + t0) * p.H + h0) * W2 - 2;  // pixel index of (tt, hh, wp) = (0, 0, 0)
+#pragma unroll
+    for (int i = 0; i < HREG; ++i) {
+      const int gq = hgeo[i];
+      const int tt = gq & 3, hh = (gq >> 2) & 63, wp = gq >> 8;
+      const bool v = gq >= 0 && (unsigned)(t0 + tt) < (unsigned)p.T && (unsigned)(h0 + hh) < (unsigned)p.H &&
+                     (unsigned)(wp - 2) < (unsigned)W2;
+      const uint32_t off = v ? (uint32_t)((base + (tt * p.H + hh) * W2 + wp) * 16) : 0x80000000u;
+      hreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < HREG; ++i) {
+      const int f = tid + 256 * i;
+      if (f < HALO) *(uint4*)(X + f * 8) = hreg[i];
+    }
+  };
+
+  // per-lane constant operand addresses (bytes): A rows of the two channel fragments, B pixels
+  // of this wave's position fragments (tail positions clamped to a real one; never stored)
+  uint32_t abase[2], bbase[PFW];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf)
+    abase[nf] = (uint32_t)(((nh * 32 + nf * 16 + l16) * STF_LDW + lg * 8) * 2);
+  const int pf0 = ph == 0 ? 0 : PFW;
+  const int npf = ph == 0 ? PFW : PF - PFW;
+#pragma unroll
+  for (int j = 0; j < PFW; ++j) {
+    int pos = (pf0 + j) * 16 + l16;
+    pos = pos < ROWS ? pos : ROWS - 1;
+    const int hr = pos / WO, wo = pos - hr * WO;
+    // absolute LDS byte address (X follows the weight), so only the per-step tap offset
+    // (<= 40 KB) is left for the ds_read immediate
+    bbase[j] = (uint32_t)(64 * STF_LDW * 2 + (((2 * hr) * WPX + wo + lg) * 8) * 2);
+  }
+  const char* Wb = (const char*)Ws;
+  const char* Xb = (const char*)smem;
+
+  float s1[2][4], s2[2][4];
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s1[nf][r] = 0.f; s2[nf][r] = 0.f; }
+
+  int it = blockIdx.x;
+  if (it < p.nitems) {
+    load(it);
+    store();
+  }
+  if (it + (int)gridDim.x < p.nitems) load(it + gridDim.x);
+  __syncthreads();
+  for (; it < p.nitems; it += gridDim.x) {
+    f32x4 acc[2][PFW];
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+      for (int j = 0; j < PFW; ++j) acc[nf][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 21; ++ks) {
+      constexpr int dummy = 0;
+      (void)dummy;
+      const int dt = ks / 7, dh = ks % 7;
+      const uint32_t boff = (uint32_t)(((dt * HROWS + dh) * WPX) * 16);
+      bf16x8 af[2], bf[PFW];
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) af[nf] = *(const bf16x8*)(Wb + abase[nf] + ks * 64);
+#pragma unroll
+      for (int j = 0; j < PFW; ++j) bf[j] = *(const bf16x8*)(Xb + bbase[j] + boff);
+#pragma unroll
+      for (int j = 0; j < PFW; ++j)
+        if (j < npf)
+#pragma unroll
+          for (int nf = 0; nf < 2; ++nf)
+            acc[nf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nf], bf[j], acc[nf][j], 0, 0, 0);
+    }
+    // epilogue: C[i = n][j = p]: lane holds channels 4*lg + r of position l16
+    const int hg = it % hg_per, q = it / hg_per;
+    const long long m0 = ((long long)q * p.Ho + hg * HR) * WO;
+#pragma unroll
+    for (int j = 0; j < PFW; ++j) {
+      const int pos = (pf0 + j) * 16 + l16;
+      if (j < npf && pos < ROWS) {
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          const f32x4 v = acc[nf][j];
+          uint2 o;
+          o.x = pack2bf(v[0], v[1]);
+          o.y = pack2bf(v[2], v[3]);
+          *(uint2*)(p.y + (m0 + pos) * 64 + nh * 32 + nf * 16 + lg * 4) = o;
+          const float q0 = __uint_as_float(o.x << 16), q1 = __uint_as_float(o.x & 0xffff0000u);
+          const float q2 = __uint_as_float(o.y << 16), q3 = __uint_as_float(o.y & 0xffff0000u);
+          s1[nf][0] += q0; s1[nf][1] += q1; s1[nf][2] += q2; s1[nf][3] += q3;
+          s2[nf][0] += q0 * q0; s2[nf][1] += q1 * q1; s2[nf][2] += q2 * q2; s2[nf][3] += q3 * q3;
+        }
+      }
+    }
+    __syncthreads();  // every wave done reading this item's halo
+    const bool more = it + (int)gridDim.x < p.nitems;
+    if (more) store();
+    if (it + 2 * (int)gridDim.x < p.nitems) load(it + 2 * gridDim.x);
+    __syncthreads();
+  }
+  // statistics: reduce over the 16 lanes of a channel group, then over the position-half waves
+#pragma unroll
+  for (int nf = 0; nf < 2; ++nf)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float a = s1[nf][r], b2 = s2[nf][r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b2 += __shfl_xor(b2, o, 64); }
+      if (l16 == 0) {
+        const int c = nh * 32 + nf * 16 + lg * 4 + r;
+        atomicAdd(&red[c], a);
+        atomicAdd(&red[64 + c], b2);
+      }
+    }
+  __syncthreads();
+  if (tid < 128) p.stats[(long long)blockIdx.x * 128 + tid] = red[tid];
+}
+
+template <int W2>
+static int launch_stem_fwd(StemFwdParams& p, int grid, hipStream_t stream) {
+  constexpr int HALO = 3 * (2 * STW_HR + 5) * (W2 + 4);
+  const size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + 128 * 4;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)stem_fwd_kernel<W2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(stem_fwd_kernel<W2>, dim3(grid), dim3(256), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // Weight packing: fp32 [Cout][Cin_p][KT][KH][KW] -> bf16 [Npad][Kpad]
 //   mode 0 (forward): row n = cout, k = (tap, c)        with c < Cin (c >= Cin_p -> 0)
 //   mode 1 (dgrad)  : row n = cin,  k = (tap', cout)    with tap' = flipped tap
@@ -1616,4 +1814,29 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, float* slab, lo
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, slab, dw, grid,
                      64, 672, 64, 8, 8, 84, accumulate);
   return (int)hipGetLastError();
+}
+
+// Stem forward (see stem_fwd_kernel): y [M, 64] bf16 and BN partials stats[nparts][2][64];
+// returns the number of partial rows written (> 0), or a negative value for geometries it does
+// not cover (the caller falls back to the generic implicit GEMM).
+MILNCE_API int milnce_stem_fwd(const void* x2, const void* wpacked, int Kpad, void* y, float* stats,
+                               long long stats_floats, int B, int T, int H, int W2, hipStream_t stream) {
+  StemFwdParams p;
+  p.x = (const bf16_t*)x2; p.w = (const bf16_t*)wpacked; p.y = (bf16_t*)y; p.stats = stats;
+  p.B = B; p.T = T; p.H = H; p.Kpad = Kpad;
+  p.To = (T + 2 - 3) / 2 + 1;
+  p.Ho = (H + 6 - 7) / 2 + 1;
+  if (p.Ho % STW_HR || Kpad < 672) return -1;
+  p.nitems = B * p.To * (p.Ho / STW_HR);
+  p.x_bytes = (long long)B * T * H * W2 * 16;
+  if (p.x_bytes > 0x7FFFFFF0LL) return -1;
+  int grid = 256;
+  if (grid > p.nitems) grid = p.nitems;
+  if ((long long)grid * 128 > stats_floats) return -1;
+  int rc;
+  if (W2 == 100) rc = launch_stem_fwd<100>(p, grid, stream);
+  else if (W2 == 112) rc = launch_stem_fwd<112>(p, grid, stream);
+  else if (W2 == 32) rc = launch_stem_fwd<32>(p, grid, stream);
+  else return -1;
+  return rc ? -rc - 1000 : grid;
 }

@@ -37,6 +37,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_maxpool_s1_bwd_fused": [P, P, P, P, P, P] + [I] * 5 + [P],
     "milnce_set_pool_s1_impl": [I],
     "milnce_stem_wgrad": [P, P, P, L, P, I, I, I, I, I, P],
+    "milnce_stem_fwd": [P, P, I, P, P, L, I, I, I, I, P],
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],

@@ -269,6 +269,7 @@ def _grad_done(param: torch.Tensor) -> None:
 
 
 _STEM_WGRAD = os.environ.get("MILNCE_STEM_WGRAD", "1") != "0"
+_STEM_FWD = os.environ.get("MILNCE_STEM_FWD", "1") != "0"
 
 
 def _is_paired_stem(plan: ConvPlan) -> bool:
@@ -353,11 +354,25 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     plan = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
     dev = x.device
     wp = _pack(weight, plan, 0)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
-    y = conv_forward_raw(x, wp, plan, stats)
+    nparts = plan.grid_m
+    y = None
+    if _STEM_FWD and _is_paired_stem(plan) and x.dtype == BF16:
+        # halo-tiled stem kernel (csrc/conv.hip stem_fwd_kernel); its statistics rows are per workgroup
+        y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=dev)
+        stats = torch.empty((256 * 128,), dtype=F32, device=dev)
+        rc = lib().milnce_stem_fwd(ptr(x), ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
+                                   plan.H, plan.W, stream())
+        if rc > 0:
+            nparts = rc
+        else:
+            y = None
+    if y is None:
+        nparts = plan.grid_m
+        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+        y = conv_forward_raw(x, wp, plan, stats)
     C = plan.Cout
     ss = torch.empty((4 * C,), dtype=F32, device=dev)
-    call("milnce_bn_finalize", ptr(stats), plan.grid_m, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
+    call("milnce_bn_finalize", ptr(stats), nparts, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
          ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(momentum), float(eps), int(training),
          ptr(ss), stream())
     return plan, y, ss

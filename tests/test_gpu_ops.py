@@ -630,3 +630,31 @@ def test_stem_wgrad_halo_kernel(B, T, S):
     acc = dw.clone()
     h.conv_wgrad(dy, x2, plan, out=acc)
     assert rel_err(acc, 2 * dw) < 1e-5
+
+
+@pytest.mark.parametrize("B,T,S", [(2, 8, 64), (1, 4, 200)])
+def test_stem_fwd_halo_kernel(B, T, S):
+    """Halo-tiled stem forward (LDS-resident weights) vs the fp32 conv of the paired-width
+    formulation, and its BN partial statistics vs the sums of the stored outputs."""
+    from mil_nce_howto100m_amd.ops._lib import lib, ptr, stream
+    torch.manual_seed(32)
+    h = hip()
+    W2 = S // 2
+    x2 = torch.randn(B, T, S, W2, 8, device=DEV).to(torch.bfloat16)
+    x2[..., 3] = 0
+    x2[..., 7] = 0
+    w2 = torch.randn(64, 8, 3, 7, 4, device=DEV) * 0.05
+    plan = h.conv_plan(x2.shape, w2.shape, (2, 2, 1), (1, 3, 2), W2)
+    wp = h._pack(w2, plan, 0)
+    y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, 64), dtype=torch.bfloat16, device=DEV)
+    stats = torch.empty((256 * 128,), device=DEV)
+    n = lib().milnce_stem_fwd(ptr(x2), ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
+                              plan.H, plan.W, stream())
+    assert n > 0
+    xr = x2.float().permute(0, 4, 1, 2, 3)
+    yr = F.conv3d(xr, w2.to(torch.bfloat16).float(), None, (2, 2, 1), (1, 3, 2))[..., :W2].permute(0, 2, 3, 4, 1)
+    assert rel_err(y, yr) < 1e-2
+    st = stats[: n * 128].view(n, 2, 64).sum(0)
+    yf = y.float().reshape(-1, 64)
+    assert rel_err(st[0], yf.sum(0)) < 1e-4
+    assert rel_err(st[1], (yf * yf).sum(0)) < 1e-4
