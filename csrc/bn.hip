@@ -12,35 +12,56 @@
 #include "common.h"
 
 // ---------------------------------------------------------------------------------------
-// Block = 32 channels x 8 partial-row groups; the partial slab [nparts][2][Npad] is read
-// coalesced along channels and reduced in fp64 (nparts can be ~1000 per-block partials).
-__global__ __launch_bounds__(256) void bn_finalize_kernel(
+// Partial-slab reductions ([nparts][2][stride] fp32 -> per-channel fp64 sums). They are
+// latency-bound (a few MB over few channels), so a block is 8 channels x 128 row groups of
+// 1024 threads: each thread sums ~nparts/128 rows with two chains in flight, then a fixed-order
+// LDS tree reduces the 128 groups (deterministic).
+constexpr int FIN_CH = 8, FIN_RG = 128;
+
+__device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int nparts, int stride, int c, bool ok,
+                                           double& s1, double& s2) {
+  __shared__ double red[2][FIN_RG][FIN_CH];
+  const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
+  double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+  if (ok) {
+    int i = rg;
+    for (; i + FIN_RG < nparts; i += 2 * FIN_RG) {
+      const float* p0 = part + (long long)i * 2 * stride + c;
+      const float* p1 = p0 + (long long)FIN_RG * 2 * stride;
+      a1 += (double)p0[0];
+      a2 += (double)p0[stride];
+      b1 += (double)p1[0];
+      b2 += (double)p1[stride];
+    }
+    for (; i < nparts; i += FIN_RG) {
+      a1 += (double)part[(long long)i * 2 * stride + c];
+      a2 += (double)part[(long long)i * 2 * stride + stride + c];
+    }
+  }
+  red[0][rg][cl] = a1 + b1;
+  red[1][rg][cl] = a2 + b2;
+  __syncthreads();
+#pragma unroll
+  for (int h = FIN_RG / 2; h >= 1; h >>= 1) {
+    if (rg < h) {
+      red[0][rg][cl] += red[0][rg + h][cl];
+      red[1][rg][cl] += red[1][rg + h][cl];
+    }
+    __syncthreads();
+  }
+  s1 = red[0][0][cl];
+  s2 = red[1][0][cl];
+}
+
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
     float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */) {
-  __shared__ double red[2][8][32];
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
+  const int c = blockIdx.x * FIN_CH + threadIdx.x % FIN_CH;
   if (training && blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
-  double s = 0.0, q = 0.0;
-  if (training && c < C) {
-    int i = rg;
-    for (; i + 24 < nparts; i += 32) {
-      const float* p0 = part + (long long)i * 2 * Npad + c;
-      const long long st = 8LL * 2 * Npad;
-      s += (double)p0[0] + (double)p0[st] + (double)p0[2 * st] + (double)p0[3 * st];
-      q += (double)p0[Npad] + (double)p0[st + Npad] + (double)p0[2 * st + Npad] + (double)p0[3 * st + Npad];
-    }
-    for (; i < nparts; i += 8) {
-      s += (double)part[(long long)i * 2 * Npad + c];
-      q += (double)part[(long long)i * 2 * Npad + Npad + c];
-    }
-  }
-  red[0][rg][cl] = s;
-  red[1][rg][cl] = q;
-  __syncthreads();
-  if (rg != 0 || c >= C) return;
-  for (int k = 1; k < 8; ++k) { s += red[0][k][cl]; q += red[1][k][cl]; }
+  double s, q;
+  fin_reduce(part, training ? nparts : 0, Npad, c, training && c < C, s, q);
+  if (threadIdx.x >= FIN_CH || c >= C) return;
   float mean, var;
   if (training) {
     const double m = s / count;
@@ -182,44 +203,15 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
 // part rows have stride 2*ps (ps = C for bn_bwd_reduce partials, Npad for conv-epilogue partials).
-// 1024 threads = 32 channels x 32 row groups; each thread keeps two independent fp64 chains
-// so consecutive partial rows are in flight together (the reduction is latency-, not
-// bandwidth-bound: a few MB spread over C/32 blocks).
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps,
                                                                int C, double count, const float* __restrict__ gamma,
                                                                const float* __restrict__ ss,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                float* __restrict__ coef, int accumulate, int batch_stats) {
-  __shared__ double red[2][32][33];
-  const int cl = threadIdx.x & 31, rg = threadIdx.x >> 5;
-  const int c = blockIdx.x * 32 + cl;
-  double s1 = 0.0, s2 = 0.0, t1 = 0.0, t2 = 0.0;
-  if (c < C) {
-    int i = rg;
-    for (; i + 96 < nparts; i += 128) {  // four rows per thread in flight
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float* a = part + (long long)(i + 32 * u) * 2 * ps + c;
-        v[2 * u] = a[0];
-        v[2 * u + 1] = a[ps];
-      }
-      s1 += (double)v[0] + (double)v[2];
-      s2 += (double)v[1] + (double)v[3];
-      t1 += (double)v[4] + (double)v[6];
-      t2 += (double)v[5] + (double)v[7];
-    }
-    for (; i < nparts; i += 32) {
-      s1 += part[(long long)i * 2 * ps + c];
-      s2 += part[(long long)i * 2 * ps + ps + c];
-    }
-  }
-  red[0][rg][cl] = s1 + t1;
-  red[1][rg][cl] = s2 + t2;
-  __syncthreads();
-  if (rg != 0 || c >= C) return;
-  s1 = 0.0; s2 = 0.0;
-  for (int k = 0; k < 32; ++k) { s1 += red[0][k][cl]; s2 += red[1][k][cl]; }
+  const int c = blockIdx.x * FIN_CH + threadIdx.x % FIN_CH;
+  double s1, s2;
+  fin_reduce(part, nparts, ps, c, c < C, s1, s2);
+  if (threadIdx.x >= FIN_CH || c >= C) return;
   // accumulate: dgamma/dbeta are the parameters' gradient buffers (written in place, += across
   // gradient-accumulation passes); otherwise fresh outputs
   dbeta[c] = accumulate ? dbeta[c] + (float)s1 : (float)s1;
@@ -269,7 +261,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 MILNCE_API int milnce_bn_finalize(const float* part, int nparts, int Npad, int C, double count, const float* gamma,
                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
                                   float eps, int training, float* out, hipStream_t stream) {
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 31) / 32), dim3(256), 0, stream, part, nparts, Npad, C,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream, part,
+                     nparts, Npad, C,
                      count, gamma, beta, rmean, rvar, nbt, momentum, eps, training, out);
   return (int)hipGetLastError();
 }
@@ -303,7 +296,8 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
                        (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
     ps = C;
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 31) / 32), dim3(1024), 0, stream, part, nparts, ps, C,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
+                     part, nparts, ps, C,
                      (double)M, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   const int rpi = 256 / (C / 8);
   long long nblk = (M + 16LL * rpi - 1) / (16LL * rpi);  // >= 16 rows per thread

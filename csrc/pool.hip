@@ -331,7 +331,9 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
                                                      const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                      uint32_t npos, uint32_t pos_per_block,
                                                      const bf16_t* __restrict__ bn_y, int bn_ld,
-                                                     const float* __restrict__ bn_ss, float* __restrict__ part) {
+                                                     const float* __restrict__ bn_ss, float* __restrict__ part,
+                                                     const bf16_t* __restrict__ gx = nullptr,
+                                                     float* __restrict__ gs = nullptr) {
   __shared__ float red[16 * 256];
   const int cpr = p.C >> 3, rpi = 256 / cpr;
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
@@ -342,15 +344,47 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
   acc_bn.zero();
   const uint32_t pos_begin = blockIdx.x * pos_per_block;
   const uint32_t pos_end = min(npos, pos_begin + pos_per_block);
+  // gate reduction of the pool input's producer (SelfGating): gs[b, c] += sum dx * gx, flushed
+  // with one atomic per channel whenever the thread's clip changes
+  const uint32_t plane = (uint32_t)p.T * p.H * p.W;
+  float sacc[8];
+  uint32_t cur_b = 0xffffffffu;
+  auto gs_add = [&](uint32_t ps, const uint4& v, const uint4& xg) {
+    const uint32_t bb = ps / plane;
+    if (bb != cur_b) {
+      if (cur_b != 0xffffffffu) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sacc[k] = 0.f;
+      cur_b = bb;
+    }
+    float q[8], xv[8];
+    unpack8(v, q);
+    unpack8(xg, xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sacc[k] += q[k] * xv[k];
+  };
   for (uint32_t pos = pos_begin + rr; active && pos < pos_end; pos += 2 * rpi) {
     const uint32_t pos2 = pos + rpi;
     const bool two = pos2 < pos_end;
     float a0[8], a1[8];
+    // the gate operand rows are loaded up front, with the gather's loads
+    uint4 xg0 = make_uint4(0, 0, 0, 0), xg1 = make_uint4(0, 0, 0, 0);
+    if (gs != nullptr) {
+      xg0 = *(const uint4*)(gx + (size_t)pos * p.C + c0);
+      xg1 = *(const uint4*)(gx + (size_t)(two ? pos2 : pos) * p.C + c0);
+    }
     pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, pos, c0, a0);
     pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, two ? pos2 : pos, c0, a1);
     const uint4 v0 = pack8(a0), v1 = pack8(a1);
     *(uint4*)(dx + (size_t)pos * p.C + c0) = v0;
     if (two) *(uint4*)(dx + (size_t)pos2 * p.C + c0) = v1;
+    if (gs != nullptr) {
+      gs_add(pos, v0, xg0);
+      if (two) gs_add(pos2, v1, xg1);
+    }
     if (bn) {
       float dr[8];
       unpack8(v0, dr);
@@ -360,6 +394,10 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
         acc_bn.add(dr, bn_y + (size_t)pos2 * bn_ld + c0, bn_ss, p.C, c0);
       }
     }
+  }
+  if (gs != nullptr && cur_b != 0xffffffffu) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
   }
   if (bn) acc_bn.commit(red, part, p.C, cpr, rpi, cc, rr, active);
 }
@@ -856,7 +894,7 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
 
 static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* arg, void* dx, long long n,
                              const void* bn_y, int bn_ld, const float* bn_ss, float* part, int nparts,
-                             hipStream_t s) {
+                             hipStream_t s, const void* gx = nullptr, float* gs = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
   if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
@@ -880,7 +918,8 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
 #define X(a, b, c, e, f, h)                                                                                      \
   if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                              \
     hipLaunchKernelGGL((maxpool_bwd_t<a, b, c, e, f, h>), dim3(nparts), dim3(256), 0, s, p, d, (const bf16_t*)dy, \
-                       (const uint8_t*)arg, (bf16_t*)dx, npos, ppb, (const bf16_t*)bn_y, bn_ld, bn_ss, part);    \
+                       (const uint8_t*)arg, (bf16_t*)dx, npos, ppb, (const bf16_t*)bn_y, bn_ld, bn_ss, part,     \
+                       (const bf16_t*)gx, gs);                                                                    \
     return true;                                                                                                 \
   }
   MILNCE_POOL_SHAPES(X)
@@ -959,4 +998,20 @@ MILNCE_API int milnce_maxpool_s1_bwd_fused(const void* dy, const void* arg, cons
                      s1_bwd_lds(rows, G), stream, p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg,
                      (const bf16_t*)acc_in, (const bf16_t*)x, gs, (bf16_t*)dx);
   return (int)hipGetLastError();
+}
+
+// TF-SAME pool backward whose input x is a SelfGating output: dx as milnce_maxpool_bwd (no BN
+// partials) plus gs[b, c] += sum_thw dx * x (gs zeroed by the caller), which the gate backward
+// uses instead of re-reading its gradient and output.
+MILNCE_API int milnce_maxpool_bwd_gate(const void* dy, const void* arg, void* dx, int B, int T, int H, int W, int C,
+                                       int To, int Ho, int Wo, int kt, int kh, int kw, int st, int sh, int sw,
+                                       int pt0, int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad,
+                                       const void* x, float* gs, int nparts, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256) return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
+  const long long n = (long long)B * T * H * W * (C / 8);
+  if (is_s1_333(p)) return (int)hipErrorInvalidValue;
+  if (pool_bwd_special(p, dy, arg, dx, n, nullptr, 0, nullptr, nullptr, nparts, stream, x, gs))
+    return (int)hipGetLastError();
+  return (int)hipErrorInvalidValue;
 }

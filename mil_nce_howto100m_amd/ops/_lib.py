@@ -38,6 +38,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_set_pool_s1_impl": [I],
     "milnce_stem_wgrad": [P, P, P, L, P, I, I, I, I, I, P],
     "milnce_stem_fwd": [P, P, I, P, P, L, I, I, I, I, P],
+    "milnce_maxpool_bwd_gate": [P, P, P] + [I] * 21 + [P, P, I, P],
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],

@@ -881,20 +881,33 @@ class _MaxPool(torch.autograd.Function):
         geo = [B, T, H, W, C, To, Ho, Wo, *kernel, *stride, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
                pads[2][0], pads[2][1], zero_pad]
         call("milnce_maxpool_fwd", ptr(x), ptr(y), ptr(arg), *geo, stream())
-        ctx.save_for_backward(arg)
         ctx.geo = geo
         xb = getattr(x, "_milnce_bn", None)
         special = (tuple(kernel), tuple(stride)) in _POOL_SPECIAL  # csrc/pool.hip MILNCE_POOL_SHAPES
         ctx.x_bn = xb if (xb is not None and (special or (256 % (C // 8) == 0 and xb[2] == C))) else None
+        # a SelfGating output: the backward also returns the gate's reduction sum dx * x
+        ctx.x_gate = bool(getattr(x, "_milnce_gate", False)) and special and tf_same and ctx.x_bn is None
+        if ctx.x_gate:
+            ctx.save_for_backward(arg, x)
+        else:
+            ctx.save_for_backward(arg)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        (arg,) = ctx.saved_tensors
+        arg = ctx.saved_tensors[0]
         geo = ctx.geo
         B, T, H, W, C = geo[:5]
         dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dy.device)
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
+        if ctx.x_gate:
+            x = ctx.saved_tensors[1]
+            gs = torch.zeros((B, C), dtype=F32, device=dy.device)
+            call("milnce_maxpool_bwd_gate", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo, ptr(x), ptr(gs), nparts,
+                 stream())
+            dx._milnce_gs = gs
+            dx._milnce_gsver = dx._version
+            return dx, None, None, None
         xb = ctx.x_bn
         part = torch.empty((nparts * 2 * C,), dtype=F32, device=dy.device) if xb is not None else None
         call("milnce_maxpool_bwd", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo,

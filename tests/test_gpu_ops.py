@@ -658,3 +658,30 @@ def test_stem_fwd_halo_kernel(B, T, S):
     yf = y.float().reshape(-1, 64)
     assert rel_err(st[0], yf.sum(0)) < 1e-4
     assert rel_err(st[1], (yf * yf).sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("kernel,stride", [((1, 3, 3), (1, 2, 2)), ((3, 3, 3), (2, 2, 2)), ((2, 2, 2), (2, 2, 2))])
+def test_pool_backward_gate_sum(kernel, stride):
+    """SelfGating -> TF-SAME pool: the pool backward's fused gate reduction (sum dx * x, used by
+    the gate backward instead of its own reduce pass) gives the same gradients as the unfused
+    reduce on the same bf16 values."""
+    torch.manual_seed(41)
+    h = hip()
+    B, T, HW, C = 3, 4, 13, 64
+    z = torch.rand(B, T, HW, HW, C, device=DEV).to(torch.bfloat16)
+    fc = nn.Linear(C, C).to(DEV)
+    res = []
+    d = None
+    for fused in (True, False):
+        fc.weight.grad = fc.bias.grad = None
+        zh = z.clone().requires_grad_(True)
+        x = h.gate_concat([zh], [fc.weight], [fc.bias], [z.float().sum(dim=(1, 2, 3))])
+        if not fused:
+            x._milnce_gate = False
+        y = h.maxpool3d(x, kernel, stride, True)
+        if d is None:
+            d = torch.randn_like(y.float()).to(torch.bfloat16)
+        y.backward(d)
+        res.append((zh.grad.float(), fc.weight.grad.clone(), fc.bias.grad.clone()))
+    for a, b in zip(*res):
+        assert rel_err(a, b) < 1e-2
