@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
         f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
         acc[k] += f[k];
       }
-      *(uint4*)(z + row * ldz + c0) = pack8(f);
+      if (z != nullptr) *(uint4*)(z + row * ldz + c0) = pack8(f);  // z == null: gating sums only
     }
   }
   if (gsum == nullptr) return;
@@ -306,5 +306,73 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
   const int rpb = (int)((M + nblk - 1) / nblk);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((int)nblk), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
                      (const bf16_t*)y, ldy, ss, coef, C, M, rpb, (bf16_t*)dy, lddy);
+  return (int)hipGetLastError();
+}
+
+// BN-backward finalize only (dgamma, dbeta, coef from the partials) for consumers that apply the
+// BN backward inside their own pass (pool.hip milnce_maxpool_bwd_apply).
+MILNCE_API int milnce_bn_bwd_finalize(const float* part, int nparts, int ps, int C, double count,
+                                      const float* gamma, const float* ss, float* dgamma, float* dbeta, float* coef,
+                                      int accumulate, int batch_stats, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
+                     part, nparts, ps, C, count, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Lazy SelfGating gradient: the layer's dz is the gate backward's bf16(dout * g + dmean / thw)
+// (gate.hip gate_bwd_apply_kernel produced the BN partials without storing dz); it is rebuilt here
+// from dout. Grid (splits, B): g and dmean are per clip. dout / g / dmean point at the branch's
+// first channel, with row strides ldo (dout) and ldg (g, dmean).
+__global__ __launch_bounds__(256) void bn_bwd_apply_gate_kernel(
+    const bf16_t* __restrict__ dout, int ldo, const float* __restrict__ g, const float* __restrict__ dmean, int ldg,
+    float inv_thw, int thw, int rows_per_block, const bf16_t* __restrict__ y, int ldy,
+    const float* __restrict__ ss, const float* __restrict__ coef, int C, bf16_t* __restrict__ dy, int lddy) {
+  const int cpr = C >> 3, rpi = 256 / cpr;
+  const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
+  if (rr >= rpi) return;
+  const int c0 = cc * 8, b = blockIdx.y;
+  float sc[8], sh[8], mean[8], istd[8], k0[8], k1[8], k2[8], gg[8], dm[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = c0 + k;
+    mean[k] = ss[c]; istd[k] = ss[C + c]; sc[k] = ss[2 * C + c]; sh[k] = ss[3 * C + c];
+    k0[k] = coef[c]; k1[k] = coef[C + c]; k2[k] = coef[2 * C + c];
+    gg[k] = g[(size_t)b * ldg + c];
+    dm[k] = dmean[(size_t)b * ldg + c] * inv_thw;
+  }
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
+  const size_t row0 = (size_t)b * thw;
+#pragma unroll 4
+  for (int r = r_begin + rr; r < r_end; r += rpi) {
+    const size_t row = row0 + r;
+    float d[8], v[8], o[8];
+    unpack8(*(const uint4*)(dout + row * ldo + c0), d);
+    unpack8(*(const uint4*)(y + row * ldy + c0), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float dz = bf2f(f2bf(fmaf(d[k], gg[k], dm[k])));  // the value gate_bwd_apply reduced
+      const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? dz : 0.f;
+      const float xh = (v[k] - mean[k]) * istd[k];
+      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+    }
+    *(uint4*)(dy + row * lddy + c0) = pack8(o);
+  }
+}
+
+// milnce_bn_bwd with a lazy SelfGating dz (see bn_bwd_apply_gate_kernel); the partials are required.
+MILNCE_API int milnce_bn_bwd_gate(const void* dout, int ldo, const float* g, const float* dmean, int ldg, int B,
+                                  int thw, const void* y, int ldy, const float* ss, int C, const float* gamma,
+                                  float* part, int nparts, int ps, float* dgamma, float* dbeta, float* coef, void* dy,
+                                  int lddy, int accumulate, int batch_stats, hipStream_t stream) {
+  if (C % 8 || C > 2048) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
+                     part, nparts, ps, C, (double)B * thw, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
+  const int rpi = 256 / (C / 8);
+  int splits = (thw + 16 * rpi - 1) / (16 * rpi);  // >= 16 rows per thread
+  if (splits < 1) splits = 1;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(bn_bwd_apply_gate_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)dout, ldo, g,
+                     dmean, ldg, 1.f / thw, thw, rpb, (const bf16_t*)y, ldy, ss, coef, C, (bf16_t*)dy, lddy);
   return (int)hipGetLastError();
 }

@@ -528,7 +528,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-    __syncthreads();  // tap table ready; previous tile's epilogue done with the LDS
+    // LDS-only barrier: the previous tile's output stores stay in flight (a __syncthreads() would
+    // wait for them); the ring's counted vmcnt waits stay exact, older stores only add to the count
+    ring_barrier();  // tap table ready; previous tile's epilogue done with the LDS
 
     auto issue = [&](int kt) {
       bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
@@ -596,7 +598,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave done reading the ring before the epilogue reuses it
+    ring_barrier();  // every wave done reading the ring before the epilogue reuses it
 
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -611,7 +613,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
         *(uint2*)(Es + row * LDE + col) = o;
       }
     }
-    __syncthreads();
+    ring_barrier();
     // store: thread = fixed 16-B chunk column cc of RPP rows per pass (BN/8 need not divide the
     // block size; the EPI 2 partials then accumulate per fixed channel chunk)
     constexpr int OCPR = BN / 8;
@@ -922,7 +924,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
         compute(0);
         wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg2, xreg2, Ds + R * LDN, Xs + R * LDK, tid, d_ccol,
                                                          x_ccol, p.in_scale);
-        __syncthreads();
+        lds_barrier();  // LDS only: the loads of stage s + 2 stay in flight across the barrier
       }
       if (s + 1 >= nsteps) break;
       // odd step s+1: stage s+1 in LDS buf 1 / set 1 free; stage s+2 in flight in set 0
@@ -935,7 +937,7 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
           wgrad_row_table(rtab + ((s + 4) & 3) * R, p, m_begin + (s + 4) * R, m_end, b_first, tid);
         compute(1);
         wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
-        __syncthreads();
+        lds_barrier();
       }
     }
   }
@@ -1478,11 +1480,11 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
         }
       }
     }
-    __syncthreads();  // every wave done reading this item's halo
+    lds_barrier();  // every wave done reading this item's halo (output stores stay in flight)
     const bool more = it + (int)gridDim.x < p.nitems;
     if (more) store();
     if (it + 2 * (int)gridDim.x < p.nitems) load(it + 2 * gridDim.x);
-    __syncthreads();
+    lds_barrier();  // LDS only: the register prefetch of item it + 2 * grid stays in flight
   }
   // statistics: reduce over the 16 lanes of a channel group, then over the position-half waves
 #pragma unroll

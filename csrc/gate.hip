@@ -24,6 +24,7 @@ struct SegTable {
   const bf16_t* bn_y[MAXSEG];   // producer BN raw output of each branch (backward partials), or null
   const float* bn_ss[MAXSEG];   // its [mean, invstd, scale, shift]
   int bn_ld[MAXSEG];            // row stride of bn_y
+  int lazy[MAXSEG];             // forward: branch z not materialised, z = bf16(relu(bn_y*scale+shift))
 };
 
 __device__ __forceinline__ int seg_of(const SegTable& t, int c) {
@@ -69,8 +70,24 @@ __global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float
 #pragma unroll
   for (int k = 0; k < 8; ++k) gg[k] = g[(size_t)b * Ctot + c + k];
   const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
-  const bf16_t* zs = t.z[s] + (size_t)b * thw * C + cl;
   bf16_t* o = out + (size_t)b * thw * Ctot + c;
+  if (t.lazy[s]) {
+    // z = relu(y * scale + shift) rounded to bf16 (the value bn_relu_apply would have stored)
+    float sc[8], sh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { sc[k] = t.bn_ss[s][2 * C + cl + k]; sh[k] = t.bn_ss[s][3 * C + cl + k]; }
+    const bf16_t* ys = t.bn_y[s] + (size_t)b * thw * t.bn_ld[s] + cl;
+#pragma unroll 4
+    for (int r = r_begin + rr; r < r_end; r += rpi) {
+      float f[8];
+      unpack8(*(const uint4*)(ys + (size_t)r * t.bn_ld[s]), f);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f))) * gg[k];
+      *(uint4*)(o + (size_t)r * Ctot) = pack8(f);
+    }
+    return;
+  }
+  const bf16_t* zs = t.z[s] + (size_t)b * thw * C + cl;
 #pragma unroll 4
   for (int r = r_begin + rr; r < r_end; r += rpi) {
     float f[8];
@@ -173,9 +190,10 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
       float d[8];
       unpack8(*(const uint4*)(dout + row * Ctot + c), d);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = d[k] * gg[k] + dm[k];
+      for (int k = 0; k < 8; ++k) d[k] = fmaf(d[k], gg[k], dm[k]);
       const uint4 dv = pack8(d);
-      *(uint4*)(t.dz[s] + row * C + cl) = dv;
+      // dz == null: lazy gradient, rebuilt from dout by the BN backward (bn.hip milnce_bn_bwd_gate)
+      if (t.dz[s] != nullptr) *(uint4*)(t.dz[s] + row * C + cl) = dv;
       if (bn) {
         float y[8], dr[8];
         unpack8(dv, dr);  // partials from the stored (bf16) gradient
@@ -284,6 +302,7 @@ static SegTable make_table(int nseg, const int* widths, const void* const* z, vo
     t.bn_y[i] = nullptr;
     t.bn_ss[i] = nullptr;
     t.bn_ld[i] = 0;
+    t.lazy[i] = 0;
   }
   return t;
 }
@@ -293,15 +312,27 @@ static int grid_for(long long n) {
   return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
 }
 
+// lazy (may be null): per-branch flag; a lazy branch's z is read as relu(bn_y * scale + shift)
+// from (bn_y[i], bn_ld[i], bn_ss[i]) instead of z[i].
 MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z, const float* const* w,
                                const float* const* bias, const float* gsum, int B, int thw, float* mean, float* g,
-                               void* out, hipStream_t stream) {
+                               void* out, const int* lazy, const void* const* bn_y, const float* const* bn_ss,
+                               const int* bn_ld, hipStream_t stream) {
   SegTable t = make_table(nseg, widths, z, nullptr, w, bias, nullptr, nullptr);
+  for (int i = 0; i < nseg && lazy != nullptr; ++i) {
+    t.lazy[i] = lazy[i];
+    if (lazy[i]) {
+      t.bn_y[i] = (const bf16_t*)bn_y[i];
+      t.bn_ss[i] = bn_ss[i];
+      t.bn_ld[i] = bn_ld[i];
+    }
+  }
   const int Ctot = t.off[nseg];
   int cmax = 0;
   for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
   hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum,
                      1.f / thw, Ctot, mean, g);
+  if (out == nullptr) return (int)hipGetLastError();  // gate values only: a fused consumer applies them
   if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
   const int rpi = 256 / (Ctot / 8);
   const int splits = (thw + 32 * rpi - 1) / (32 * rpi);  // >= 32 row iterations per thread
@@ -345,6 +376,21 @@ MILNCE_API int milnce_gate_bwd_apply(int nseg, const int* widths, void* const* d
   const int rpb = (thw + splits - 1) / splits;
   hipLaunchKernelGGL(gate_bwd_apply_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, g, dmean,
                      Ctot, thw, 1.f / thw, rpb, part);
+  return (int)hipGetLastError();
+}
+
+// gs[b, c] += sum over the clip's rows of a[row, c] * v[row, c]  (a, v: [B * rows_per_b, C] bf16; gs
+// zeroed by the caller): the SelfGating reduction taken on a pooled gate output (hip_ops._GatedPool).
+MILNCE_API int milnce_gate_dot(const void* a, const void* v, int B, int rows_per_b, int C, float* gs,
+                               hipStream_t stream) {
+  if (C % 8 || C > 2048) return (int)hipErrorInvalidValue;
+  const int widths[1] = {C};
+  const void* zs[1] = {v};
+  SegTable t = make_table(1, widths, zs, nullptr, nullptr, nullptr, nullptr, nullptr);
+  const int splits = (rows_per_b + 511) / 512;
+  const int rpb = (rows_per_b + splits - 1) / splits;
+  hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)a, C,
+                     rows_per_b, rpb, gs);
   return (int)hipGetLastError();
 }
 

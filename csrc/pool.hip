@@ -165,7 +165,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolParams p, const bf
 // clamped address and masked afterwards, so the whole window's loads are in flight at once
 // (the generic kernels above serialise on their per-tap branches).
 struct PoolDivs {
-  FastDiv fcpr, fWo, fHo, fTo, fW, fH, fT;
+  FastDiv fcpr, fWo, fHo, fTo, fW, fH, fT, fplane;  // fplane: T * H * W (input clip)
 };
 
 // BN: x is the raw conv output of a train-mode BN layer and z = relu(x * scale + shift) is
@@ -174,7 +174,8 @@ struct PoolDivs {
 template <int KT, int KH, int KW, int ST, int SH, int SW, bool BN = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ x,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
-                                                     uint32_t nout_chunks, const float* __restrict__ ss = nullptr) {
+                                                     uint32_t nout_chunks, const float* __restrict__ ss = nullptr,
+                                                     const float* __restrict__ gate = nullptr) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nout_chunks; i += gridDim.x * blockDim.x) {
     uint32_t r = fdiv(i, d.fcpr);
     const int c0 = (int)(i - r * d.fcpr.d) * 8;
@@ -202,7 +203,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
           const size_t off = in[t] ? ((size_t)(ti * p.H + hi) * p.W + wi) * p.C : 0;
           v[t] = *(const uint4*)(xb + off);
         }
-    float best[8], sc[8], sh[8];
+    float best[8], sc[8], sh[8], gv[8];
     uint32_t bi[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -211,6 +212,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
       if constexpr (BN) {
         sc[k] = ss[2 * p.C + c0 + k];
         sh[k] = ss[3 * p.C + c0 + k];
+        gv[k] = gate != nullptr ? gate[(size_t)b * p.C + c0 + k] : 1.f;
       }
     }
 #pragma unroll
@@ -220,6 +222,10 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
       if constexpr (BN) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f)));  // = the stored z
+        if (gate != nullptr) {  // SelfGating output z * gate[b, c], as gate_scale would store it
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(f[k] * gv[k]));
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -325,32 +331,43 @@ __device__ __forceinline__ void pool_bwd_one(const PoolParams& p, const PoolDivs
 
 // Thread = fixed 8-channel chunk cc = tid % cpr of rpi = 256/cpr input positions per step; block
 // blockIdx.x walks positions [pos_begin, pos_end), two positions per thread per iteration so
-// both gathers' loads are in flight together.
-template <int KT, int KH, int KW, int ST, int SH, int SW>
+// both gathers' loads are in flight together. MODE (compile time, so every variant keeps only
+// the registers it needs):
+//   POOL_BWD_PLAIN  dx = gathered gradient (+ BN partials of the producer, + SelfGating sums gs)
+//   POOL_BWD_GATED  dx = bf16(gathered * g[b, c] + dmean[b, c] / thw): the producer gate's input
+//                   gradient (its reduction already done), + BN partials; dx may be null
+//   POOL_BWD_APPLY  dx = BN backward of the (optionally gated, gate_g != null) gradient with the
+//                   finalised coefficients coef: the producer conv's output gradient
+enum { POOL_BWD_PLAIN = 0, POOL_BWD_GATED = 1, POOL_BWD_APPLY = 2 };
+
+template <int KT, int KH, int KW, int ST, int SH, int SW, int MODE = POOL_BWD_PLAIN>
 __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ dy,
                                                      const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                      uint32_t npos, uint32_t pos_per_block,
                                                      const bf16_t* __restrict__ bn_y, int bn_ld,
                                                      const float* __restrict__ bn_ss, float* __restrict__ part,
                                                      const bf16_t* __restrict__ gx = nullptr,
-                                                     float* __restrict__ gs = nullptr) {
+                                                     float* __restrict__ gs = nullptr,
+                                                     const float* __restrict__ gate_g = nullptr,
+                                                     const float* __restrict__ gate_dm = nullptr,
+                                                     float inv_thw = 0.f, const float* __restrict__ coef = nullptr) {
   __shared__ float red[16 * 256];
   const int cpr = p.C >> 3, rpi = 256 / cpr;
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
   const bool active = rr < rpi;
   const int c0 = cc * 8;
-  const bool bn = bn_y != nullptr;
+  const bool bn = MODE != POOL_BWD_APPLY && bn_y != nullptr && part != nullptr;  // BN partial sums of dz
+  const bool gated = MODE == POOL_BWD_GATED || (MODE == POOL_BWD_APPLY && gate_g != nullptr);
   BnAcc acc_bn;
   acc_bn.zero();
   const uint32_t pos_begin = blockIdx.x * pos_per_block;
   const uint32_t pos_end = min(npos, pos_begin + pos_per_block);
   // gate reduction of the pool input's producer (SelfGating): gs[b, c] += sum dx * gx, flushed
   // with one atomic per channel whenever the thread's clip changes
-  const uint32_t plane = (uint32_t)p.T * p.H * p.W;
   float sacc[8];
   uint32_t cur_b = 0xffffffffu;
   auto gs_add = [&](uint32_t ps, const uint4& v, const uint4& xg) {
-    const uint32_t bb = ps / plane;
+    const uint32_t bb = fdiv(ps, d.fplane);
     if (bb != cur_b) {
       if (cur_b != 0xffffffffu) {
 #pragma unroll
@@ -366,22 +383,65 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
 #pragma unroll
     for (int k = 0; k < 8; ++k) sacc[k] += q[k] * xv[k];
   };
+  // SelfGating backward of the producer: dz = bf16(dx * g + dmean / thw), per-clip constants
+  float gcur[8], dcur[8];
+  uint32_t gb = 0xffffffffu;
+  auto gate_apply = [&](uint32_t ps, uint4& v) {
+    const uint32_t bb = fdiv(ps, d.fplane);
+    if (bb != gb) {
+      gb = bb;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        gcur[k] = gate_g[(size_t)bb * p.C + c0 + k];
+        dcur[k] = gate_dm[(size_t)bb * p.C + c0 + k] * inv_thw;
+      }
+    }
+    float q[8];
+    unpack8(v, q);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = fmaf(q[k], gcur[k], dcur[k]);
+    v = pack8(q);
+  };
+  // BN backward constants of this thread's channels (APPLY): dy = k0 * (dz*mask - k1 - xhat*k2)
+  float bsc[8], bsh[8], bmu[8], bis[8], k0[8], k1[8], k2[8];
+  if constexpr (MODE == POOL_BWD_APPLY) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = active ? c0 + k : 0;
+      bmu[k] = bn_ss[c]; bis[k] = bn_ss[p.C + c]; bsc[k] = bn_ss[2 * p.C + c]; bsh[k] = bn_ss[3 * p.C + c];
+      k0[k] = coef[c]; k1[k] = coef[p.C + c]; k2[k] = coef[2 * p.C + c];
+    }
+  }
+  auto bn_apply = [&](uint32_t ps, uint4& v) {
+    float dz[8], yv[8], o[8];
+    unpack8(v, dz);
+    unpack8(*(const uint4*)(bn_y + (size_t)ps * bn_ld + c0), yv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float gm = (yv[k] * bsc[k] + bsh[k] > 0.f) ? dz[k] : 0.f;
+      const float xh = (yv[k] - bmu[k]) * bis[k];
+      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+    }
+    v = pack8(o);
+  };
   for (uint32_t pos = pos_begin + rr; active && pos < pos_end; pos += 2 * rpi) {
     const uint32_t pos2 = pos + rpi;
     const bool two = pos2 < pos_end;
     float a0[8], a1[8];
     // the gate operand rows are loaded up front, with the gather's loads
     uint4 xg0 = make_uint4(0, 0, 0, 0), xg1 = make_uint4(0, 0, 0, 0);
-    if (gs != nullptr) {
+    if (MODE == POOL_BWD_PLAIN && gs != nullptr) {
       xg0 = *(const uint4*)(gx + (size_t)pos * p.C + c0);
       xg1 = *(const uint4*)(gx + (size_t)(two ? pos2 : pos) * p.C + c0);
     }
     pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, pos, c0, a0);
     pool_bwd_one<KT, KH, KW, ST, SH, SW>(p, d, dy, arg, two ? pos2 : pos, c0, a1);
-    const uint4 v0 = pack8(a0), v1 = pack8(a1);
-    *(uint4*)(dx + (size_t)pos * p.C + c0) = v0;
-    if (two) *(uint4*)(dx + (size_t)pos2 * p.C + c0) = v1;
-    if (gs != nullptr) {
+    uint4 v0 = pack8(a0), v1 = pack8(a1);
+    if (gated) {
+      gate_apply(pos, v0);
+      if (two) gate_apply(pos2, v1);
+    }
+    if (MODE == POOL_BWD_PLAIN && gs != nullptr) {
       gs_add(pos, v0, xg0);
       if (two) gs_add(pos2, v1, xg1);
     }
@@ -394,8 +454,16 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
         acc_bn.add(dr, bn_y + (size_t)pos2 * bn_ld + c0, bn_ss, p.C, c0);
       }
     }
+    if constexpr (MODE == POOL_BWD_APPLY) {
+      bn_apply(pos, v0);
+      if (two) bn_apply(pos2, v1);
+    }
+    if (dx != nullptr) {  // null: BN partial sums only (a later APPLY pass re-gathers dz)
+      *(uint4*)(dx + (size_t)pos * p.C + c0) = v0;
+      if (two) *(uint4*)(dx + (size_t)pos2 * p.C + c0) = v1;
+    }
   }
-  if (gs != nullptr && cur_b != 0xffffffffu) {
+  if (MODE == POOL_BWD_PLAIN && gs != nullptr && cur_b != 0xffffffffu) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
   }
@@ -836,6 +904,7 @@ static PoolDivs make_divs(const PoolParams& p) {
   d.fcpr = make_fastdiv(p.C / 8);
   d.fWo = make_fastdiv(p.Wo); d.fHo = make_fastdiv(p.Ho); d.fTo = make_fastdiv(p.To);
   d.fW = make_fastdiv(p.W); d.fH = make_fastdiv(p.H); d.fT = make_fastdiv(p.T);
+  d.fplane = make_fastdiv(p.T * p.H * p.W);
   return d;
 }
 
@@ -848,7 +917,7 @@ static bool is_s1_333(const PoolParams& p) {
 }
 
 static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s,
-                             const float* bn_ss = nullptr) {
+                             const float* bn_ss = nullptr, const float* gate = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
   if (bn_ss != nullptr) {
@@ -857,7 +926,7 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
 #define X(a, b, c, e, f, h)                                                                                      \
     if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                            \
       hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true>), dim3(grid), dim3(256), 0, s, p, d,             \
-                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss);                       \
+                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);                       \
       return true;                                                                                               \
     }
     MILNCE_POOL_SHAPES(X)
@@ -894,7 +963,9 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
 
 static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* arg, void* dx, long long n,
                              const void* bn_y, int bn_ld, const float* bn_ss, float* part, int nparts,
-                             hipStream_t s, const void* gx = nullptr, float* gs = nullptr) {
+                             hipStream_t s, const void* gx = nullptr, float* gs = nullptr,
+                             const float* gate_g = nullptr, const float* gate_dm = nullptr, float inv_thw = 0.f,
+                             const float* coef = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
   if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
@@ -915,15 +986,19 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   }
   const uint32_t npos = (uint32_t)(n / (p.C / 8));
   const uint32_t ppb = (npos + nparts - 1) / nparts;
-#define X(a, b, c, e, f, h)                                                                                      \
-  if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                              \
-    hipLaunchKernelGGL((maxpool_bwd_t<a, b, c, e, f, h>), dim3(nparts), dim3(256), 0, s, p, d, (const bf16_t*)dy, \
+  const int mode = coef != nullptr ? POOL_BWD_APPLY : (gate_g != nullptr ? POOL_BWD_GATED : POOL_BWD_PLAIN);
+#define XM(a, b, c, e, f, h, m)                                                                                  \
+  if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h && mode == m) {                 \
+    hipLaunchKernelGGL((maxpool_bwd_t<a, b, c, e, f, h, m>), dim3(nparts), dim3(256), 0, s, p, d, (const bf16_t*)dy, \
                        (const uint8_t*)arg, (bf16_t*)dx, npos, ppb, (const bf16_t*)bn_y, bn_ld, bn_ss, part,     \
-                       (const bf16_t*)gx, gs);                                                                    \
+                       (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef);                                                                    \
     return true;                                                                                                 \
   }
+#define X(a, b, c, e, f, h) XM(a, b, c, e, f, h, POOL_BWD_PLAIN) XM(a, b, c, e, f, h, POOL_BWD_GATED) \
+  XM(a, b, c, e, f, h, POOL_BWD_APPLY)
   MILNCE_POOL_SHAPES(X)
 #undef X
+#undef XM
   return false;
 }
 
@@ -977,6 +1052,7 @@ MILNCE_API int milnce_maxpool_bwd(const void* dy, const void* arg, void* dx, int
   PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
   const long long n = (long long)B * T * H * W * (C / 8);
   if (pool_bwd_special(p, dy, arg, dx, n, bn_y, bn_ld, bn_ss, part, nparts, stream)) return (int)hipGetLastError();
+  if (dx == nullptr) return (int)hipErrorInvalidValue;  // partials-only passes: specialised shapes
   if (bn_y != nullptr && (256 % (C / 8) != 0 || bn_ld != C)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(nparts), dim3(256), 0, stream, p, (const bf16_t*)dy,
                      (const uint8_t*)arg, (bf16_t*)dx, n, (const bf16_t*)bn_y, bn_ss, part);
@@ -1012,6 +1088,63 @@ MILNCE_API int milnce_maxpool_bwd_gate(const void* dy, const void* arg, void* dx
   const long long n = (long long)B * T * H * W * (C / 8);
   if (is_s1_333(p)) return (int)hipErrorInvalidValue;
   if (pool_bwd_special(p, dy, arg, dx, n, nullptr, 0, nullptr, nullptr, nparts, stream, x, gs))
+    return (int)hipGetLastError();
+  return (int)hipErrorInvalidValue;
+}
+
+// SelfGating of a lazy BN-ReLU input followed by a TF-SAME max pool, in one pass over the raw conv
+// output x: pools bf16(bf16(relu(x * scale + shift)) * gate[b, c]), the gate output the unfused ops
+// would store (specialised window shapes only).
+MILNCE_API int milnce_bn_relu_gate_maxpool_fwd(const void* x, const float* ss, const float* gate, void* y, void* arg,
+                                               int B, int T, int H, int W, int C, int To, int Ho, int Wo, int kt,
+                                               int kh, int kw, int st, int sh, int sw, int pt0, int pt1, int ph0,
+                                               int ph1, int pw0, int pw1, int zero_pad, hipStream_t stream) {
+  if (C % 8 || gate == nullptr) return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
+  const long long n = (long long)B * To * Ho * Wo * (C / 8);
+  if (!pool_fwd_special(p, x, y, arg, n, stream, ss, gate)) return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// Its backward down to the BN layer: dz = bf16(bf16(pool_bwd(dy)) * g + dmean / thw), the SelfGating
+// backward once its reduction (milnce_gate_dot on the pooled output) and fc backward are done, plus
+// the BN-backward partials of dz (thw = T * H * W). dz may be null (partials only).
+MILNCE_API int milnce_maxpool_bwd_gated(const void* dy, const void* arg, void* dz, int B, int T, int H, int W, int C,
+                                        int To, int Ho, int Wo, int kt, int kh, int kw, int st, int sh, int sw,
+                                        int pt0, int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad,
+                                        const void* bn_y, int bn_ld, const float* bn_ss, float* part, int nparts,
+                                        const float* g, const float* dmean, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256 || bn_y == nullptr || g == nullptr || dmean == nullptr) return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
+  const long long n = (long long)B * T * H * W * (C / 8);
+  if (is_s1_333(p)) return (int)hipErrorInvalidValue;
+  const int thw = T * H * W;
+  const float inv_thw = 1.f / thw;
+  if (pool_bwd_special(p, dy, arg, dz, n, bn_y, bn_ld, bn_ss, part, nparts, stream, nullptr, nullptr, g, dmean,
+                       inv_thw))
+    return (int)hipGetLastError();
+  return (int)hipErrorInvalidValue;
+}
+
+// Pool backward with the BN backward of the pool input's producer applied on the fly (dz gated as in
+// milnce_maxpool_bwd_gated when g != null): out = the producer conv's output gradient, so the
+// full-resolution dz is never stored. coef = milnce_bn_bwd_finalize of the partials a first pass
+// (milnce_maxpool_bwd / milnce_maxpool_bwd_gated with dz = null) produced.
+MILNCE_API int milnce_maxpool_bwd_apply(const void* dy, const void* arg, void* out, int B, int T, int H, int W, int C,
+                                        int To, int Ho, int Wo, int kt, int kh, int kw, int st, int sh, int sw,
+                                        int pt0, int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad,
+                                        const void* bn_y, int bn_ld, const float* bn_ss, const float* coef,
+                                        const float* g, const float* dmean, int nparts, hipStream_t stream) {
+  if (C % 8 || C / 8 > 256 || bn_y == nullptr || coef == nullptr || out == nullptr ||
+      (g == nullptr) != (dmean == nullptr))
+    return (int)hipErrorInvalidValue;
+  PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
+  const long long n = (long long)B * T * H * W * (C / 8);
+  if (is_s1_333(p)) return (int)hipErrorInvalidValue;
+  const int thw = T * H * W;
+  const float inv_thw = 1.f / thw;
+  if (pool_bwd_special(p, dy, arg, out, n, bn_y, bn_ld, bn_ss, nullptr, nparts, stream, nullptr, nullptr, g, dmean,
+                       inv_thw, coef))
     return (int)hipGetLastError();
   return (int)hipErrorInvalidValue;
 }

@@ -244,8 +244,8 @@ class S3D(nn.Module):
             net = ops.maxpool_tf_same(net, *self.maxpool_2a)
         net = self.conv_2b(net)
         net, gsum = self.conv_2c(net, want_gsum=True)
-        net = self.gating(net, gsum)
-        net = ops.maxpool_tf_same(net, *self.maxpool_3a)
+        # SelfGating + maxpool_3a (fused on GPU: the full-resolution gate output is never stored)
+        net = ops.gated_maxpool_tf_same(net, gsum, self.gating.fc.weight, self.gating.fc.bias, *self.maxpool_3a)
         for name in self._plan:
             if name.startswith("maxpool"):
                 net = ops.maxpool_tf_same(net, *getattr(self, name))

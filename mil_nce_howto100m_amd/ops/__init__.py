@@ -94,6 +94,13 @@ def maxpool_tf_same(x, kernel, stride):
     return aten.maxpool_tf_same(x, kernel, stride)
 
 
+def gated_maxpool_tf_same(z, gsum, fc_weight, fc_bias, kernel, stride):
+    """SelfGating(z) then a TF-SAME max pool (conv_2c -> gating -> maxpool_3a)."""
+    if use_hip(z):
+        return _hip().gated_maxpool(z, gsum, fc_weight, fc_bias, kernel, stride)
+    return aten.maxpool_tf_same(aten.gate_concat([z], [fc_weight], [fc_bias]), kernel, stride)
+
+
 def maxpool_s1(x):
     if use_hip(x):
         return _hip().maxpool3d(x, (3, 3, 3), (1, 1, 1), tf_same=False)

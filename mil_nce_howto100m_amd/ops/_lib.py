@@ -26,7 +26,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
     "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, I, I, P],
-    "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P],
+    "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P],
     "milnce_gate_bwd_reduce": [I, P, P, P, P, I, I, P, P],
     "milnce_gate_bwd_apply": [I, P, P, P, P, P, I, I, P, P, P, P, I, P],
     "milnce_avgpool": [P, I, I, I, P, P],
@@ -39,6 +39,12 @@ SIGNATURES: Dict[str, list] = {
     "milnce_stem_wgrad": [P, P, P, L, P, I, I, I, I, I, P],
     "milnce_stem_fwd": [P, P, I, P, P, L, I, I, I, I, P],
     "milnce_maxpool_bwd_gate": [P, P, P] + [I] * 21 + [P, P, I, P],
+    "milnce_bn_relu_gate_maxpool_fwd": [P, P, P, P, P] + [I] * 21 + [P],
+    "milnce_maxpool_bwd_gated": [P, P, P] + [I] * 21 + [P, I, P, P, I, P, P, P],
+    "milnce_maxpool_bwd_apply": [P, P, P] + [I] * 21 + [P, I, P, P, P, P, I, P],
+    "milnce_gate_dot": [P, P, I, I, I, P, P],
+    "milnce_bn_bwd_gate": [P, I, P, P, I, I, I, P, I, P, I, P, P, I, I, P, P, P, P, I, I, I, P],
+    "milnce_bn_bwd_finalize": [P, I, I, I, D, P, P, P, P, P, I, I, P],
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],

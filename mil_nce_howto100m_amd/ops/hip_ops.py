@@ -225,6 +225,72 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
 
 _FUSE_BN_BWD = True
 
+# BN-ReLU outputs that only feed a SelfGating are not materialised: the producer computes just
+# the gating sums, returns a stride-0 placeholder tagged with (y, ss, ld), and the gate applies
+# relu(y * scale + shift) while scaling (csrc/gate.hip lazy segments).
+_LAZY_GATE_Z = os.environ.get("MILNCE_LAZY_GATE_Z", "1") != "0"
+# Gradients that only feed their producer's BN backward are not stored either ("lazy dz"):
+#  * SelfGating inputs: the gate backward computes only the BN partial sums and the BN backward
+#    rebuilds dz = bf16(dout * g + dmean / thw) from dout (milnce_bn_bwd_gate);
+#  * pool inputs (stem -> maxpool_2a, gate -> maxpool_3a): the pool backward computes only the BN
+#    partial sums and a second gather pass applies the BN backward (milnce_maxpool_bwd_apply).
+#    Off by default: the second gather costs as much as the dz round trip it saves (A/B on MI355X:
+#    78.6 vs 78.3 ms/step).
+_LAZY_GATE_DZ = os.environ.get("MILNCE_LAZY_GATE_DZ", "1") != "0"
+_LAZY_POOL_DZ = os.environ.get("MILNCE_LAZY_POOL_DZ", "0") == "1"
+
+
+def _lazy_z(shape, device, bn_info) -> torch.Tensor:
+    z = torch.empty((1,), dtype=BF16, device=device).expand(*shape)
+    z._milnce_bn = bn_info
+    z._milnce_lazy = True
+    return z
+
+
+def _is_lazy(t) -> bool:
+    return bool(getattr(t, "_milnce_lazy", False))
+
+
+def _materialize(z: torch.Tensor) -> torch.Tensor:
+    """The bf16 relu(y * scale + shift) a lazy placeholder stands for."""
+    y, ss, ld = z._milnce_bn
+    out = torch.empty(z.shape, dtype=BF16, device=z.device)
+    B = z.shape[0]
+    thw = out.numel() // (B * z.shape[-1])
+    call("milnce_bn_relu_apply", ptr(y), ld, ptr(out), z.shape[-1], ptr(ss), z.shape[-1], B, thw, None, stream())
+    return out
+
+
+def _lazy_dz(shape, device, info) -> torch.Tensor:
+    """Placeholder for a gradient that is not stored (see ``_LAZY_GATE_DZ``); info =
+    ("gate", dout, channel offset, g, dmean, thw) or ("pool", dout, arg, geo, g, dmean, nparts)."""
+    dz = torch.empty((1,), dtype=BF16, device=device).expand(*shape)
+    dz._milnce_lazydz = info
+    return dz
+
+
+def _lazy_dz_info(dz):
+    return getattr(dz, "_milnce_lazydz", None) if dz is not None else None
+
+
+def _bn_bwd_lazy(info, B, M, y, ldy, ss, C, gamma, part, nparts, ps, dgamma, dbeta, coef, dy, lddy, accumulate,
+                 training):
+    """BN backward whose dz is a lazy gradient (see ``_lazy_dz``)."""
+    if info[0] == "gate":
+        _, dout, off, g, dmean, thw = info
+        ld = dout.shape[-1]
+        call("milnce_bn_bwd_gate", ptr(dout) + 2 * off, ld, ptr(g) + 4 * off, ptr(dmean) + 4 * off, ld, B, thw,
+             ptr(y), ldy, ptr(ss), C, ptr(gamma), ptr(part), nparts, ps, ptr(dgamma), ptr(dbeta), ptr(coef),
+             ptr(dy), lddy, int(accumulate), int(training), stream())
+        return
+    _, dout, arg, geo, g, dmean, pool_parts = info
+    if lddy != C:
+        raise RuntimeError("lazy pool gradient needs a dense output gradient")
+    call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(M), ptr(gamma), ptr(ss), ptr(dgamma), ptr(dbeta),
+         ptr(coef), int(accumulate), int(training), stream())
+    call("milnce_maxpool_bwd_apply", ptr(dout), ptr(arg), ptr(dy), *geo, ptr(y), ldy, ptr(ss), ptr(coef), ptr(g),
+         ptr(dmean), pool_parts, stream())
+
 
 def set_bn_bwd_fusion(enabled: bool) -> bool:
     """Toggle producer-side BN-backward partial sums (for A/B tests); returns the old value."""
@@ -383,10 +449,14 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     partials when the producer of dz attached them), dgrad, wgrad; BN and weight gradients are
     accumulated in place into flat-buffer grads when possible."""
     plan: ConvPlan = ctx.plan
-    dz = dz.contiguous()
+    lazy = _lazy_dz_info(dz)
+    if lazy is None:
+        dz = dz.contiguous()
     C = plan.Cout
     dev = dz.device
     fused = take_bn_partials(dz)
+    if lazy is not None and fused is None:
+        raise RuntimeError("lazy gradient without its BN partial sums")
     if fused is not None:
         part, nparts, ps = fused
     else:
@@ -400,9 +470,13 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     dgamma = g_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
     dbeta = b_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
     dy = torch.empty_like(y)
-    call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
-         int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, int(direct_bn),
-         int(ctx.training), stream())
+    if lazy is not None:
+        _bn_bwd_lazy(lazy, plan.B, plan.M, y, C, ss, C, gamma, part, nparts, ps, dgamma, dbeta, coef, dy, C,
+                     direct_bn, ctx.training)
+    else:
+        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps,
+             int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef), ptr(dy), C, int(direct_bn),
+             int(ctx.training), stream())
     if direct_bn:
         _grad_done(gamma)
         _grad_done(beta)
@@ -428,10 +502,11 @@ class _ConvBNReLU(torch.autograd.Function):
         plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
                                      training, wo_override)
         C = plan.Cout
-        z = torch.empty_like(y)
         gsum = torch.zeros((plan.B, C), dtype=F32, device=x.device) if want_gsum else None
-        call("milnce_bn_relu_apply", ptr(y), C, ptr(z), C, ptr(ss), C, plan.B, plan.To * plan.Ho * plan.Wo,
-             ptr(gsum), stream())
+        lazy = want_gsum and _LAZY_GATE_Z
+        z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
+        call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
+             plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
         ctx.save_for_backward(x, weight, y, ss, gamma)
         ctx.beta = beta  # parameter handle only (its gradient buffer may be written in place)
         ctx.training = bool(training)
@@ -483,11 +558,18 @@ class _ConvBNReLUPool(torch.autograd.Function):
         x, weight, y, ss, gamma, arg = ctx.saved_tensors
         geo = ctx.geo
         B, T, H, W, C = geo[:5]
-        dz = torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
+        dout = dout.contiguous()
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
         part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
-        call("milnce_maxpool_bwd", ptr(dout.contiguous()), ptr(arg), ptr(dz), *geo, ptr(y), C, ptr(ss), ptr(part),
-             nparts, stream())
+        if _LAZY_POOL_DZ and _FUSE_BN_BWD:
+            # BN partial sums only; the BN backward re-gathers dz and applies itself in one pass
+            call("milnce_maxpool_bwd", ptr(dout), ptr(arg), None, *geo, ptr(y), C, ptr(ss), ptr(part), nparts,
+                 stream())
+            dz = _lazy_dz((B, T, H, W, C), dout.device, ("pool", dout, arg, geo, None, None, nparts))
+        else:
+            dz = torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
+            call("milnce_maxpool_bwd", ptr(dout), ptr(arg), ptr(dz), *geo, ptr(y), C, ptr(ss), ptr(part), nparts,
+                 stream())
         attach_bn_partials(dz, part, nparts, C)
         dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
@@ -609,10 +691,13 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
         call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
              ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
              float(hyper[i][1]), int(training), ptr(ss), stream())
-        z = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev)
         g = torch.zeros((plan.B, c), dtype=F32, device=dev) if (i == 0 and want_gsum0) else None
         ysl = y2[:, off:off + c]
-        call("milnce_bn_relu_apply", ptr(ysl), ctot, ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g), stream())
+        lazy = g is not None and _LAZY_GATE_Z
+        z = (_lazy_z((plan.B, plan.To, plan.Ho, plan.Wo, c), dev, (ysl, ss, ctot)) if lazy
+             else torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev))
+        call("milnce_bn_relu_apply", ptr(ysl), ctot, None if lazy else ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g),
+             stream())
         z._milnce_bn = (ysl, ss, ctot)
         zs.append(z)
         sss.append(ss)
@@ -646,8 +731,12 @@ def _group_backward(ctx, grads, saved=None):
         dz = grads[i]
         if dz is None:
             dz = torch.zeros((plan.M, c), dtype=BF16, device=dev)
-        dz = dz.contiguous()
+        lazy = _lazy_dz_info(dz)
+        if lazy is None:
+            dz = dz.contiguous()
         fused = take_bn_partials(dz)
+        if lazy is not None and fused is None:
+            raise RuntimeError("lazy gradient without its BN partial sums")
         if fused is not None:
             part, nparts, ps = fused
         else:
@@ -659,9 +748,13 @@ def _group_backward(ctx, grads, saved=None):
         direct_bn = g_direct is not None and b_direct is not None
         dgamma = g_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
         dbeta = b_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
-        call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
-             ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
-             ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
+        if lazy is not None:
+            _bn_bwd_lazy(lazy, plan.B, plan.M, y2[:, off:], ctot, sss[i], c, gammas[i], part, nparts, ps, dgamma,
+                         dbeta, coef, dY[:, off:], ctot, direct_bn, ctx.training)
+        else:
+            call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
+                 ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
+                 ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
         if direct_bn:
             _grad_done(gammas[i])
             _grad_done(ctx.betas[i])
@@ -784,12 +877,17 @@ class _GateConcat(torch.autograd.Function):
         mean = torch.empty((B, ctot), dtype=F32, device=dev)
         g = torch.empty((B, ctot), dtype=F32, device=dev)
         out = torch.empty((B, T, H, W, ctot), dtype=BF16, device=dev)
+        lazy = [int(_is_lazy(z)) for z in zs]
+        bn_info = [z._milnce_bn if _is_lazy(z) else (None, None, 0) for z in zs]
         call("milnce_gate_fwd", nseg, _arr(ctypes.c_int, widths), _arr(ctypes.c_void_p, [ptr(z) for z in zs]),
              _arr(ctypes.c_void_p, [ptr(w) for w in ws]), _arr(ctypes.c_void_p, [ptr(b) for b in bs]),
-             ptr(gsum), B, thw, ptr(mean), ptr(g), ptr(out), stream())
+             ptr(gsum), B, thw, ptr(mean), ptr(g), ptr(out), _arr(ctypes.c_int, lazy),
+             _arr(ctypes.c_void_p, [ptr(i[0]) for i in bn_info]), _arr(ctypes.c_void_p, [ptr(i[1]) for i in bn_info]),
+             _arr(ctypes.c_int, [int(i[2]) for i in bn_info]), stream())
         ctx.save_for_backward(*zs, *ws, g, mean)
         ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
         ctx.z_bn = [getattr(z, "_milnce_bn", None) for z in zs]
+        ctx.lazy = lazy
         out._milnce_gate = True  # consumers may return sum_thw dout * out with the gradient
         return out
 
@@ -804,7 +902,6 @@ class _GateConcat(torch.autograd.Function):
         B = g.shape[0]
         ctot = g.shape[1]
         dev = dout.device
-        dzs = [torch.empty_like(z) for z in zs]
         widths = _arr(ctypes.c_int, ctx.widths)
         gs = take_gate_sums(dout)
         if gs is not None:
@@ -812,7 +909,8 @@ class _GateConcat(torch.autograd.Function):
             dpre = gs * (1.0 - g)
         else:
             dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
-            call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zs]), ptr(dout),
+            zr = [_materialize(z) if _is_lazy(z) else z for z in zs]
+            call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zr]), ptr(dout),
                  ptr(g), B, ctx.thw, ptr(dpre), stream())
         # per-branch fc backward: plain GEMMs on hipBLASLt
         dmean = torch.empty((B, ctot), dtype=F32, device=dev)
@@ -827,7 +925,13 @@ class _GateConcat(torch.autograd.Function):
         have_bn = all(zb is not None for zb in ctx.z_bn)
         nparts = B * int(max(1, min(_ceil(2048, B), _ceil(ctx.thw, 128))))
         part = torch.empty((nparts * 2 * ctot,), dtype=F32, device=dev) if have_bn else None
-        call("milnce_gate_bwd_apply", nseg, widths, _arr(ctypes.c_void_p, [ptr(d) for d in dzs]), ptr(dout),
+        # a lazy input's gradient is not stored either: its BN backward rebuilds it from dout
+        lazy_dz = [bool(have_bn and _FUSE_BN_BWD and _LAZY_GATE_DZ and lz) for lz in ctx.lazy]
+        offs = [sum(ctx.widths[:i]) for i in range(nseg)]
+        dzs = [_lazy_dz(z.shape, dev, ("gate", dout, offs[i], g, dmean, ctx.thw)) if lazy_dz[i]
+               else torch.empty(z.shape, dtype=BF16, device=dev) for i, z in enumerate(zs)]
+        call("milnce_gate_bwd_apply", nseg, widths,
+             _arr(ctypes.c_void_p, [0 if lz else ptr(d) for lz, d in zip(lazy_dz, dzs)]), ptr(dout),
              ptr(g), ptr(dmean), B, ctx.thw,
              _arr(ctypes.c_void_p, [ptr(zb[0]) for zb in ctx.z_bn]) if have_bn else None,
              _arr(ctypes.c_void_p, [ptr(zb[1]) for zb in ctx.z_bn]) if have_bn else None,
@@ -842,7 +946,8 @@ class _GateConcat(torch.autograd.Function):
 
 
 def gate_concat(branches, fc_weights, fc_biases, gsums=None):
-    branches = [b.contiguous() if b.dtype == BF16 else b.to(BF16).contiguous() for b in branches]
+    branches = [b if _is_lazy(b) else (b.contiguous() if b.dtype == BF16 else b.to(BF16).contiguous())
+                for b in branches]
     if gsums is None or any(s is None for s in gsums):
         gsums = [b.float().sum(dim=(1, 2, 3)) for b in branches]
     gsum = gsums[0] if len(gsums) == 1 else torch.cat(gsums, dim=1)
@@ -918,6 +1023,75 @@ class _MaxPool(torch.autograd.Function):
         return dx, None, None, None
 
 
+_FUSE_GATE_POOL = os.environ.get("MILNCE_FUSE_GATE_POOL", "1") != "0"
+
+
+class _GatedPool(torch.autograd.Function):
+    """SelfGating of a lazy BN-ReLU output followed by its TF-SAME max pool (conv_2c -> gating ->
+    maxpool_3a, ``s3dg.py:290-296``) without the full-resolution gate output: the pool applies
+    BN + ReLU + gate inside its loads. Backward: the gate reduction is taken on the pooled tensor
+    (sum_thw dx * x = sum dy * pooled, every routed gradient lands on its arg-max cell), so the fc
+    backward runs first and the pool backward then yields the BN layer's dz = bf16(dx * g + dmean /
+    thw) directly (with its BN partial sums; lazily, see ``_LAZY_POOL_DZ``)."""
+
+    @staticmethod
+    def forward(ctx, z, gsum, w, bias, kernel, stride):
+        y, ss, ld = z._milnce_bn
+        B, T, H, W, C = z.shape
+        dev = y.device
+        mean = torch.empty((B, C), dtype=F32, device=dev)
+        g = torch.empty((B, C), dtype=F32, device=dev)
+        call("milnce_gate_fwd", 1, _arr(ctypes.c_int, [C]), _arr(ctypes.c_void_p, [0]), _arr(ctypes.c_void_p, [ptr(w)]),
+             _arr(ctypes.c_void_p, [ptr(bias)]), ptr(gsum), B, T * H * W, ptr(mean), ptr(g), None, None, None, None,
+             None, stream())
+        pads = aten.tf_same_pad(kernel, stride)
+        To = _pool_out(T, kernel[0], stride[0], *pads[0])
+        Ho = _pool_out(H, kernel[1], stride[1], *pads[1])
+        Wo = _pool_out(W, kernel[2], stride[2], *pads[2])
+        out = torch.empty((B, To, Ho, Wo, C), dtype=BF16, device=dev)
+        arg = torch.empty((B, To, Ho, Wo, C), dtype=torch.uint8, device=dev)
+        geo = [B, T, H, W, C, To, Ho, Wo, *kernel, *stride, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
+               pads[2][0], pads[2][1], 1]
+        call("milnce_bn_relu_gate_maxpool_fwd", ptr(y), ptr(ss), ptr(g), ptr(out), ptr(arg), *geo, stream())
+        ctx.save_for_backward(y, ss, g, mean, w, out, arg)
+        ctx.geo, ctx.ld = geo, ld
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, ss, g, mean, w, out, arg = ctx.saved_tensors
+        geo = ctx.geo
+        B, T, H, W, C, To, Ho, Wo = geo[:8]
+        dout = dout.contiguous()
+        gs = torch.zeros((B, C), dtype=F32, device=dout.device)
+        call("milnce_gate_dot", ptr(dout), ptr(out), B, To * Ho * Wo, C, ptr(gs), stream())
+        dpre = gs * (1.0 - g)
+        dw = dpre.t().mm(mean)
+        db = dpre.sum(0)
+        dmean = dpre.mm(w).contiguous()
+        nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
+        lazy = _LAZY_POOL_DZ and _FUSE_BN_BWD
+        dz = None if lazy else torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
+        call("milnce_maxpool_bwd_gated", ptr(dout), ptr(arg), ptr(dz), *geo, ptr(y), ctx.ld, ptr(ss), ptr(part),
+             nparts, ptr(g), ptr(dmean), stream())
+        if lazy:
+            dz = _lazy_dz((B, T, H, W, C), dout.device, ("pool", dout, arg, geo, g, dmean, nparts))
+        attach_bn_partials(dz, part, nparts, C)
+        return dz, None, dw, db, None, None
+
+
+def gated_maxpool(z, gsum, fc_weight, fc_bias, kernel, stride):
+    """SelfGating(z) followed by a TF-SAME max pool; fused (``_GatedPool``) when z is a lazy
+    BN-ReLU output with its gating sum."""
+    C = z.shape[-1]
+    if (_FUSE_GATE_POOL and _is_lazy(z) and gsum is not None and (tuple(kernel), tuple(stride)) in _POOL_SPECIAL
+            and C % 8 == 0 and C // 8 <= 256 and z._milnce_bn[2] == C):
+        return _GatedPool.apply(z, gsum.contiguous(), fc_weight, fc_bias, tuple(kernel), tuple(stride))
+    x = gate_concat([z], [fc_weight], [fc_bias], None if gsum is None else [gsum])
+    return maxpool3d(x, kernel, stride, True)
+
+
 def maxpool3d(x, kernel, stride, tf_same: bool):
     return _MaxPool.apply(x.contiguous(), tuple(kernel), tuple(stride), bool(tf_same))
 
@@ -929,13 +1103,24 @@ class _AvgPool(torch.autograd.Function):
         out = torch.zeros((B, C), dtype=F32, device=x.device)
         call("milnce_avgpool", ptr(x), B, T * H * W, C, ptr(out), stream())
         ctx.shape = (B, T, H, W, C)
+        ctx.x_gate = bool(getattr(x, "_milnce_gate", False))
+        if ctx.x_gate:
+            ctx.save_for_backward(out)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         B, T, H, W, C = ctx.shape
+        thw = T * H * W
+        dout = dout.contiguous().float()
         dx = torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
-        call("milnce_avgpool_bwd", ptr(dout.contiguous().float()), B, T * H * W, C, ptr(dx), stream())
+        call("milnce_avgpool_bwd", ptr(dout), B, thw, C, ptr(dx), stream())
+        if ctx.x_gate:
+            # the SelfGating reduction of x's producer comes for free: dx is the broadcast
+            # bf16(dout / thw), so sum_thw dx * x = bf16(dout / thw) * thw * mean(x)
+            (mean,) = ctx.saved_tensors
+            dx._milnce_gs = (dout / thw).to(BF16).float() * (mean * thw)
+            dx._milnce_gsver = dx._version
         return dx
 
 
