@@ -171,7 +171,7 @@ struct PoolDivs {
 // BN: x is the raw conv output of a train-mode BN layer and z = relu(x * scale + shift) is
 // pooled without being materialised (ss = [mean, invstd, scale, shift] per channel); padded
 // cells stay zero candidates, as for the z the unfused pool would read.
-template <int KT, int KH, int KW, int ST, int SH, int SW, bool BN = false>
+template <int KT, int KH, int KW, int ST, int SH, int SW, bool BN = false, bool GATE = false>
 __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ x,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                      uint32_t nout_chunks, const float* __restrict__ ss = nullptr,
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
       if constexpr (BN) {
         sc[k] = ss[2 * p.C + c0 + k];
         sh[k] = ss[3 * p.C + c0 + k];
-        gv[k] = gate != nullptr ? gate[(size_t)b * p.C + c0 + k] : 1.f;
+        if constexpr (GATE) gv[k] = gate[(size_t)b * p.C + c0 + k];
       }
     }
 #pragma unroll
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
       if constexpr (BN) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f)));  // = the stored z
-        if (gate != nullptr) {  // SelfGating output z * gate[b, c], as gate_scale would store it
+        if constexpr (GATE) {  // SelfGating output z * gate[b, c], as gate_scale would store it
 #pragma unroll
           for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(f[k] * gv[k]));
         }
@@ -925,8 +925,12 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
     const int grid = (int)(g > 65536 ? 65536 : g);
 #define X(a, b, c, e, f, h)                                                                                      \
     if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                            \
-      hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true>), dim3(grid), dim3(256), 0, s, p, d,             \
-                         (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);                       \
+      if (gate != nullptr)                                                                                       \
+        hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, true>), dim3(grid), dim3(256), 0, s, p, d,     \
+                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);               \
+      else                                                                                                       \
+        hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, false>), dim3(grid), dim3(256), 0, s, p, d,    \
+                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, nullptr);            \
       return true;                                                                                               \
     }
     MILNCE_POOL_SHAPES(X)

@@ -67,6 +67,7 @@ class ConvPlan:
     impl: int = 0         # forward kernel variant (csrc/conv.hip launch_v3_impl); 0 = not tuned yet
     d_impl: int = 0       # dgrad kernel variant
     w_impl: int = 0       # wgrad kernel variant (2: register-staged, 3/4: LDS-DMA ring, 3/2 stages)
+    w_occ: int = 4        # wgrad split-K target: workgroups per CU (fewer splits = smaller slab to reduce)
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -344,12 +345,13 @@ def _is_paired_stem(plan: ConvPlan) -> bool:
             plan.s == (2, 2, 1) and plan.p == (1, 3, 2) and plan.Wo == plan.W)
 
 
-def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int) -> Tuple[int, int, int]:
-    """(Npad, Kpad, splits) of a wgrad tiling: split-K over m until >= 4 blocks per CU."""
+def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int, occ: int = 4) -> Tuple[int, int, int]:
+    """(Npad, Kpad, splits) of a wgrad tiling: split-K over m until >= occ blocks per CU. More
+    splits fill the chip better but every split writes (and the reduce reads) a full fp32 slab."""
     npad = _ceil(Cout, tn) * tn
     kpad = _ceil(Ktot, tk) * tk
     tiles = (npad // tn) * (kpad // tk)
-    splits = max(1, min(_ceil(4 * _NUM_CU, tiles), _ceil(M, 32 * 8)))
+    splits = max(1, min(_ceil(occ * _NUM_CU, tiles), _ceil(M, 32 * 8)))
     return npad, kpad, splits
 
 
@@ -363,6 +365,7 @@ def _wgrad_tiles(Cout: int) -> List[int]:
 
 
 _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
+_W_OCCS = (4, 2)  # split-K occupancy candidates (workgroups per CU)
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -381,8 +384,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         if rc == 0:
             return dw
 
-    def launch_with(tn, impl, target, accumulate):
-        npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk)
+    def launch_with(tn, impl, target, accumulate, occ):
+        npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
         slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
         call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
              plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
@@ -396,16 +399,17 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             cands = []
             for tn in _wgrad_tiles(plan.Cout):
                 for impl in _WIDE_W_IMPLS.get(tn, _W_IMPLS):
-                    cands.append((tn, impl))
+                    for occ in _W_OCCS:
+                        cands.append((tn, impl, occ))
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
-            default = (plan.w_tn, _DEFAULT_IMPL)
+            default = (plan.w_tn, _DEFAULT_IMPL, 4)
             best = _tune(lambda c: launch_with(*inv[c], scratch, 0), tuple(code.values()),
                          default=code.get(default))
-            tn, impl = inv[best]
-            plan.w_tn, plan.w_impl = tn, impl
-            plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk)
-    launch_with(plan.w_tn, plan.w_impl, dw, acc)
+            tn, impl, occ = inv[best]
+            plan.w_tn, plan.w_impl, plan.w_occ = tn, impl, occ
+            plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
+    launch_with(plan.w_tn, plan.w_impl, dw, acc, plan.w_occ)
     return dw
 
 
