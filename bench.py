@@ -99,7 +99,7 @@ def main():
     final_loss = float(losses[-1].item()) if losses else float("nan")
     if opts.profile_steps and cuda:
         from torch.profiler import ProfilerActivity, profile
-        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
             for _ in range(opts.profile_steps):
                 trainer.train_step(data.batch(step))
                 step += 1
@@ -108,6 +108,14 @@ def main():
             os.makedirs("gpurun_out", exist_ok=True)
             with open("gpurun_out/torch_profile.txt", "w") as f:
                 f.write(prof.key_averages().table(sort_by="cuda_time_total", row_limit=80))
+            # where the small ATen ops (adds, fills, reductions) come from
+            with open("gpurun_out/torch_profile_stacks.txt", "w") as f:
+                for e in prof.key_averages(group_by_stack_n=8):
+                    if e.key.startswith(("aten::add", "aten::fill", "aten::zero", "aten::sum", "aten::copy",
+                                         "aten::mul", "aten::mm", "aten::addmm", "aten::sub", "aten::div")):
+                        f.write(f"{e.key} count={e.count} cuda_us={e.device_time_total:.0f}\n")
+                        for fr in e.stack:
+                            f.write(f"    {fr}\n")
     ms = 1000.0 * dt / max(1, opts.steps)
     pairs = b * ctx.world_size * opts.steps / dt
     if ctx.is_main:

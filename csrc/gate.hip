@@ -6,7 +6,7 @@
 //           per clip and branch), gate_scale writes z_i * g_i straight into its channel slice of
 //           the concatenated block output (no separate th.cat pass).
 // backward: gate_bwd_reduce  dpre[b, c] = (sum_thw dout * z) * g * (1 - g)   (all branches)
-//           [hipBLASLt]      dmean = dpre W; dW = dpre^T mean; db = sum_b dpre (tiny GEMMs)
+//           gate_fc_bwd      dmean = dpre W; dW += dpre^T mean; db += sum_b dpre (all branches)
 //           gate_bwd_apply   dz_i = dout_i * g_i + dmean_i / THW              (all branches)
 #include "common.h"
 
@@ -284,6 +284,113 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dout, int C, int th
   }
 }
 
+
+// SelfGating fc backward of every branch in one launch (replaces 3 hipBLASLt GEMMs, a reduction,
+// a copy and two AccumulateGrad adds per branch). dpre[b, c] = src[b, c] * (g ? 1 - g[b, c] : 1)
+// (src = g * sum_thw dout * z when g is given, else the finished dpre). Blocks [0, wend) compute
+// dW[co, ci] = sum_b dpre[b, co] * mean[b, ci] and db[co] = sum_b dpre[b, co] on 16 co x 64 ci
+// tiles (the tile's dpre columns staged in LDS); blocks [wend, ...) compute dmean[b, ci] =
+// sum_co dpre[b, co] * W[co, ci] on 16 b x 64 ci tiles (the 16 dpre rows staged in LDS). Each
+// wave owns 4 rows of its tile, so the LDS reads are wave-uniform broadcasts. Bit s of acc_mask:
+// accumulate into dw[s] / db[s] (a flat data-parallel gradient buffer) instead of storing.
+struct FcTiles {
+  int wstart[MAXSEG + 1];
+  int mstart[MAXSEG + 1];
+};
+
+__global__ __launch_bounds__(256) void gate_fc_bwd_kernel(SegTable t, FcTiles ft, const float* __restrict__ src,
+                                                          const float* __restrict__ g,
+                                                          const float* __restrict__ mean, int B, int Ctot,
+                                                          int acc_mask, float* __restrict__ dmean) {
+  extern __shared__ float sd[];
+  int tile = blockIdx.x;
+  const bool wpart = tile < ft.wstart[t.nseg];
+  int s = 0;
+  if (wpart) {
+    while (tile >= ft.wstart[s + 1]) ++s;
+    tile -= ft.wstart[s];
+  } else {
+    tile -= ft.wstart[t.nseg];
+    while (tile >= ft.mstart[s + 1]) ++s;
+    tile -= ft.mstart[s];
+  }
+  const int c0 = t.off[s], C = t.off[s + 1] - c0;
+  const int nci = (C + 63) / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int ci = (tile % nci) * 64 + lane;
+  const bool cv = ci < C;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (wpart) {
+    const int co0 = (tile / nci) * 16;
+    for (int i = threadIdx.x; i < B * 16; i += 256) {
+      const int b = i >> 4, co = co0 + (i & 15);
+      float v = 0.f;
+      if (co < C) {
+        const long long k = (long long)b * Ctot + c0 + co;
+        v = src[k];
+        if (g != nullptr) v *= 1.f - g[k];
+      }
+      sd[i] = v;
+    }
+    __syncthreads();
+    float dbs[4] = {0.f, 0.f, 0.f, 0.f};
+    const float* mp = mean + c0 + (cv ? ci : 0);
+    for (int b = 0; b < B; ++b) {
+      const float m = mp[(long long)b * Ctot];
+      const float4 d = *(const float4*)&sd[b * 16 + wv * 4];
+      acc[0] += d.x * m;
+      acc[1] += d.y * m;
+      acc[2] += d.z * m;
+      acc[3] += d.w * m;
+      dbs[0] += d.x;
+      dbs[1] += d.y;
+      dbs[2] += d.z;
+      dbs[3] += d.w;
+    }
+    const bool accum = (acc_mask >> s) & 1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = co0 + wv * 4 + j;
+      if (co >= C) continue;
+      if (cv) {
+        float* p = t.dw[s] + (long long)co * C + ci;
+        *p = accum ? *p + acc[j] : acc[j];
+      }
+      if (tile % nci == 0 && lane == 0) {
+        float* p = t.db[s] + co;
+        *p = accum ? *p + dbs[j] : dbs[j];
+      }
+    }
+  } else {
+    const int b0 = (tile / nci) * 16;
+    for (int i = threadIdx.x; i < 16 * C; i += 256) {
+      const int j = i / C, co = i - j * C, b = b0 + j;
+      float v = 0.f;
+      if (b < B) {
+        const long long k = (long long)b * Ctot + c0 + co;
+        v = src[k];
+        if (g != nullptr) v *= 1.f - g[k];
+      }
+      sd[i] = v;
+    }
+    __syncthreads();
+    const float* wp = t.w[s] + (cv ? ci : 0);
+    const float* r = sd + wv * 4 * C;
+    for (int co = 0; co < C; ++co) {
+      const float w = wp[(long long)co * C];
+      acc[0] += r[co] * w;
+      acc[1] += r[C + co] * w;
+      acc[2] += r[2 * C + co] * w;
+      acc[3] += r[3 * C + co] * w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = b0 + wv * 4 + j;
+      if (b < B && cv) dmean[(long long)b * Ctot + c0 + ci] = acc[j];
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 static SegTable make_table(int nseg, const int* widths, const void* const* z, void* const* dz,
                            const float* const* w, const float* const* bias, float* const* dw, float* const* db) {
@@ -343,7 +450,7 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
 }
 
 // Phase 1: dpre[B, Ctot] = (sum_thw dout * z) * g * (1 - g)   (dpre zeroed by the caller).
-// The tiny per-branch GEMMs (dW = dpre^T mean, dmean = dpre W) run on hipBLASLt in between.
+// The per-branch fc backward (milnce_gate_fc_bwd) runs in between.
 MILNCE_API int milnce_gate_bwd_reduce(int nseg, const int* widths, const void* const* z, const void* dout,
                                       const float* g, int B, int thw, float* dpre, hipStream_t stream) {
   SegTable t = make_table(nseg, widths, z, nullptr, nullptr, nullptr, nullptr, nullptr);
@@ -354,6 +461,32 @@ MILNCE_API int milnce_gate_bwd_reduce(int nseg, const int* widths, const void* c
                      thw, rpb, dpre);
   const long long n = (long long)B * Ctot;
   hipLaunchKernelGGL(gate_dpre_kernel, dim3(grid_for(n)), dim3(256), 0, stream, dpre, g, n);
+  return (int)hipGetLastError();
+}
+
+// The SelfGating fc backward of all nseg branches (gate_fc_bwd_kernel): dw[i], db[i] (accumulated
+// where bit i of acc_mask is set) and dmean [B, Ctot]. Returns hipErrorInvalidValue for shapes
+// whose LDS staging would not fit (the caller then falls back to library GEMMs).
+MILNCE_API int milnce_gate_fc_bwd(int nseg, const int* widths, const float* src, const float* g, const float* mean,
+                                  const float* const* w, float* const* dw, float* const* db, int acc_mask, int B,
+                                  float* dmean, hipStream_t stream) {
+  SegTable t = make_table(nseg, widths, nullptr, nullptr, w, nullptr, dw, db);
+  const int Ctot = t.off[nseg];
+  FcTiles ft;
+  ft.wstart[0] = ft.mstart[0] = 0;
+  int cmax = 0;
+  for (int i = 0; i < MAXSEG; ++i) {
+    const int C = i < nseg ? widths[i] : 0;
+    cmax = C > cmax ? C : cmax;
+    const int nci = (C + 63) / 64;
+    ft.wstart[i + 1] = ft.wstart[i] + nci * ((C + 15) / 16);
+    ft.mstart[i + 1] = ft.mstart[i] + nci * ((B + 15) / 16);
+  }
+  const size_t lds = sizeof(float) * 16 * (size_t)(B > cmax ? B : cmax);
+  if (nseg < 1 || nseg > MAXSEG || B < 1 || lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  const int grid = ft.wstart[nseg] + ft.mstart[nseg];
+  hipLaunchKernelGGL(gate_fc_bwd_kernel, dim3(grid), dim3(256), lds, stream, t, ft, src, g, mean, B, Ctot, acc_mask,
+                     dmean);
   return (int)hipGetLastError();
 }
 

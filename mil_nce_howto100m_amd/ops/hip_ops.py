@@ -384,7 +384,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         if rc == 0:
             return dw
 
-    def launch_with(tn, impl, target, accumulate, occ):
+    def launch_with(tn, impl, occ, target, accumulate):
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
         slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
         call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
@@ -409,7 +409,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             tn, impl, occ = inv[best]
             plan.w_tn, plan.w_impl, plan.w_occ = tn, impl, occ
             plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
-    launch_with(plan.w_tn, plan.w_impl, dw, acc, plan.w_occ)
+    launch_with(plan.w_tn, plan.w_impl, plan.w_occ, dw, acc)
     return dw
 
 
@@ -867,6 +867,38 @@ def _arr(ctype, vals):
     return (ctype * len(vals))(*vals)
 
 
+def gate_fc_backward(src, g, mean, ws, bs, widths):
+    """SelfGating fc backward of every branch in one kernel (csrc/gate.hip gate_fc_bwd_kernel):
+    dpre = src * (1 - g) (src itself when g is None), dmean = dpre W, dW = dpre^T mean, db = sum_b
+    dpre per branch. Weight / bias gradients that live in the data-parallel flat buffer are
+    accumulated there in place (returned as None), the others are returned as fresh tensors."""
+    B, ctot = mean.shape
+    if ctot != sum(widths):
+        raise ValueError("gate_fc_backward: mean / src rows must be the concat of the branches")
+    dev = mean.device
+    dmean = torch.empty((B, ctot), dtype=F32, device=dev)
+    dws, dbs, acc_mask, done = [], [], 0, []
+    for i, (w, b, c) in enumerate(zip(ws, bs, widths)):
+        wd, bd = _direct_grad(w), _direct_grad(b)
+        if wd is not None and bd is not None:
+            dws.append(wd)
+            dbs.append(bd)
+            acc_mask |= 1 << i
+            done.append(i)
+        else:
+            dws.append(torch.empty((c, c), dtype=F32, device=dev))
+            dbs.append(torch.empty((c,), dtype=F32, device=dev))
+    call("milnce_gate_fc_bwd", len(widths), _arr(ctypes.c_int, widths), ptr(src.contiguous()),
+         ptr(None if g is None else g.contiguous()), ptr(mean.contiguous()),
+         _arr(ctypes.c_void_p, [ptr(w) for w in ws]), _arr(ctypes.c_void_p, [ptr(d) for d in dws]),
+         _arr(ctypes.c_void_p, [ptr(d) for d in dbs]), acc_mask, B, ptr(dmean), stream())
+    for i in done:
+        _grad_done(ws[i])
+        _grad_done(bs[i])
+        dws[i] = dbs[i] = None
+    return dmean, dws, dbs
+
+
 class _GateConcat(torch.autograd.Function):
     @staticmethod
     def forward(ctx, nseg, gsum, *args):
@@ -890,6 +922,7 @@ class _GateConcat(torch.autograd.Function):
              _arr(ctypes.c_int, [int(i[2]) for i in bn_info]), stream())
         ctx.save_for_backward(*zs, *ws, g, mean)
         ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
+        ctx.bs = bs  # parameter handles only (their gradient buffers may be written in place)
         ctx.z_bn = [getattr(z, "_milnce_bn", None) for z in zs]
         ctx.lazy = lazy
         out._milnce_gate = True  # consumers may return sum_thw dout * out with the gradient
@@ -908,24 +941,16 @@ class _GateConcat(torch.autograd.Function):
         dev = dout.device
         widths = _arr(ctypes.c_int, ctx.widths)
         gs = take_gate_sums(dout)
-        if gs is not None:
-            # gs = sum dout * bf16(z * g) = g * sum dout * z  ->  dpre = gs * (1 - g)
-            dpre = gs * (1.0 - g)
-        else:
+        # gs = sum dout * bf16(z * g) = g * sum dout * z, so dpre = gs * (1 - g) (in gate_fc_backward)
+        if gs is None:
             dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
             zr = [_materialize(z) if _is_lazy(z) else z for z in zs]
             call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zr]), ptr(dout),
                  ptr(g), B, ctx.thw, ptr(dpre), stream())
-        # per-branch fc backward: plain GEMMs on hipBLASLt
-        dmean = torch.empty((B, ctot), dtype=F32, device=dev)
-        dws, dbs = [], []
-        off = 0
-        for w, c in zip(ws, ctx.widths):
-            dp = dpre[:, off:off + c]
-            dws.append(dp.t().mm(mean[:, off:off + c]))
-            dbs.append(dp.sum(0))
-            dmean[:, off:off + c].copy_(dp.mm(w))
-            off += c
+        if gs is not None:
+            dmean, dws, dbs = gate_fc_backward(gs, g, mean, ws, ctx.bs, ctx.widths)
+        else:
+            dmean, dws, dbs = gate_fc_backward(dpre, None, mean, ws, ctx.bs, ctx.widths)
         have_bn = all(zb is not None for zb in ctx.z_bn)
         nparts = B * int(max(1, min(_ceil(2048, B), _ceil(ctx.thw, 128))))
         part = torch.empty((nparts * 2 * ctot,), dtype=F32, device=dev) if have_bn else None
@@ -1059,6 +1084,7 @@ class _GatedPool(torch.autograd.Function):
         call("milnce_bn_relu_gate_maxpool_fwd", ptr(y), ptr(ss), ptr(g), ptr(out), ptr(arg), *geo, stream())
         ctx.save_for_backward(y, ss, g, mean, w, out, arg)
         ctx.geo, ctx.ld = geo, ld
+        ctx.bias = bias
         return out
 
     @staticmethod
@@ -1069,10 +1095,7 @@ class _GatedPool(torch.autograd.Function):
         dout = dout.contiguous()
         gs = torch.zeros((B, C), dtype=F32, device=dout.device)
         call("milnce_gate_dot", ptr(dout), ptr(out), B, To * Ho * Wo, C, ptr(gs), stream())
-        dpre = gs * (1.0 - g)
-        dw = dpre.t().mm(mean)
-        db = dpre.sum(0)
-        dmean = dpre.mm(w).contiguous()
+        dmean, (dw,), (db,) = gate_fc_backward(gs, g, mean, [w], [ctx.bias], [C])
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
         part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
         lazy = _LAZY_POOL_DZ and _FUSE_BN_BWD

@@ -766,3 +766,47 @@ def test_lazy_pool_dz_matches_stored():
     stored = _gated_pool_grads(h, "_LAZY_POOL_DZ", False)
     for a, b in zip(lazy, stored):
         assert rel_err(a, b) < 1e-5
+
+def test_gate_fc_backward_kernel():
+    """One-launch SelfGating fc backward (csrc/gate.hip gate_fc_bwd_kernel) vs fp32 PyTorch GEMMs,
+    both the stored and the in-place accumulated (flat-buffer) gradient paths."""
+    torch.manual_seed(11)
+    h = hip()
+    widths = [384, 128, 40, 96]
+    B = 256
+    ctot = sum(widths)
+    src = torch.randn(B, ctot, device=DEV)
+    g = torch.rand(B, ctot, device=DEV)
+    mean = torch.randn(B, ctot, device=DEV)
+    ws = [torch.randn(c, c, device=DEV, requires_grad=True) for c in widths]
+    bs = [torch.randn(c, device=DEV, requires_grad=True) for c in widths]
+    # branches 1 and 3 accumulate into existing flat-buffer style grads
+    for i in (1, 3):
+        for p in (ws[i], bs[i]):
+            p.grad = torch.randn_like(p)
+            p._milnce_flat_grad = True
+    prev = {i: (ws[i].grad.clone(), bs[i].grad.clone()) for i in (1, 3)}
+    dmean, dws, dbs = h.gate_fc_backward(src, g, mean, ws, bs, widths)
+    torch.cuda.synchronize()
+    dpre = src * (1 - g)
+    off = 0
+    for i, c in enumerate(widths):
+        dp = dpre[:, off:off + c]
+        rw = dp.t().mm(mean[:, off:off + c])
+        rb = dp.sum(0)
+        assert rel_err(dmean[:, off:off + c], dp.mm(ws[i].detach())) < 1e-5
+        if i in prev:
+            assert dws[i] is None and dbs[i] is None
+            assert rel_err(ws[i].grad, prev[i][0] + rw) < 1e-5
+            assert rel_err(bs[i].grad, prev[i][1] + rb) < 1e-5
+        else:
+            assert rel_err(dws[i], rw) < 1e-5
+            assert rel_err(dbs[i], rb) < 1e-5
+        off += c
+    # g = None: src is the finished dpre
+    c0 = widths[0]
+    dmean2, dws2, dbs2 = h.gate_fc_backward(dpre[:, :c0].contiguous(), None, mean[:, :c0].contiguous(), ws[:1],
+                                            bs[:1], widths[:1])
+    assert rel_err(dmean2, dpre[:, :c0].mm(ws[0].detach())) < 1e-5
+    assert rel_err(dws2[0], dpre[:, :c0].t().mm(mean[:, :c0])) < 1e-5
+    assert rel_err(dbs2[0], dpre[:, :c0].sum(0)) < 1e-5
