@@ -249,19 +249,25 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
 // part[blockIdx][2][C] (mask = y*scale + shift > 0, xhat = (y - mean) * invstd).
 struct BnAcc {
   float a1[8], a2[8];
+  float mu[8], is[8], sc[8], sh[8];  // the thread's channels' [mean, invstd, scale, shift], loaded once
   __device__ __forceinline__ void zero() {
 #pragma unroll
     for (int k = 0; k < 8; ++k) { a1[k] = 0.f; a2[k] = 0.f; }
   }
-  __device__ __forceinline__ void add(const float* d, const bf16_t* ypos, const float* ss, int C, int c0) {
+  __device__ __forceinline__ void load(const float* ss, int C, int c0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mu[k] = ss[c0 + k]; is[k] = ss[C + c0 + k]; sc[k] = ss[2 * C + c0 + k]; sh[k] = ss[3 * C + c0 + k];
+    }
+  }
+  __device__ __forceinline__ void add(const float* d, const bf16_t* ypos) {
     float yv[8];
     unpack8(*(const uint4*)ypos, yv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      const float gm = (yv[k] * ss[2 * C + c] + ss[3 * C + c] > 0.f) ? d[k] : 0.f;
+      const float gm = (yv[k] * sc[k] + sh[k] > 0.f) ? d[k] : 0.f;
       a1[k] += gm;
-      a2[k] += gm * (yv[k] - ss[c]) * ss[C + c];
+      a2[k] += gm * (yv[k] - mu[k]) * is[k];
     }
   }
   __device__ __forceinline__ void commit(float* red, float* part, int C, int cpr, int rpi, int cc, int rr,
@@ -329,6 +335,50 @@ __device__ __forceinline__ void pool_bwd_one(const PoolParams& p, const PoolDivs
   }
 }
 
+// Quad gather for the 1x3x3 stride-(1,2,2) window with no leading padding and H = 2 Ho, W = 2 Wo
+// (maxpool_2a / maxpool_3a): the 2x2 input quad (2 h2 + eh, 2 w2 + ew) is covered by the outputs
+// (h2 - jh, w2 - jw), jh, jw in {0, 1}, at window offsets (eh + 2 jh, ew + 2 jw) (< 3 to count).
+// One thread loads those 4 output cells once for 4 inputs instead of 4 cells per input.
+__device__ __forceinline__ void pool_bwd_quad(const PoolParams& p, const bf16_t* __restrict__ dy,
+                                              const uint8_t* __restrict__ arg, uint32_t bt, int h2, int w2,
+                                              int c0, float (*acc)[8]) {
+  uint4 g[4];
+  uint2 a[4];
+  bool ok[4];
+#pragma unroll
+  for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+    for (int jw = 0; jw < 2; ++jw) {
+      const int u = jh * 2 + jw, ho = h2 - jh, wo = w2 - jw;
+      ok[u] = (ho >= 0) & (wo >= 0);
+      const size_t o = ((size_t)(bt * p.Ho + (ok[u] ? ho : 0)) * p.Wo + (ok[u] ? wo : 0)) * p.C + c0;
+      g[u] = *(const uint4*)(dy + o);
+      a[u] = *(const uint2*)(arg + o);
+    }
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[e][k] = 0.f;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int jh = u >> 1, jw = u & 1;
+    float gf[8];
+    unpack8(g[u], gf);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int eh = e >> 1, ew = e & 1;
+      const int dh = eh + 2 * jh, dw = ew + 2 * jw;
+      if (dh >= 3 || dw >= 3) continue;  // compile-time after unrolling
+      const uint32_t tap = (uint32_t)(dh * 3 + dw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t ak = ((k < 4 ? a[u].x : a[u].y) >> (8 * (k & 3))) & 0xff;
+        acc[e][k] += (ok[u] & (ak == tap)) ? gf[k] : 0.f;
+      }
+    }
+  }
+}
+
 // Thread = fixed 8-channel chunk cc = tid % cpr of rpi = 256/cpr input positions per step; block
 // blockIdx.x walks positions [pos_begin, pos_end), two positions per thread per iteration so
 // both gathers' loads are in flight together. MODE (compile time, so every variant keeps only
@@ -340,7 +390,7 @@ __device__ __forceinline__ void pool_bwd_one(const PoolParams& p, const PoolDivs
 //                   finalised coefficients coef: the producer conv's output gradient
 enum { POOL_BWD_PLAIN = 0, POOL_BWD_GATED = 1, POOL_BWD_APPLY = 2 };
 
-template <int KT, int KH, int KW, int ST, int SH, int SW, int MODE = POOL_BWD_PLAIN>
+template <int KT, int KH, int KW, int ST, int SH, int SW, int MODE = POOL_BWD_PLAIN, bool QUAD = false>
 __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ dy,
                                                      const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                      uint32_t npos, uint32_t pos_per_block,
@@ -360,6 +410,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
   const bool gated = MODE == POOL_BWD_GATED || (MODE == POOL_BWD_APPLY && gate_g != nullptr);
   BnAcc acc_bn;
   acc_bn.zero();
+  if (bn && active) acc_bn.load(bn_ss, p.C, c0);
   const uint32_t pos_begin = blockIdx.x * pos_per_block;
   const uint32_t pos_end = min(npos, pos_begin + pos_per_block);
   // gate reduction of the pool input's producer (SelfGating): gs[b, c] += sum dx * gx, flushed
@@ -424,7 +475,35 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     }
     v = pack8(o);
   };
-  for (uint32_t pos = pos_begin + rr; active && pos < pos_end; pos += 2 * rpi) {
+  // one input position's epilogue (the quad path; the pair loop below interleaves two of them)
+  auto finish = [&](uint32_t ps, const float* a) {
+    uint4 v = pack8(a);
+    if (gated) gate_apply(ps, v);
+    if (MODE == POOL_BWD_PLAIN && gs != nullptr) gs_add(ps, v, *(const uint4*)(gx + (size_t)ps * p.C + c0));
+    if (bn) {
+      float dr[8];
+      unpack8(v, dr);
+      acc_bn.add(dr, bn_y + (size_t)ps * bn_ld + c0);
+    }
+    if constexpr (MODE == POOL_BWD_APPLY) bn_apply(ps, v);
+    if (dx != nullptr) *(uint4*)(dx + (size_t)ps * p.C + c0) = v;
+  };
+  if constexpr (QUAD) {  // pos indexes 2x2 input quads (b, t, h2, w2)
+    for (uint32_t q = pos_begin + rr; active && q < pos_end; q += rpi) {
+      const uint32_t r = fdiv(q, d.fWo);
+      const int w2 = (int)(q - r * p.Wo);
+      const uint32_t bt = fdiv(r, d.fHo);
+      const int h2 = (int)(r - bt * p.Ho);
+      float a[4][8];
+      pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
+      const uint32_t p00 = (bt * p.H + 2 * h2) * p.W + 2 * w2;
+      finish(p00, a[0]);
+      finish(p00 + 1, a[1]);
+      finish(p00 + p.W, a[2]);
+      finish(p00 + p.W + 1, a[3]);
+    }
+  }
+  for (uint32_t pos = pos_begin + rr; !QUAD && active && pos < pos_end; pos += 2 * rpi) {
     const uint32_t pos2 = pos + rpi;
     const bool two = pos2 < pos_end;
     float a0[8], a1[8];
@@ -448,10 +527,10 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     if (bn) {
       float dr[8];
       unpack8(v0, dr);
-      acc_bn.add(dr, bn_y + (size_t)pos * bn_ld + c0, bn_ss, p.C, c0);
+      acc_bn.add(dr, bn_y + (size_t)pos * bn_ld + c0);
       if (two) {
         unpack8(v1, dr);
-        acc_bn.add(dr, bn_y + (size_t)pos2 * bn_ld + c0, bn_ss, p.C, c0);
+        acc_bn.add(dr, bn_y + (size_t)pos2 * bn_ld + c0);
       }
     }
     if constexpr (MODE == POOL_BWD_APPLY) {
@@ -965,6 +1044,13 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
   return false;
 }
 
+// milnce_pool_set_quad(0) turns the quad gather off (A/B runs and the equality test)
+static bool g_pool_quad = true;
+MILNCE_API int milnce_pool_set_quad(int on) {
+  g_pool_quad = on != 0;
+  return 0;
+}
+
 static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* arg, void* dx, long long n,
                              const void* bn_y, int bn_ld, const float* bn_ss, float* part, int nparts,
                              hipStream_t s, const void* gx = nullptr, float* gs = nullptr,
@@ -991,6 +1077,19 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   const uint32_t npos = (uint32_t)(n / (p.C / 8));
   const uint32_t ppb = (npos + nparts - 1) / nparts;
   const int mode = coef != nullptr ? POOL_BWD_APPLY : (gate_g != nullptr ? POOL_BWD_GATED : POOL_BWD_PLAIN);
+  if (p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 && p.ph == 0 &&
+      p.pw == 0 && p.To == p.T && p.H == 2 * p.Ho && p.W == 2 * p.Wo && g_pool_quad) {
+    const uint32_t nq = npos / 4, qpb = (nq + nparts - 1) / nparts;
+#define XQ(m)                                                                                                    \
+    if (mode == m) {                                                                                             \
+      hipLaunchKernelGGL((maxpool_bwd_t<1, 3, 3, 1, 2, 2, m, true>), dim3(nparts), dim3(256), 0, s, p, d,        \
+                         (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, nq, qpb, (const bf16_t*)bn_y,     \
+                         bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef);             \
+      return true;                                                                                               \
+    }
+    XQ(POOL_BWD_PLAIN) XQ(POOL_BWD_GATED) XQ(POOL_BWD_APPLY)
+#undef XQ
+  }
 #define XM(a, b, c, e, f, h, m)                                                                                  \
   if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h && mode == m) {                 \
     hipLaunchKernelGGL((maxpool_bwd_t<a, b, c, e, f, h, m>), dim3(nparts), dim3(256), 0, s, p, d, (const bf16_t*)dy, \

@@ -29,6 +29,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P],
     "milnce_gate_bwd_reduce": [I, P, P, P, P, I, I, P, P],
     "milnce_gate_fc_bwd": [I, P, P, P, P, P, P, P, I, I, P, P],
+    "milnce_pool_set_quad": [I],
     "milnce_gate_bwd_apply": [I, P, P, P, P, P, I, I, P, P, P, P, I, P],
     "milnce_avgpool": [P, I, I, I, P, P],
     "milnce_avgpool_bwd": [P, I, I, I, P, P],

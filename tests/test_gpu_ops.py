@@ -724,10 +724,10 @@ def test_lazy_gate_inputs_match_materialised():
         assert rel_err(a, b) < 1e-5
 
 
-def _gated_pool_grads(h, flag, value, seed=61):
+def _gated_pool_grads(h, flag, value, seed=61, HW=13):
     """conv-BN-ReLU(want gate sum) -> gated_maxpool with hip_ops.<flag> = value: outputs and grads."""
     torch.manual_seed(seed)
-    B, T, HW, cin, C = 2, 4, 13, 32, 64
+    B, T, cin, C = 2, 4, 32, 64
     x = torch.randn(B, T, HW, HW, cin, device=DEV).to(torch.bfloat16)
     conv = nn.Conv3d(cin, C, (3, 1, 1), 1, (1, 0, 0), bias=False).to(DEV)
     fc = nn.Linear(C, C).to(DEV)
@@ -810,3 +810,36 @@ def test_gate_fc_backward_kernel():
     assert rel_err(dmean2, dpre[:, :c0].mm(ws[0].detach())) < 1e-5
     assert rel_err(dws2[0], dpre[:, :c0].t().mm(mean[:, :c0])) < 1e-5
     assert rel_err(dbs2[0], dpre[:, :c0].sum(0)) < 1e-5
+
+
+def _bn_pool_grads(h, seed=62, HW=14):
+    """conv-BN-ReLU -> TF-SAME 1x3x3/2 max pool (stem -> maxpool_2a): pool backward with the BN
+    partial sums of its producer."""
+    torch.manual_seed(seed)
+    x = torch.randn(2, 4, HW, HW, 16, device=DEV).to(torch.bfloat16).requires_grad_(True)
+    conv = nn.Conv3d(16, 64, (1, 3, 3), 1, (0, 1, 1), bias=False).to(DEV)
+    bn = nn.BatchNorm3d(64).to(DEV)
+    z = h.conv_bn_relu(x, conv.weight, bn, (1, 1, 1), (0, 1, 1), True)
+    z = z[0] if isinstance(z, tuple) else z
+    out = h.maxpool3d(z, (1, 3, 3), (1, 2, 2), True)
+    d = torch.randn(out.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(seed)).to(torch.bfloat16)
+    out.backward(d)
+    return (out.float(), x.grad.float(), conv.weight.grad.clone(), bn.weight.grad.clone(), bn.bias.grad.clone())
+
+
+@pytest.mark.parametrize("gated", [False, True])
+def test_pool_quad_gather_matches_per_position(gated):
+    """The 2x2-quad gather of the 1x3x3/2 pool backward (csrc/pool.hip pool_bwd_quad, even H, W)
+    vs the per-position gather: same routed gradients (BN partials summed in another order)."""
+    from mil_nce_howto100m_amd.ops._lib import lib
+    h = hip()
+    res = {}
+    for on in (1, 0):
+        lib().milnce_pool_set_quad(on)
+        try:
+            res[on] = (_gated_pool_grads(h, "_FUSE_GATE_POOL", True, HW=14) if gated else _bn_pool_grads(h))
+        finally:
+            lib().milnce_pool_set_quad(1)
+    assert torch.equal(res[1][0], res[0][0])
+    for a, b in zip(res[1][1:], res[0][1:]):
+        assert rel_err(a, b) < 1e-5
