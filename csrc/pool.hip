@@ -166,6 +166,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(PoolParams p, const bf
 // (the generic kernels above serialise on their per-tap branches).
 struct PoolDivs {
   FastDiv fcpr, fWo, fHo, fTo, fW, fH, fT, fplane;  // fplane: T * H * W (input clip)
+  FastDiv fmt, fmh, fmw;  // block counts of the stride-2 block gather (pool_bwd_block)
 };
 
 // BN: x is the raw conv output of a train-mode BN layer and z = relu(x * scale + shift) is
@@ -379,6 +380,52 @@ __device__ __forceinline__ void pool_bwd_quad(const PoolParams& p, const bf16_t*
   }
 }
 
+// Block gather for stride-2, 3-wide windows (maxpool_2a / 3a: 1x3x3 / (1,2,2); maxpool_4a:
+// 3x3x3 / 2). Along a (K=3, S=2, leading pad p in {0, 1}) dim, block index m covers the inputs
+// i = 2m - p + e (e in {0, 1}), whose windows are the outputs o = m - j (j in {0, 1}) at window
+// offset e + 2j (counted when < 3); with NT == 1 the T dim is (K=1, S=1): t -> t. One thread
+// loads the NT*4 output cells once for its NT*4 inputs instead of NT*4 cells per input.
+template <int NT>
+__device__ __forceinline__ void pool_bwd_block(const PoolParams& p, const bf16_t* __restrict__ dy,
+                                               const uint8_t* __restrict__ arg, uint32_t b, int mt, int mh, int mw,
+                                               int c0, float (*acc)[8]) {
+  constexpr int NU = NT * 4;
+  uint4 g[NU];
+  uint2 a[NU];
+  bool ok[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int jt = u >> 2, jh = (u >> 1) & 1, jw = u & 1;
+    const int to = mt - jt, ho = mh - jh, wo = mw - jw;
+    ok[u] = (to >= 0) & (to < p.To) & (ho >= 0) & (ho < p.Ho) & (wo >= 0) & (wo < p.Wo);
+    const size_t o = ok[u] ? ((((size_t)b * p.To + to) * p.Ho + ho) * p.Wo + wo) * p.C + c0 : (size_t)c0;
+    g[u] = *(const uint4*)(dy + o);
+    a[u] = *(const uint2*)(arg + o);
+  }
+#pragma unroll
+  for (int e = 0; e < NU; ++e)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[e][k] = 0.f;
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int jt = u >> 2, jh = (u >> 1) & 1, jw = u & 1;
+    float gf[8];
+    unpack8(g[u], gf);
+#pragma unroll
+    for (int e = 0; e < NU; ++e) {
+      const int et = e >> 2, eh = (e >> 1) & 1, ew = e & 1;
+      const int dt = NT == 2 ? et + 2 * jt : 0, dh = eh + 2 * jh, dw = ew + 2 * jw;
+      if (dt >= 3 || dh >= 3 || dw >= 3) continue;  // compile-time after unrolling
+      const uint32_t tap = (uint32_t)((dt * 3 + dh) * 3 + dw);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t ak = ((k < 4 ? a[u].x : a[u].y) >> (8 * (k & 3))) & 0xff;
+        acc[e][k] += (ok[u] & (ak == tap)) ? gf[k] : 0.f;
+      }
+    }
+  }
+}
+
 // Thread = fixed 8-channel chunk cc = tid % cpr of rpi = 256/cpr input positions per step; block
 // blockIdx.x walks positions [pos_begin, pos_end), two positions per thread per iteration so
 // both gathers' loads are in flight together. MODE (compile time, so every variant keeps only
@@ -390,7 +437,7 @@ __device__ __forceinline__ void pool_bwd_quad(const PoolParams& p, const bf16_t*
 //                   finalised coefficients coef: the producer conv's output gradient
 enum { POOL_BWD_PLAIN = 0, POOL_BWD_GATED = 1, POOL_BWD_APPLY = 2 };
 
-template <int KT, int KH, int KW, int ST, int SH, int SW, int MODE = POOL_BWD_PLAIN, bool QUAD = false>
+template <int KT, int KH, int KW, int ST, int SH, int SW, int MODE = POOL_BWD_PLAIN, int QUAD = 0>
 __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ dy,
                                                      const uint8_t* __restrict__ arg, bf16_t* __restrict__ dx,
                                                      uint32_t npos, uint32_t pos_per_block,
@@ -488,7 +535,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     if constexpr (MODE == POOL_BWD_APPLY) bn_apply(ps, v);
     if (dx != nullptr) *(uint4*)(dx + (size_t)ps * p.C + c0) = v;
   };
-  if constexpr (QUAD) {  // pos indexes 2x2 input quads (b, t, h2, w2)
+  if constexpr (QUAD == 1) {  // pos indexes 2x2 input quads (b, t, h2, w2) of an even H, W plane
     for (uint32_t q = pos_begin + rr; active && q < pos_end; q += rpi) {
       const uint32_t r = fdiv(q, d.fWo);
       const int w2 = (int)(q - r * p.Wo);
@@ -503,7 +550,27 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       finish(p00 + p.W + 1, a[3]);
     }
   }
-  for (uint32_t pos = pos_begin + rr; !QUAD && active && pos < pos_end; pos += 2 * rpi) {
+  if constexpr (QUAD == 2) {  // pos indexes input blocks (b, mt, mh, mw), see pool_bwd_block
+    constexpr int NT = KT == 3 ? 2 : 1, NU = NT * 4;
+    for (uint32_t q = pos_begin + rr; active && q < pos_end; q += rpi) {
+      const uint32_t r = fdiv(q, d.fmw);
+      const int mw = (int)(q - r * d.fmw.d);
+      const uint32_t r2 = fdiv(r, d.fmh);
+      const int mh = (int)(r - r2 * d.fmh.d);
+      const uint32_t b = fdiv(r2, d.fmt);
+      const int mt = (int)(r2 - b * d.fmt.d);
+      float a[NU][8];
+      pool_bwd_block<NT>(p, dy, arg, b, mt, mh, mw, c0, a);
+#pragma unroll
+      for (int e = 0; e < NU; ++e) {
+        const int it = NT == 2 ? 2 * mt - p.pt + (e >> 2) : mt;
+        const int ih = 2 * mh - p.ph + ((e >> 1) & 1), iw = 2 * mw - p.pw + (e & 1);
+        if (it >= 0 && it < p.T && ih >= 0 && ih < p.H && iw >= 0 && iw < p.W)
+          finish(((b * p.T + it) * p.H + ih) * p.W + iw, a[e]);
+      }
+    }
+  }
+  for (uint32_t pos = pos_begin + rr; QUAD == 0 && active && pos < pos_end; pos += 2 * rpi) {
     const uint32_t pos2 = pos + rpi;
     const bool two = pos2 < pos_end;
     float a0[8], a1[8];
@@ -984,6 +1051,9 @@ static PoolDivs make_divs(const PoolParams& p) {
   d.fWo = make_fastdiv(p.Wo); d.fHo = make_fastdiv(p.Ho); d.fTo = make_fastdiv(p.To);
   d.fW = make_fastdiv(p.W); d.fH = make_fastdiv(p.H); d.fT = make_fastdiv(p.T);
   d.fplane = make_fastdiv(p.T * p.H * p.W);
+  d.fmt = make_fastdiv(p.kt == 3 ? (p.T + p.pt + 1) / 2 : p.T);
+  d.fmh = make_fastdiv((p.H + p.ph + 1) / 2);
+  d.fmw = make_fastdiv((p.W + p.pw + 1) / 2);
   return d;
 }
 
@@ -1077,17 +1147,34 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   const uint32_t npos = (uint32_t)(n / (p.C / 8));
   const uint32_t ppb = (npos + nparts - 1) / nparts;
   const int mode = coef != nullptr ? POOL_BWD_APPLY : (gate_g != nullptr ? POOL_BWD_GATED : POOL_BWD_PLAIN);
-  if (p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 && p.ph == 0 &&
-      p.pw == 0 && p.To == p.T && p.H == 2 * p.Ho && p.W == 2 * p.Wo && g_pool_quad) {
-    const uint32_t nq = npos / 4, qpb = (nq + nparts - 1) / nparts;
-#define XQ(m)                                                                                                    \
-    if (mode == m) {                                                                                             \
-      hipLaunchKernelGGL((maxpool_bwd_t<1, 3, 3, 1, 2, 2, m, true>), dim3(nparts), dim3(256), 0, s, p, d,        \
+  const bool blk133 = p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 &&
+                      p.To == p.T && p.ph <= 1 && p.pw <= 1;
+  const bool blk333 = p.kt == 3 && p.kh == 3 && p.kw == 3 && p.st == 2 && p.sh == 2 && p.sw == 2 && p.pt <= 1 &&
+                      p.ph <= 1 && p.pw <= 1;
+  if ((blk133 || blk333) && g_pool_quad) {
+    const uint32_t nb = npos / (p.T * p.H * p.W);
+    const uint32_t nq = nb * d.fmt.d * d.fmh.d * d.fmw.d, qpb = (nq + nparts - 1) / nparts;
+    // an even H, W plane without leading padding takes the leaner quad indexing (pool_bwd_quad)
+    const bool even = blk133 && p.ph == 0 && p.pw == 0 && p.H == 2 * p.Ho && p.W == 2 * p.Wo;
+#define XQ(a, m)                                                                                                 \
+    if (mode == m && even) {                                                                                     \
+      hipLaunchKernelGGL((maxpool_bwd_t<1, 3, 3, 1, 2, 2, m, 1>), dim3(nparts), dim3(256), 0, s, p, d,           \
                          (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, nq, qpb, (const bf16_t*)bn_y,     \
                          bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef);             \
       return true;                                                                                               \
+    }                                                                                                            \
+    if (mode == m) {                                                                                             \
+      hipLaunchKernelGGL((maxpool_bwd_t<a, 3, 3, a == 3 ? 2 : 1, 2, 2, m, 2>), dim3(nparts), dim3(256), 0, s,    \
+                         p, d, (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, nq, qpb,                     \
+                         (const bf16_t*)bn_y, bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm,        \
+                         inv_thw, coef);                                                                         \
+      return true;                                                                                               \
     }
-    XQ(POOL_BWD_PLAIN) XQ(POOL_BWD_GATED) XQ(POOL_BWD_APPLY)
+    if (blk133) {
+      XQ(1, POOL_BWD_PLAIN) XQ(1, POOL_BWD_GATED) XQ(1, POOL_BWD_APPLY)
+    } else {
+      XQ(3, POOL_BWD_PLAIN) XQ(3, POOL_BWD_GATED) XQ(3, POOL_BWD_APPLY)
+    }
 #undef XQ
   }
 #define XM(a, b, c, e, f, h, m)                                                                                  \

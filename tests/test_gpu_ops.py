@@ -843,3 +843,30 @@ def test_pool_quad_gather_matches_per_position(gated):
     assert torch.equal(res[1][0], res[0][0])
     for a, b in zip(res[1][1:], res[0][1:]):
         assert rel_err(a, b) < 1e-5
+
+
+@pytest.mark.parametrize("shape", [(2, 8, 25, 25, 32), (2, 5, 11, 12, 24), (1, 4, 14, 14, 64)])
+@pytest.mark.parametrize("kernel,stride", [((1, 3, 3), (1, 2, 2)), ((3, 3, 3), (2, 2, 2))])
+def test_pool_block_gather_bitwise(shape, kernel, stride):
+    """Stride-2 block gather (pool_bwd_block: odd/even sizes, leading pads 0 and 1) vs the
+    per-position gather: the same taps summed in the same order, so bitwise equal."""
+    from mil_nce_howto100m_amd.ops._lib import lib
+    torch.manual_seed(13)
+    h = hip()
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    x[:, :, :3, :3, :8] = 0.5  # ties
+    grads = {}
+    for on in (1, 0):
+        lib().milnce_pool_set_quad(on)
+        try:
+            xh = x.clone().requires_grad_(True)
+            y = h.maxpool3d(xh, kernel, stride, True)
+            d = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(5)).to(torch.bfloat16)
+            y.backward(d)
+            grads[on] = xh.grad.clone()
+        finally:
+            lib().milnce_pool_set_quad(1)
+    assert torch.equal(grads[1], grads[0])
+    xr = x.float().requires_grad_(True)
+    aten.maxpool_tf_same(xr, kernel, stride).backward(d.float())
+    assert rel_err(grads[1], xr.grad) < 1e-2
