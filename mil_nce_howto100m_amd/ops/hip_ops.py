@@ -235,10 +235,11 @@ _LAZY_GATE_Z = os.environ.get("MILNCE_LAZY_GATE_Z", "1") != "0"
 #    rebuilds dz = bf16(dout * g + dmean / thw) from dout (milnce_bn_bwd_gate);
 #  * pool inputs (stem -> maxpool_2a, gate -> maxpool_3a): the pool backward computes only the BN
 #    partial sums and a second gather pass applies the BN backward (milnce_maxpool_bwd_apply).
-#    Off by default: the second gather costs as much as the dz round trip it saves (A/B on MI355X:
-#    78.6 vs 78.3 ms/step).
+#    On by default since the stride-2 pool backward gathers per input quad (pool_bwd_quad): the
+#    second gather is now cheaper than the dz round trip it saves (A/B on MI355X: 73.2 vs 73.9
+#    ms/step; with the per-position gather it was 78.6 vs 78.3).
 _LAZY_GATE_DZ = os.environ.get("MILNCE_LAZY_GATE_DZ", "1") != "0"
-_LAZY_POOL_DZ = os.environ.get("MILNCE_LAZY_POOL_DZ", "0") == "1"
+_LAZY_POOL_DZ = os.environ.get("MILNCE_LAZY_POOL_DZ", "1") != "0"
 
 
 def _lazy_z(shape, device, bn_info) -> torch.Tensor:
