@@ -17,6 +17,7 @@
 // 1024 threads: each thread sums ~nparts/128 rows with two chains in flight, then a fixed-order
 // LDS tree reduces the 128 groups (deterministic).
 constexpr int FIN_CH = 8, FIN_RG = 128;
+constexpr int BN_U = 4;  // rows in flight per thread in the streaming apply kernels
 
 __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int nparts, int stride, int c, bool ok,
                                            double& s1, double& s2) {
@@ -107,20 +108,28 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
     sh[k] = active ? ss[3 * C + c0 + k] : 0.f;
     acc[k] = 0.f;
   }
-  if (active) {
+  if (active && r_begin + rr < r_end) {
     const long long base = (long long)b * rows_per_b;
-#pragma unroll 4
-    for (int r = r_begin + rr; r < r_end; r += rpi) {
-      const long long row = base + r;
-      uint4 v = *(const uint4*)(y + row * ldy + c0);
-      float f[8];
-      unpack8(v, f);
+    // BN_U rows in flight per thread: every load of a batch is issued before the first use (rows
+    // past the end re-read the last row and are masked), so the wave is not one-load-at-a-time.
+    for (int r0 = r_begin + rr; r0 < r_end; r0 += BN_U * rpi) {
+      uint4 v[BN_U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
-        acc[k] += f[k];
+      for (int u = 0; u < BN_U; ++u)
+        v[u] = *(const uint4*)(y + (base + min(r0 + u * rpi, r_end - 1)) * ldy + c0);
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const int r = r0 + u * rpi;
+        if (r >= r_end) break;
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
+          acc[k] += f[k];
+        }
+        if (z != nullptr) *(uint4*)(z + (base + r) * ldz + c0) = pack8(f);  // z == null: gating sums only
       }
-      if (z != nullptr) *(uint4*)(z + row * ldz + c0) = pack8(f);  // z == null: gating sums only
     }
   }
   if (gsum == nullptr) return;
@@ -242,18 +251,30 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
   const long long r_begin = (long long)blockIdx.x * rows_per_block;
   const long long r_end = min(M, r_begin + rows_per_block);
-#pragma unroll 4
-  for (long long r = r_begin + rr; r < r_end; r += rpi) {
-    float g[8], v[8], o[8];
-    unpack8(*(const uint4*)(dz + r * ldz + c0), g);
-    unpack8(*(const uint4*)(y + r * ldy + c0), v);
+  if (r_begin + rr >= r_end) return;
+  for (long long r0 = r_begin + rr; r0 < r_end; r0 += BN_U * rpi) {
+    uint4 gv[BN_U], yv[BN_U];  // whole batch issued before the first use (see bn_relu_apply_kernel)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? g[k] : 0.f;
-      const float xh = (v[k] - mean[k]) * istd[k];
-      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+    for (int u = 0; u < BN_U; ++u) {
+      const long long rc = min(r0 + u * rpi, r_end - 1);
+      gv[u] = *(const uint4*)(dz + rc * ldz + c0);
+      yv[u] = *(const uint4*)(y + rc * ldy + c0);
     }
-    *(uint4*)(dy + r * lddy + c0) = pack8(o);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long long r = r0 + u * rpi;
+      if (r >= r_end) break;
+      float g[8], v[8], o[8];
+      unpack8(gv[u], g);
+      unpack8(yv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? g[k] : 0.f;
+        const float xh = (v[k] - mean[k]) * istd[k];
+        o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+      }
+      *(uint4*)(dy + r * lddy + c0) = pack8(o);
+    }
   }
 }
 
@@ -343,20 +364,32 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_gate_kernel(
   }
   const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
   const size_t row0 = (size_t)b * thw;
-#pragma unroll 4
-  for (int r = r_begin + rr; r < r_end; r += rpi) {
-    const size_t row = row0 + r;
-    float d[8], v[8], o[8];
-    unpack8(*(const uint4*)(dout + row * ldo + c0), d);
-    unpack8(*(const uint4*)(y + row * ldy + c0), v);
+  if (r_begin + rr >= r_end) return;
+  for (int r0 = r_begin + rr; r0 < r_end; r0 += BN_U * rpi) {
+    uint4 dv[BN_U], yv[BN_U];  // whole batch issued before the first use (see bn_relu_apply_kernel)
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float dz = bf2f(f2bf(fmaf(d[k], gg[k], dm[k])));  // the value gate_bwd_apply reduced
-      const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? dz : 0.f;
-      const float xh = (v[k] - mean[k]) * istd[k];
-      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+    for (int u = 0; u < BN_U; ++u) {
+      const size_t rc = row0 + min(r0 + u * rpi, r_end - 1);
+      dv[u] = *(const uint4*)(dout + rc * ldo + c0);
+      yv[u] = *(const uint4*)(y + rc * ldy + c0);
     }
-    *(uint4*)(dy + row * lddy + c0) = pack8(o);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int r = r0 + u * rpi;
+      if (r >= r_end) break;
+      const size_t row = row0 + r;
+      float d[8], v[8], o[8];
+      unpack8(dv[u], d);
+      unpack8(yv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = bf2f(f2bf(fmaf(d[k], gg[k], dm[k])));  // the value gate_bwd_apply reduced
+        const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? dz : 0.f;
+        const float xh = (v[k] - mean[k]) * istd[k];
+        o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+      }
+      *(uint4*)(dy + row * lddy + c0) = pack8(o);
+    }
   }
 }
 
