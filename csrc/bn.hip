@@ -296,7 +296,9 @@ static int pick_splits(long long rows, int target_rows) {
 MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, const float* ss, int C, int B,
                                     int rows_per_b, float* gsum, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
-  const int splits = pick_splits(rows_per_b, 512);
+  // ~16 rows per thread (4 batches of BN_U): wide-C layers with few rows per clip (Mixed_4/5) get
+  // enough blocks to fill 256 CUs instead of a couple of long serial blocks per CU.
+  const int splits = pick_splits(rows_per_b, 4 * BN_U * (256 / (C / 8)));
   const int rpb = (rows_per_b + splits - 1) / splits;
   hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy,
                      (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, gsum);

@@ -154,6 +154,7 @@ __global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict
 // Grid (splits, B), each thread owns one fixed 8-channel chunk of the concat row, so when the
 // branches carry producer-BN info the BN-backward partial sums of every branch's last BN layer
 // (sum dz*mask, sum dz*mask*xhat) are produced here: part[b * splits + split][2][Ctot].
+constexpr int GATE_U = 4;  // rows in flight per thread in gate_bwd_apply_kernel
 __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ dmean, int Ctot, int thw,
@@ -182,27 +183,43 @@ __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const b
     a2[k] = 0.f;
   }
   const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
-  if (active) {
+  if (active && r_begin + rr < r_end) {
     const size_t row0 = (size_t)b * thw;
-#pragma unroll 4
-    for (int r = r_begin + rr; r < r_end; r += rpi) {
-      const size_t row = row0 + r;
-      float d[8];
-      unpack8(*(const uint4*)(dout + row * Ctot + c), d);
+    // dz == null: lazy gradient, rebuilt from dout by the BN backward (bn.hip milnce_bn_bwd_gate)
+    bf16_t* const dzp = t.dz[s];
+    const bf16_t* const yp = bn ? t.bn_y[s] : nullptr;
+    const int yld = t.bn_ld[s];
+    // GATE_U rows in flight per thread: the whole batch of loads is issued before the first use
+    // (rows past the end re-read the last row and are masked).
+    for (int r0 = r_begin + rr; r0 < r_end; r0 += GATE_U * rpi) {
+      uint4 ov[GATE_U], yv[GATE_U];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) d[k] = fmaf(d[k], gg[k], dm[k]);
-      const uint4 dv = pack8(d);
-      // dz == null: lazy gradient, rebuilt from dout by the BN backward (bn.hip milnce_bn_bwd_gate)
-      if (t.dz[s] != nullptr) *(uint4*)(t.dz[s] + row * C + cl) = dv;
-      if (bn) {
-        float y[8], dr[8];
-        unpack8(dv, dr);  // partials from the stored (bf16) gradient
-        unpack8(*(const uint4*)(t.bn_y[s] + row * t.bn_ld[s] + cl), y);
+      for (int u = 0; u < GATE_U; ++u) {
+        const size_t rc = row0 + min(r0 + u * rpi, r_end - 1);
+        ov[u] = *(const uint4*)(dout + rc * Ctot + c);
+        if (bn) yv[u] = *(const uint4*)(yp + rc * yld + cl);
+      }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? dr[k] : 0.f;
-          a1[k] += gm;
-          a2[k] += gm * (y[k] - mean[k]) * istd[k];
+      for (int u = 0; u < GATE_U; ++u) {
+        const int r = r0 + u * rpi;
+        if (r >= r_end) break;
+        const size_t row = row0 + r;
+        float d[8];
+        unpack8(ov[u], d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[k] = fmaf(d[k], gg[k], dm[k]);
+        const uint4 dv = pack8(d);
+        if (dzp != nullptr) *(uint4*)(dzp + row * C + cl) = dv;
+        if (bn) {
+          float y[8], dr[8];
+          unpack8(dv, dr);  // partials from the stored (bf16) gradient
+          unpack8(yv[u], y);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float gm = (y[k] * sc[k] + sh[k] > 0.f) ? dr[k] : 0.f;
+            a1[k] += gm;
+            a2[k] += gm * (y[k] - mean[k]) * istd[k];
+          }
         }
       }
     }
