@@ -1546,6 +1546,51 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, bf16_t* __restri
   }
 }
 
+// Every registered weight of the step packed in ONE launch (ops/hip_ops.py _WeightPacker): a
+// descriptor per (weight, mode), blocks assigned by prefix (blk0); element mapping identical to
+// pack_weight_kernel. Replaces ~100 tiny per-conv pack launches per training step.
+struct PackDesc {
+  const float* w;
+  bf16_t* out;
+  int Cout, Cin, Cin_p, KT, KH, KW, Npad, Kpad, mode, blk0, pad0, pad1;
+};
+static_assert(sizeof(PackDesc) == 64, "PackDesc layout is mirrored by a ctypes.Structure");
+constexpr int PACK_ITEMS = 8;  // elements per thread per block
+
+__global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackDesc* __restrict__ descs, int n) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].blk0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const PackDesc d = descs[lo];
+  const int taps = d.KT * d.KH * d.KW;
+  const long long total = (long long)d.Npad * d.Kpad;
+  const long long base = (long long)(blockIdx.x - d.blk0) * 256 * PACK_ITEMS + threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < PACK_ITEMS; ++i) {
+    const long long idx = base + (long long)i * 256;
+    if (idx >= total) break;
+    const int nn = idx / d.Kpad;
+    const int k = idx % d.Kpad;
+    float v = 0.f;
+    if (d.mode == 0) {
+      const int tap = k / d.Cin, c = k % d.Cin;
+      if (nn < d.Cout && tap < taps && c < d.Cin_p) v = d.w[((long long)nn * d.Cin_p + c) * taps + tap];
+    } else {
+      const int tap2 = k / d.Cout, co = k % d.Cout;
+      if (nn < d.Cin_p && tap2 < taps) v = d.w[((long long)co * d.Cin_p + nn) * taps + (taps - 1 - tap2)];
+    }
+    d.out[idx] = f2bf(v);
+  }
+}
+
+MILNCE_API int milnce_pack_weights_multi(const void* descs, int n, int total_blocks, hipStream_t stream) {
+  if (n <= 0 || total_blocks <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_weight_multi_kernel, dim3(total_blocks), dim3(256), 0, stream, (const PackDesc*)descs, n);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 template <int BM, int BN, int BK, bool U8, int EPI>
 static int launch_fwd_epi(ConvParams& p, hipStream_t stream) {

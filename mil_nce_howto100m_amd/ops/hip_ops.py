@@ -22,6 +22,69 @@ BF16 = torch.bfloat16
 F32 = torch.float32
 
 
+class _ZeroArena:
+    """Small zero-initialised fp32 accumulators (SelfGating channel sums, gate-backward dots) carved
+    from one buffer that a single fill re-zeroes per training step, instead of one
+    ``torch.zeros`` launch each (~80 fills per flagship step). Only active between
+    ``zero_arena_begin()`` and ``zero_arena_end()`` (the trainer brackets its step with them), so
+    nothing handed out can outlive the step; elsewhere, on the first step (sizing) and on overflow
+    it falls back to ``torch.zeros``. Slices are built with ``set_`` rather than as views, so each
+    has its own autograd version counter."""
+
+    ALIGN = 64  # fp32 elements: 256-B aligned slices
+
+    def __init__(self):
+        self.buf: Optional[torch.Tensor] = None
+        self.off = 0
+        self.demand = 0
+        self.active = False
+
+    def begin(self, device: torch.device) -> None:
+        if self.demand and (self.buf is None or self.buf.numel() < self.demand or self.buf.device != device):
+            self.buf = torch.zeros(self.demand, dtype=F32, device=device)  # fresh zeros
+        elif self.buf is not None and self.off:
+            self.buf[:self.off].zero_()  # the slices handed out during the previous step
+        self.off = 0
+        self.demand = 0
+        self.active = True
+
+    def end(self) -> None:
+        self.active = False
+
+    def zeros(self, shape: Tuple[int, ...], device: torch.device) -> torch.Tensor:
+        n = math.prod(shape)
+        if not self.active:
+            return torch.zeros(shape, dtype=F32, device=device)
+        na = _ceil(n, self.ALIGN) * self.ALIGN
+        self.demand += na
+        buf = self.buf
+        if buf is None or buf.device != device or self.off + na > buf.numel():
+            return torch.zeros(shape, dtype=F32, device=device)
+        stride = tuple(math.prod(shape[i + 1:]) for i in range(len(shape)))
+        t = torch.empty(0, dtype=F32, device=device).set_(buf.untyped_storage(), self.off, tuple(shape), stride)
+        self.off += na
+        return t
+
+
+_ARENA = _ZeroArena()
+
+
+def zero_arena_begin(device: torch.device) -> None:
+    """Training-step start: re-zero the accumulator arena and pre-pack the step's conv weights."""
+    if device.type == "cuda":
+        _ARENA.begin(device)
+        _PACKER.begin(device)
+
+
+def zero_arena_end() -> None:
+    _ARENA.end()
+    _PACKER.end()
+
+
+def _zeros_f32(shape: Tuple[int, ...], device: torch.device) -> torch.Tensor:
+    return _ARENA.zeros(tuple(int(v) for v in shape), device)
+
+
 def _ceil(a: int, b: int) -> int:
     return (a + b - 1) // b
 
@@ -131,7 +194,81 @@ def conv_plan(x_shape, w_shape, stride, padding, wo_override: int = 0) -> ConvPl
     return plan
 
 
+class _PackDesc(ctypes.Structure):
+    """Mirror of csrc/conv.hip ``PackDesc`` (64 bytes)."""
+    _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p)] + \
+        [(f, ctypes.c_int) for f in ("Cout", "Cin", "Cin_p", "KT", "KH", "KW", "Npad", "Kpad", "mode", "blk0",
+                                     "pad0", "pad1")]
+
+
+class _WeightPacker:
+    """Packs every conv weight of a training step in ONE kernel launch at step start (the weights
+    are fixed between the previous optimizer step and this one), instead of one small pack launch
+    per conv and direction. Entries register themselves the first time ``_pack`` sees a parameter
+    weight inside a step (that step packs per call); from the next step on ``_pack`` returns the
+    pre-packed persistent buffer. Outside a step, or for weights that are not parameters (the
+    concatenated 1x1 group weights), packing stays per call."""
+
+    def __init__(self):
+        self.entries: Dict[Tuple[int, int, int], list] = {}  # (w ptr, mode, plan) -> [weight, plan, mode, out]
+        self.descs: Optional[torch.Tensor] = None
+        self.total_blocks = 0
+        self.active = False
+        self.packed = False
+
+    def begin(self, device: torch.device) -> None:
+        self.active = True
+        self.packed = False
+        if not self.entries:
+            return
+        if self.descs is None:
+            arr = (_PackDesc * len(self.entries))()
+            blk = 0
+            for i, (w, plan, mode, out) in enumerate(self.entries.values()):
+                kt, kh, kw = plan.k
+                npad, kpad = (plan.Npad, plan.Kpad) if mode == 0 else (plan.d_Npad, plan.d_Kpad)
+                arr[i] = _PackDesc(w.data_ptr(), out.data_ptr(), plan.Cout, plan.Cin, plan.Cin_p, kt, kh, kw,
+                                   npad, kpad, mode, blk, 0, 0)
+                blk += _ceil(npad * kpad, 256 * 8)
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            self.descs = host.to(device)
+            self.total_blocks = blk
+        call("milnce_pack_weights_multi", ptr(self.descs), len(self.entries), self.total_blocks, stream())
+        self.packed = True
+
+    def end(self) -> None:
+        self.active = False
+        self.packed = False
+
+    def lookup(self, weight: torch.Tensor, plan: ConvPlan, mode: int) -> Optional[torch.Tensor]:
+        if not self.active:
+            return None
+        e = self.entries.get((weight.data_ptr(), mode, id(plan)))
+        return e[3] if e is not None and self.packed else None
+
+    def register(self, weight: torch.Tensor, plan: ConvPlan, mode: int, out: torch.Tensor) -> None:
+        # parameters only (leaf, requires grad): their storage is fixed for the whole step; the
+        # entry keeps a reference, so the address cannot be recycled for another tensor
+        if self.active and weight.is_leaf and weight.requires_grad and weight.is_contiguous():
+            key = (weight.data_ptr(), mode, id(plan))
+            if key not in self.entries:
+                self.entries[key] = [weight, plan, mode, out]
+                self.descs = None  # rebuilt at the next step start
+
+
+_PACKER = _WeightPacker()
+
+
 def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
+    pre = _PACKER.lookup(weight, plan, mode)
+    if pre is not None:
+        return pre
+    out = _pack_now(weight, plan, mode)
+    _PACKER.register(weight, plan, mode, out)
+    return out
+
+
+def _pack_now(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
     kt, kh, kw = plan.k
     if mode == 0:
         out = torch.empty((plan.Npad, plan.Kpad), dtype=BF16, device=weight.device)
@@ -507,7 +644,7 @@ class _ConvBNReLU(torch.autograd.Function):
         plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
                                      training, wo_override)
         C = plan.Cout
-        gsum = torch.zeros((plan.B, C), dtype=F32, device=x.device) if want_gsum else None
+        gsum = _zeros_f32((plan.B, C), x.device) if want_gsum else None
         lazy = want_gsum and _LAZY_GATE_Z
         z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
         call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
@@ -521,6 +658,7 @@ class _ConvBNReLU(torch.autograd.Function):
         if gsum is None:
             return z
         ctx.mark_non_differentiable(gsum)
+        ctx.set_materialize_grads(False)  # no zero-filled (B, C) gradient launch for gsum
         return z, gsum
 
     @staticmethod
@@ -696,7 +834,7 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
         call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
              ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
              float(hyper[i][1]), int(training), ptr(ss), stream())
-        g = torch.zeros((plan.B, c), dtype=F32, device=dev) if (i == 0 and want_gsum0) else None
+        g = _zeros_f32((plan.B, c), dev) if (i == 0 and want_gsum0) else None
         ysl = y2[:, off:off + c]
         lazy = g is not None and _LAZY_GATE_Z
         z = (_lazy_z((plan.B, plan.To, plan.Ho, plan.Wo, c), dev, (ysl, ss, ctot)) if lazy
@@ -716,6 +854,7 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
     ctx.x_bn = getattr(x, "_milnce_bn", None)
     if gsum is not None:
         ctx.mark_non_differentiable(gsum)
+        ctx.set_materialize_grads(False)  # no zero-filled (B, C) gradient launch for gsum
         return (*zs, gsum)
     return tuple(zs)
 
@@ -944,7 +1083,7 @@ class _GateConcat(torch.autograd.Function):
         gs = take_gate_sums(dout)
         # gs = sum dout * bf16(z * g) = g * sum dout * z, so dpre = gs * (1 - g) (in gate_fc_backward)
         if gs is None:
-            dpre = torch.zeros((B, ctot), dtype=F32, device=dev)
+            dpre = _zeros_f32((B, ctot), dev)
             zr = [_materialize(z) if _is_lazy(z) else z for z in zs]
             call("milnce_gate_bwd_reduce", nseg, widths, _arr(ctypes.c_void_p, [ptr(z) for z in zr]), ptr(dout),
                  ptr(g), B, ctx.thw, ptr(dpre), stream())
@@ -1037,7 +1176,7 @@ class _MaxPool(torch.autograd.Function):
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
         if ctx.x_gate:
             x = ctx.saved_tensors[1]
-            gs = torch.zeros((B, C), dtype=F32, device=dy.device)
+            gs = _zeros_f32((B, C), dy.device)
             call("milnce_maxpool_bwd_gate", ptr(dy.contiguous()), ptr(arg), ptr(dx), *geo, ptr(x), ptr(gs), nparts,
                  stream())
             dx._milnce_gs = gs
@@ -1094,7 +1233,7 @@ class _GatedPool(torch.autograd.Function):
         geo = ctx.geo
         B, T, H, W, C, To, Ho, Wo = geo[:8]
         dout = dout.contiguous()
-        gs = torch.zeros((B, C), dtype=F32, device=dout.device)
+        gs = _zeros_f32((B, C), dout.device)
         call("milnce_gate_dot", ptr(dout), ptr(out), B, To * Ho * Wo, C, ptr(gs), stream())
         dmean, (dw,), (db,) = gate_fc_backward(gs, g, mean, [w], [ctx.bias], [C])
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))

@@ -116,12 +116,20 @@ class Trainer:
             with self.timer.phase("broadcast_buffers"):
                 self.buffers()
         chunks = int(getattr(self.args, "grad_cache_chunks", 0) or 0)
-        if chunks > 1:
-            loss = self._grad_cache_backward(batch, chunks)
-        else:
-            loss = self.forward_loss(batch)
-            with self.timer.phase("backward"):
-                loss.backward()
+        arena = self.ctx.device.type == "cuda" and ops.use_hip(self.bucketer.flat)
+        if arena:
+            from ..ops import hip_ops
+            hip_ops.zero_arena_begin(self.ctx.device)
+        try:
+            if chunks > 1:
+                loss = self._grad_cache_backward(batch, chunks)
+            else:
+                loss = self.forward_loss(batch)
+                with self.timer.phase("backward"):
+                    loss.backward()
+        finally:
+            if arena:
+                hip_ops.zero_arena_end()
         with self.timer.phase("allreduce_wait"):
             self.bucketer.finish()
         with self.timer.phase("optimizer"):

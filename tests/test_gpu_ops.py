@@ -870,3 +870,40 @@ def test_pool_block_gather_bitwise(shape, kernel, stride):
     xr = x.float().requires_grad_(True)
     aten.maxpool_tf_same(xr, kernel, stride).backward(d.float())
     assert rel_err(grads[1], xr.grad) < 1e-2
+
+
+def test_step_weight_prepack_matches_per_call_pack():
+    """The one-launch step pre-pack (hip_ops._WeightPacker) is bitwise identical to the per-conv
+    pack for forward and dgrad layouts, and only kicks in from the second step."""
+    h = hip()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    cases = [((2, 4, 10, 10, 64), (192, 64, 1, 3, 3)), ((2, 4, 10, 10, 96), (128, 96, 3, 1, 1)),
+             ((2, 4, 6, 6, 256), (288, 256, 1, 1, 1))]
+    ws, plans = [], []
+    for xs, wsh in cases:
+        ws.append(nn.Parameter(torch.randn(wsh, device=dev)))
+        k = wsh[2:]
+        plans.append(h.conv_plan(xs, wsh, (1, 1, 1), tuple(kk // 2 for kk in k)))
+    h._PACKER.entries.clear()
+    h._PACKER.descs = None
+    h.zero_arena_begin(dev)
+    first = [[h._pack(w, p, m) for m in (0, 1)] for w, p in zip(ws, plans)]
+    h.zero_arena_end()
+    assert len(h._PACKER.entries) == 2 * len(cases)
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-0.5)  # "optimizer step" between the two training steps
+    h.zero_arena_begin(dev)
+    try:
+        for (w, p), prev in zip(zip(ws, plans), first):
+            for m in (0, 1):
+                got = h._pack(w, p, m)
+                assert got.data_ptr() == prev[m].data_ptr()  # the persistent pre-packed buffer
+                torch.cuda.synchronize()
+                want = h._pack_now(w, p, m)
+                assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    finally:
+        h.zero_arena_end()
+        h._PACKER.entries.clear()
+        h._PACKER.descs = None
