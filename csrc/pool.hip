@@ -510,10 +510,10 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       k0[k] = coef[c]; k1[k] = coef[p.C + c]; k2[k] = coef[2 * p.C + c];
     }
   }
-  auto bn_apply = [&](uint32_t ps, uint4& v) {
+  auto bn_apply = [&](uint32_t ps, uint4& v, const uint4* ypre = nullptr) {
     float dz[8], yv[8], o[8];
     unpack8(v, dz);
-    unpack8(*(const uint4*)(bn_y + (size_t)ps * bn_ld + c0), yv);
+    unpack8(ypre != nullptr ? *ypre : *(const uint4*)(bn_y + (size_t)ps * bn_ld + c0), yv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float gm = (yv[k] * bsc[k] + bsh[k] > 0.f) ? dz[k] : 0.f;
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     v = pack8(o);
   };
   // one input position's epilogue (the quad path; the pair loop below interleaves two of them)
-  auto finish = [&](uint32_t ps, const float* a) {
+  auto finish = [&](uint32_t ps, const float* a, const uint4* ypre = nullptr) {
     uint4 v = pack8(a);
     if (gated) gate_apply(ps, v);
     if (MODE == POOL_BWD_PLAIN && gs != nullptr) gs_add(ps, v, *(const uint4*)(gx + (size_t)ps * p.C + c0));
@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       unpack8(v, dr);
       acc_bn.add(dr, bn_y + (size_t)ps * bn_ld + c0);
     }
-    if constexpr (MODE == POOL_BWD_APPLY) bn_apply(ps, v);
+    if constexpr (MODE == POOL_BWD_APPLY) bn_apply(ps, v, ypre);
     if (dx != nullptr) *(uint4*)(dx + (size_t)ps * p.C + c0) = v;
   };
   if constexpr (QUAD == 1) {  // pos indexes 2x2 input quads (b, t, h2, w2) of an even H, W plane
@@ -542,12 +542,23 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       const uint32_t bt = fdiv(r, d.fHo);
       const int h2 = (int)(r - bt * p.Ho);
       float a[4][8];
-      pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
       const uint32_t p00 = (bt * p.H + 2 * h2) * p.W + 2 * w2;
-      finish(p00, a[0]);
-      finish(p00 + 1, a[1]);
-      finish(p00 + p.W, a[2]);
-      finish(p00 + p.W + 1, a[3]);
+      if constexpr (MODE == POOL_BWD_APPLY) {
+        // the quad's BN inputs are loaded together with the gather, not one after each store
+        uint4 yq[4];
+        const uint32_t pq[4] = {p00, p00 + 1, p00 + p.W, p00 + p.W + 1};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) yq[i] = *(const uint4*)(bn_y + (size_t)pq[i] * bn_ld + c0);
+        pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) finish(pq[i], a[i], &yq[i]);
+      } else {
+        pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
+        finish(p00, a[0]);
+        finish(p00 + 1, a[1]);
+        finish(p00 + p.W, a[2]);
+        finish(p00 + p.W + 1, a[3]);
+      }
     }
   }
   if constexpr (QUAD == 2) {  // pos indexes input blocks (b, mt, mh, mw), see pool_bwd_block
