@@ -261,9 +261,10 @@ struct BnAcc {
       mu[k] = ss[c0 + k]; is[k] = ss[C + c0 + k]; sc[k] = ss[2 * C + c0 + k]; sh[k] = ss[3 * C + c0 + k];
     }
   }
-  __device__ __forceinline__ void add(const float* d, const bf16_t* ypos) {
+  __device__ __forceinline__ void add(const float* d, const bf16_t* ypos) { addv(d, *(const uint4*)ypos); }
+  __device__ __forceinline__ void addv(const float* d, const uint4& yraw) {
     float yv[8];
-    unpack8(*(const uint4*)ypos, yv);
+    unpack8(yraw, yv);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float gm = (yv[k] * sc[k] + sh[k] > 0.f) ? d[k] : 0.f;
@@ -523,14 +524,17 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     v = pack8(o);
   };
   // one input position's epilogue (the quad path; the pair loop below interleaves two of them)
-  auto finish = [&](uint32_t ps, const float* a, const uint4* ypre = nullptr) {
+  // ypre / xpre: the position's bn_y / gx rows when the caller already loaded them
+  auto finish = [&](uint32_t ps, const float* a, const uint4* ypre = nullptr, const uint4* xpre = nullptr) {
     uint4 v = pack8(a);
     if (gated) gate_apply(ps, v);
-    if (MODE == POOL_BWD_PLAIN && gs != nullptr) gs_add(ps, v, *(const uint4*)(gx + (size_t)ps * p.C + c0));
+    if (MODE == POOL_BWD_PLAIN && gs != nullptr)
+      gs_add(ps, v, xpre != nullptr ? *xpre : *(const uint4*)(gx + (size_t)ps * p.C + c0));
     if (bn) {
       float dr[8];
       unpack8(v, dr);
-      acc_bn.add(dr, bn_y + (size_t)ps * bn_ld + c0);
+      if (ypre != nullptr) acc_bn.addv(dr, *ypre);
+      else acc_bn.add(dr, bn_y + (size_t)ps * bn_ld + c0);
     }
     if constexpr (MODE == POOL_BWD_APPLY) bn_apply(ps, v, ypre);
     if (dx != nullptr) *(uint4*)(dx + (size_t)ps * p.C + c0) = v;
@@ -543,22 +547,20 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       const int h2 = (int)(r - bt * p.Ho);
       float a[4][8];
       const uint32_t p00 = (bt * p.H + 2 * h2) * p.W + 2 * w2;
-      if constexpr (MODE == POOL_BWD_APPLY) {
-        // the quad's BN inputs are loaded together with the gather, not one after each store
-        uint4 yq[4];
-        const uint32_t pq[4] = {p00, p00 + 1, p00 + p.W, p00 + p.W + 1};
+      // the quad's per-position side inputs (BN input rows, gate input rows) are loaded together
+      // with the gather, not one after each store
+      const bool need_y = MODE == POOL_BWD_APPLY || bn;
+      const bool need_x = MODE == POOL_BWD_PLAIN && gs != nullptr;
+      const uint32_t pq[4] = {p00, p00 + 1, p00 + p.W, p00 + p.W + 1};
+      uint4 yq[4], xq[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) yq[i] = *(const uint4*)(bn_y + (size_t)pq[i] * bn_ld + c0);
-        pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) finish(pq[i], a[i], &yq[i]);
-      } else {
-        pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
-        finish(p00, a[0]);
-        finish(p00 + 1, a[1]);
-        finish(p00 + p.W, a[2]);
-        finish(p00 + p.W + 1, a[3]);
+      for (int i = 0; i < 4; ++i) {
+        if (need_y) yq[i] = *(const uint4*)(bn_y + (size_t)pq[i] * bn_ld + c0);
+        if (need_x) xq[i] = *(const uint4*)(gx + (size_t)pq[i] * p.C + c0);
       }
+      pool_bwd_quad(p, dy, arg, bt, h2, w2, c0, a);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) finish(pq[i], a[i], need_y ? &yq[i] : nullptr, need_x ? &xq[i] : nullptr);
     }
   }
   if constexpr (QUAD == 2) {  // pos indexes input blocks (b, mt, mh, mw), see pool_bwd_block
