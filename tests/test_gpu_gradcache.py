@@ -1,0 +1,50 @@
+"""GradCache step on the HIP path, inside the per-step zero arena / weight pre-pack bracket
+(ops/hip_ops.py zero_arena_begin/end): same loss and gradient as the one-shot step with eval-mode
+BN, on the second bracketed step (the one that uses the arena and the pre-packed weights)."""
+import pytest
+import torch
+
+from mil_nce_howto100m_amd.config import get_args
+from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+from mil_nce_howto100m_amd.parallel import dist as pdist
+from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+
+pytestmark = pytest.mark.gpu
+
+
+def _trainer(chunks, dev):
+    args = get_args(argv=["--batch_size", "4", "--num_frames", "8", "--video_size", "64", "--num_candidates", "2",
+                          "--word2vec_path", "", "--grad_cache_chunks", str(chunks)])
+    ctx = pdist.DistContext(device=dev)
+    pdist.set_context(ctx)
+    seed_everything(3, 0)
+    model = build_model(args, dev)
+    return Trainer(args, model, ctx, 10), args
+
+
+def test_gradcache_in_arena_matches_full_batch_on_gpu():
+    from mil_nce_howto100m_amd.ops import hip_ops
+    dev = torch.device("cuda")
+    full, args = _trainer(0, dev)
+    gc, _ = _trainer(2, dev)
+    data = SyntheticClips(4, 8, 64, 2, args.max_words, args.vocab_size, device=dev)
+    batch = data.batch(0)
+    for step in range(2):  # step 0 sizes the arena / registers the packs, step 1 uses them
+        full.model.eval()
+        gc.model.eval()
+        full.bucketer.zero()
+        gc.bucketer.zero()
+        hip_ops.zero_arena_begin(dev)
+        try:
+            loss_a = full.forward_loss(batch)
+            loss_a.backward()
+            ga = full.bucketer.flat.clone()
+            loss_b = gc._grad_cache_backward(batch, 2)
+            gb = gc.bucketer.flat.clone()
+        finally:
+            hip_ops.zero_arena_end()
+        torch.cuda.synchronize()
+        assert torch.isfinite(ga).all() and torch.isfinite(gb).all()
+        assert abs(float(loss_a) - float(loss_b)) < 2e-2 * max(1.0, abs(float(loss_a))), step
+        rel = ((ga - gb).norm() / ga.norm()).item()
+        assert rel < 5e-2, (step, rel)
