@@ -3,7 +3,13 @@
 num_candidates=4, bf16, 256 clips per GPU (BASELINE.json configs 2 and 3).
 
     python bench.py --gpus N --steps K --warmup W
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    (or under python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+With WORLD_SIZE unset and N > 1 the script is its own launcher (reference
+``main_distributed.py:57-60``): before anything touches HIP it starts N fresh child processes,
+one per GPU, with the torchrun environment on 127.0.0.1 (``parallel/launch.py``). Every rank
+checks that the process group it joined has exactly N ranks, and the JSON reports the world
+size observed through ``torch.distributed``.
 
 Each timed step is the full training step: on-device synthetic batch generation, forward of
 both towers, cross-GPU all-gather of embeddings, MIL-NCE on the global batch, backward with
@@ -40,17 +46,22 @@ def main():
                     help="GradCache micro-batches per GPU (config 5: 32f, 1024 clips/GPU)")
     opts = ap.parse_args()
 
+    if opts.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        from mil_nce_howto100m_amd.parallel.launch import launch_local
+        return launch_local(os.path.abspath(__file__), sys.argv[1:], opts.gpus)
+
     import torch
     from mil_nce_howto100m_amd.config import get_args
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
     from mil_nce_howto100m_amd.parallel import dist as pdist
     from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != opts.gpus and world == 1 and opts.gpus > 1:
-        print(f"warning: --gpus {opts.gpus} but WORLD_SIZE=1; launch with torch.distributed.run",
-              file=sys.stderr)
     ctx = pdist.init_distributed("nccl", opts.device)
+    observed = pdist.observed_world_size()
+    if observed != opts.gpus or ctx.world_size != opts.gpus:
+        print(f"error: --gpus {opts.gpus} but the process group has {observed} rank(s)", file=sys.stderr)
+        pdist.destroy()
+        return 2
     b = opts.batch_per_gpu
     args = get_args(argv=["--batch_size", str(b * ctx.world_size), "--num_frames", str(opts.num_frames),
                           "--video_size", str(opts.size), "--num_candidates", str(opts.num_candidates),
@@ -124,7 +135,7 @@ def main():
             "metric": "video-text pairs/sec/node (S3D-G MIL-NCE train step)",
             "value": round(pairs, 2),
             "unit": "pairs/s",
-            "n_gpus": ctx.world_size,
+            "n_gpus": observed,
             "steps": opts.steps,
             "warmup": opts.warmup,
             "ms_per_step": round(ms, 3),
@@ -135,18 +146,21 @@ def main():
             "data": "synthetic (on-device generator, random-init weights)",
             "config": {"model": "S3D-G + word2vec text tower, " + ("MIL-NCE" if opts.loss == "milnce"
                                                                     else f"{opts.loss} (soft-DTW)"),
-                       "global_batch": b * ctx.world_size, "seq_len": opts.num_frames,
+                       "global_batch": b * ctx.world_size,
+                       # no token sequence in the MIL-NCE step; soft-DTW: clips per sequence
+                       "seq_len": opts.seq_len if opts.loss != "milnce" else None,
                        "frames": opts.num_frames, "resolution": opts.size,
                        "num_candidates": opts.num_candidates,
-                       "parallelism": f"dp{ctx.world_size}",
-                       "grad_cache_chunks": opts.grad_cache_chunks,
-                       **({"sdtw_seq_len": opts.seq_len} if opts.loss != "milnce" else {})},
+                       "parallelism": f"dp{observed}",
+                       "backend": ctx.backend,
+                       "grad_cache_chunks": opts.grad_cache_chunks},
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
         }
         print(json.dumps(out), flush=True)
     pdist.destroy()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -6,8 +6,9 @@
 
 Process model (replaces ``main_distributed.py:35-62`` / ``mp.spawn`` + UDP IP probe):
   * under ``torchrun``/``torch.distributed.run`` (``WORLD_SIZE`` set): one rank per process;
-  * otherwise: one process per visible GPU, spawned here with a 127.0.0.1 rendezvous
-    (the reference forces ``--multiprocessing-distributed`` the same way, ``:48``);
+  * otherwise: one fresh process per visible GPU, started here with a 127.0.0.1 rendezvous
+    before anything touches HIP (``parallel/launch.py``; the reference forces
+    ``--multiprocessing-distributed`` the same way, ``:48``);
   * no GPU: single CPU process on gloo (the plumbing configuration).
 ``--batch_size`` is global per node and divided across ranks (``:88``). Data is the on-device
 synthetic generator unless ``--synthetic 0`` (which needs ffmpeg + the HowTo100M files).
@@ -15,25 +16,10 @@ synthetic generator unless ``--synthetic 0`` (which needs ffmpeg + the HowTo100M
 from __future__ import annotations
 
 import os
-import socket
 import sys
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-
-
-def _free_port() -> int:
-    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
-def worker(local_rank: int, world: int, port: int, argv):
-    os.environ.update({"RANK": str(local_rank), "LOCAL_RANK": str(local_rank), "WORLD_SIZE": str(world),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
-    run(argv)
 
 
 def run(argv):
@@ -59,13 +45,14 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     if "WORLD_SIZE" in os.environ:
         return run(argv)
-    import torch
-    n = torch.cuda.device_count()
+    # count GPUs without initialising HIP in this (parent) process, then start one fresh
+    # child per GPU (parallel/launch.py) -- the parent never touches the device
+    from mil_nce_howto100m_amd.parallel.launch import count_gpus_no_init, launch_local
+    n = count_gpus_no_init()
     if n <= 1:
         return run(argv)
-    import torch.multiprocessing as mp
-    mp.spawn(worker, nprocs=n, args=(n, _free_port(), argv))
+    return launch_local(os.path.abspath(__file__), argv, n)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

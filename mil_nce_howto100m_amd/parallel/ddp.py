@@ -59,6 +59,7 @@ class GradBucketer:
         self.buckets.append([cur_start, off])
         self.bucket_size.append(cur_count)
         self._pending: List[int] = list(self.bucket_size)
+        self._ready: set = set()
         self._handles: List[Optional[object]] = [None] * len(self.buckets)
         self.sync_enabled = True  # False: accumulate only (micro-batches before the last)
         self._hooks = []
@@ -77,6 +78,7 @@ class GradBucketer:
     def zero(self) -> None:
         self.flat.zero_()
         self._pending = list(self.bucket_size)
+        self._ready = set()
         self._handles = [None] * len(self.buckets)
 
     def _launch(self, b: int) -> None:
@@ -85,8 +87,15 @@ class GradBucketer:
                                            async_op=True)
 
     def _on_grad(self, p: torch.Tensor) -> None:
-        if not self.sync_enabled:
+        """A parameter's gradient for this step is complete (enqueued on the compute stream).
+
+        Idempotent per step: a parameter whose gradient a HIP kernel wrote in place reports
+        through ``ops.grad_sink`` when that kernel is enqueued, and autograd then still runs
+        its post-accumulate hook (with nothing to accumulate); counting both would issue the
+        bucket's all-reduce while half of its gradients are still missing."""
+        if not self.sync_enabled or id(p) in self._ready:
             return
+        self._ready.add(id(p))
         b = self.bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0 and self._handles[b] is None:
@@ -97,6 +106,7 @@ class GradBucketer:
         buffer; the pass run with sync on issues every bucket as its last gradient lands."""
         self.sync_enabled = bool(enabled)
         self._pending = list(self.bucket_size)
+        self._ready = set()
 
     def finish(self) -> None:
         """Issue buckets whose params got no gradient this step, then wait for all."""

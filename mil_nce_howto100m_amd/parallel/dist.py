@@ -77,6 +77,11 @@ def init_distributed(backend: str = "nccl", device: str = "auto", timeout_s: int
     return _CTX
 
 
+def observed_world_size() -> int:
+    """World size as torch.distributed sees it (1 without a process group)."""
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
 def set_context(ctx: DistContext) -> None:
     global _CTX
     _CTX = ctx

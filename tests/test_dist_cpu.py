@@ -88,17 +88,19 @@ def _worker_grad(rank, world, port, outdir, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,ratio", [("reference", 0.5), ("exact", 1.0)])
-def test_dp_gradient_scale(mode, ratio):
+@pytest.mark.parametrize("mode,world", [("reference", 2), ("exact", 2), ("reference", 4)])
+def test_dp_gradient_scale(mode, world):
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
     from mil_nce_howto100m_amd.parallel import dist as pdist
     from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
-    world, port = 2, _port()
+    ratio = 1.0 / world if mode == "reference" else 1.0
+    port = _port()
     with tempfile.TemporaryDirectory() as out:
         mp.spawn(_worker_grad, args=(world, port, out, mode), nprocs=world)
         res = _collect(out, world)
-    g0, g1 = res[0][1], res[1][1]
-    assert torch.allclose(g0, g1, atol=1e-6)
+    g0 = res[0][1]
+    for r in range(1, world):
+        assert torch.allclose(g0, res[r][1], atol=1e-6)
     # single process, full global batch (both ranks' samples, rank-major)
     ctx = pdist.DistContext()
     pdist.set_context(ctx)
@@ -106,9 +108,8 @@ def test_dp_gradient_scale(mode, ratio):
     seed_everything(1, 0)
     model = build_model(args, ctx.device)
     tr = Trainer(args, model, ctx, 10)
-    d0 = SyntheticClips(2, 4, 32, 2, 20, 500, rank=0, world_size=2).batch(0)
-    d1 = SyntheticClips(2, 4, 32, 2, 20, 500, rank=1, world_size=2).batch(0)
-    batch = {k: torch.cat([d0[k], d1[k]]) for k in ("video", "text")}
+    ds = [SyntheticClips(2, 4, 32, 2, 20, 500, rank=r, world_size=world).batch(0) for r in range(world)]
+    batch = {k: torch.cat([d[k] for d in ds]) for k in ("video", "text")}
     tr.model.eval()
     tr.bucketer.zero()
     loss = tr.forward_loss(batch)
