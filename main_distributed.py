@@ -33,10 +33,7 @@ def run(argv):
     ctx = pdist.init_distributed(args.dist_backend, args.device, args.dist_timeout_s)
     args.rank, args.world_size = ctx.rank, ctx.world_size
     try:
-        if args.evaluate:
-            from mil_nce_howto100m_amd.train.evaluation import evaluate_hmdb_during_training
-            evaluate_hmdb_during_training(args, ctx)
-        run_training(args, ctx)
+        run_training(args, ctx)  # -e/--evaluate: HMDB probe every max(1, total_bs // 512) epochs
     finally:
         pdist.destroy()
 

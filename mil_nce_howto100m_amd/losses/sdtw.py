@@ -4,9 +4,12 @@ The reference defines these but wires none into an entry point; here ``--loss`` 
 (BASELINE.json config 4) with a sequence batch (``data.synthetic.SyntheticSequences``).
 Semantics are reproduced, with the hard-coded constants generalised:
 
-* ``CDTW`` (``loss.py:20-32``): gathered sequences [W, n, d]; pos = sdtw(v[rank], t[rank]),
-  neg = sdtw(v[rank] vs every rank's t) (the reference's ``repeat(8, ...)`` is world size 8);
-  loss = pos - logsumexp(neg). gamma 1e-5, cosine.
+* ``CDTW`` (``loss.py:20-32``): gathered sequences [W*b, n, d] (the reference has b = 1 per
+  rank); for each of this rank's own sequences r (rows rank*b .. rank*b+b-1): pos = sdtw(v[r],
+  t[r]), neg = sdtw(v[r] vs every gathered t) (the reference's ``repeat(8, ...)`` is world size 8
+  at b = 1); loss = mean_r(pos - logsumexp(neg)). gamma 1e-5, cosine. At b = 1 this is the
+  reference's v[rank]; with b > 1 every local sequence (hence every local video embedding, the
+  only rows the gather's local-slice backward keeps) gets a gradient.
 * ``SDTW_CIDM`` (``loss.py:34-68``): contrastive-IDM regulariser on intra-sequence cosine
   distances (sigma 10 s, lambda 1, weights 1/(|dt|+1)) + sdtw(gamma 0.1, cosine); mean.
 * ``SDTW_negative`` (``loss.py:70-91``): sdtw(gamma 0.1, cosine) + sum of exp(<v, t>) over all
@@ -37,14 +40,19 @@ class CDTW(nn.Module):
     def __init__(self, args=None):
         super().__init__()
         self.rank = getattr(args, "rank", 0) if args is not None else 0
+        self.world = max(1, getattr(args, "world_size", 1) if args is not None else 1)
         self.sdtw = SoftDTW(True, gamma=1e-5, dist_func="cosine")
 
     def forward(self, video_embd, text_embd):
-        r = self.rank if self.rank < video_embd.shape[0] else 0
-        w = text_embd.shape[0]
-        pos = self.sdtw(video_embd[r].unsqueeze(0), text_embd[r].unsqueeze(0))
-        neg = self.sdtw(video_embd[r].unsqueeze(0).expand(w, -1, -1).contiguous(), text_embd)
-        return (pos - torch.logsumexp(neg, 0)).unsqueeze(0).mean()
+        total = text_embd.shape[0]
+        b = max(1, total // self.world)  # sequences per rank
+        r0 = self.rank * b if self.rank * b < total else 0
+        v = video_embd[r0:r0 + b]                                          # [b, n, d] local
+        pos = self.sdtw(v, text_embd[r0:r0 + b])                           # [b]
+        vv = v.unsqueeze(1).expand(-1, total, -1, -1).reshape((b * total,) + tuple(v.shape[1:]))
+        tt = text_embd.unsqueeze(0).expand(b, -1, -1, -1).reshape((b * total,) + tuple(text_embd.shape[1:]))
+        neg = self.sdtw(vv.contiguous(), tt.contiguous()).view(b, total)  # [b, W*b]
+        return (pos - torch.logsumexp(neg, 1)).mean()
 
 
 class SDTW_CIDM(nn.Module):

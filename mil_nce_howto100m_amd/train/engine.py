@@ -58,6 +58,8 @@ class Trainer:
     def __init__(self, args, model: S3D, ctx: pdist.DistContext, steps_per_epoch: int):
         self.args, self.model, self.ctx = args, model, ctx
         self.device = ctx.device
+        # the reference overwrites --rank / --world-size with the process's own (main_distributed.py:46-47,69)
+        args.rank, args.world_size = ctx.rank, ctx.world_size
         broadcast_parameters(model, ctx.world_size)
         params = list(model.parameters())
         scale = 1.0 / ctx.world_size if getattr(args, "grad_scale", "reference") == "reference" else 1.0
@@ -202,21 +204,16 @@ def checkpoint_dir_of(args) -> str:
 
 
 def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, float]:
-    """Epoch loop of main_distributed.py:185-200 on synthetic on-device data."""
-    from ..data.synthetic import SyntheticClips
+    """Epoch loop of main_distributed.py:185-200 over the synthetic or the HowTo100M feed."""
+    from ..data.loader import build_train_feed
 
     ctx = ctx or pdist.context()
     seed_everything(args.seed, ctx.rank)
     # batch_size is per node; divided across the node's GPUs like main_distributed.py:88.
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size)))
     local_bs = max(1, args.batch_size // max(1, local_world))
-    data = SyntheticClips(local_bs, args.num_frames, args.video_size, args.num_candidates,
-                          args.max_words, args.vocab_size, seed=args.seed, device=ctx.device,
-                          rank=ctx.rank, world_size=ctx.world_size, epoch_len=args.synthetic_len)
-    if getattr(args, "loss", "milnce") != "milnce":
-        from ..data.synthetic import SyntheticSequences
-        data = SyntheticSequences(local_bs, args.seq_len, data)
-    steps_per_epoch = len(data) if not args.steps_per_epoch else min(len(data), args.steps_per_epoch)
+    feed = build_train_feed(args, ctx, local_bs)
+    steps_per_epoch = feed.steps_per_epoch
     model = build_model(args, ctx.device)
     trainer = Trainer(args, model, ctx, steps_per_epoch)
     metrics = MetricsLogger(getattr(args, "log_jsonl", ""), ctx.rank)
@@ -236,17 +233,22 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
             log("=> loaded checkpoint '{}' (epoch {})".format(path, start_epoch), args, ctx.rank)
         else:
             log("=> no checkpoint found at '{}'".format(cdir), args, ctx.rank)
-    total_bs = local_bs * ctx.world_size
+    total_bs = local_bs * ctx.world_size  # clips per step over all ranks
     log("Starting training loop for rank: {}, total batch size: {}".format(ctx.rank, total_bs), args, ctx.rank)
     last = {}
     watchdog = Watchdog(getattr(args, "watchdog_s", 0.0), ctx.rank,
                         dump_dir=getattr(args, "log_root", "log") or "log").start()
+    eval_every = max(1, total_bs // 512)  # main_distributed.py:188
     for epoch in range(start_epoch, args.epochs):
+        if args.evaluate and epoch % eval_every == 0 and not (epoch == start_epoch and start_step):
+            from .evaluation import evaluate_hmdb_during_training
+            res = evaluate_hmdb_during_training(args, ctx, trainer.model)
+            if ctx.is_main and res:
+                metrics.write(epoch=epoch, step=trainer.global_step, hmdb=res)
         running = torch.zeros((), device=ctx.device)
         t0 = time.time()
         first = start_step if epoch == start_epoch else 0
-        for i in range(first, steps_per_epoch):
-            batch = data.batch(epoch * steps_per_epoch + i)
+        for i, batch in enumerate(feed.epoch(epoch, first), start=first):
             running += trainer.train_step(batch)
             watchdog.beat(trainer.global_step)
             if (i + 1) % args.n_display == 0:
@@ -254,7 +256,8 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
                 d = time.time() - t0
                 lr = trainer.optimizer.param_groups[0]["lr"]
                 if args.verbose:
-                    log(train_line(epoch + 1, d, total_bs * float(i) / max(1, data.epoch_len), avg, lr), args, ctx.rank)
+                    log(train_line(epoch + 1, d, total_bs * float(i) / max(1, feed.epoch_len), avg, lr), args,
+                        ctx.rank)
                 metrics.write(epoch=epoch + 1, step=trainer.global_step, loss=avg, lr=lr,
                               pairs_per_s=total_bs * args.n_display / max(d, 1e-9),
                               phase_ms=trainer.timer.summary())

@@ -37,20 +37,35 @@ def load_eval_model(args, device) -> S3D:
     return model.to(device).eval()
 
 
-def _loader(ds, batch_size, workers):
-    return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=False, drop_last=False,
-                                       num_workers=workers)
+def _native(b):
+    b = dict(b)
+    b["video"] = to_model_layout(b["video"])
+    return b
 
 
-def _native_batches(loader):
-    for b in loader:
-        b = dict(b)
-        b["video"] = to_model_layout(b["video"])
-        yield b
+def _sharded_batches(ds, batch_size, workers, rank, world):
+    """Only this rank's batches are ever decoded (eval/sharding.py sharded_loader)."""
+    from ..eval.sharding import sharded_loader
+    return sharded_loader(ds, batch_size, workers, rank, world, convert=_native)
 
 
 def _use_real(csv: str, root: str) -> bool:
     return bool(csv) and os.path.isfile(csv) and os.path.isdir(root) and ffmpeg_available()
+
+
+def _synthetic_fallback(args, csv: str, what: str) -> None:
+    """No CSV / videos / ffmpeg: an explicitly requested eval CSV is an error; otherwise the
+    synthetic labelled set runs (pipeline check only) with a loud warning."""
+    missing = [m for m, ok in (("CSV " + repr(csv), bool(csv) and os.path.isfile(csv)),
+                               ("video root " + repr(args.eval_video_root), os.path.isdir(args.eval_video_root)),
+                               ("ffmpeg", ffmpeg_available())) if not ok]
+    if getattr(args, "eval_csv", ""):
+        raise FileNotFoundError(f"{what} eval: --eval_csv given but missing: {', '.join(missing)}")
+    import warnings
+    msg = (f"{what} eval is running on SYNTHETIC clips (missing: {', '.join(missing)}); the numbers only check "
+           f"the pipeline, they are not {what} results")
+    warnings.warn(msg, RuntimeWarning, stacklevel=3)
+    print("WARNING: " + msg, flush=True)
 
 
 def _graph_env(args) -> None:
@@ -70,8 +85,9 @@ def eval_hmdb(args, device, model: Optional[S3D] = None, ctx=None) -> dict:
     csv = getattr(args, "eval_csv", "") or os.path.join("csv", "hmdb51.csv")
     if _use_real(csv, args.eval_video_root):
         ds = HMDBDataset(csv, args.eval_video_root, args.num_windows_test, args.num_frames, args.video_size)
-        batches = _native_batches(_loader(ds, args.batch_size_val, max(1, args.num_thread_reader)))
+        batches = _sharded_batches(ds, args.batch_size_val, max(1, args.num_thread_reader), rank, world)
     else:
+        _synthetic_fallback(args, csv, "HMDB")
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,
                                    args.num_frames, args.video_size, device=device).batches(args.batch_size_val)
     feats, labels, splits = extract_features(model, batches, device, rank, world)
@@ -92,8 +108,9 @@ def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None, ctx=Non
     if _use_real(csv, args.eval_video_root):
         ds = WindowedClipDataset(csv, args.eval_video_root, tok, args.num_windows_test, args.fps, args.num_frames,
                                  args.video_size, kind)
-        batches = _native_batches(_loader(ds, args.batch_size_val, max(1, args.num_thread_reader)))
+        batches = _sharded_batches(ds, args.batch_size_val, max(1, args.num_thread_reader), rank, world)
     else:
+        _synthetic_fallback(args, csv, kind)
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,
                                    args.num_frames, args.video_size, device=device).batches(args.batch_size_val)
     m = evaluate_retrieval(model, batches, device, rank, world)
@@ -102,7 +119,10 @@ def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None, ctx=Non
     return m
 
 
-def evaluate_hmdb_during_training(args, ctx) -> Optional[dict]:
-    if not ctx.is_main:
-        return None
-    return eval_hmdb(args, ctx.device)
+def evaluate_hmdb_during_training(args, ctx, model: Optional[S3D] = None) -> Optional[dict]:
+    """HMDB probe of the model being trained (``main_distributed.py:188-189``, run every
+    ``max(1, total_bs // 512)`` epochs before the epoch's training). Feature extraction is
+    sharded over all ranks; rank 0 fits the probe. The model is left in eval mode; the next
+    training step switches it back."""
+    res = eval_hmdb(args, ctx.device, model=model, ctx=ctx)
+    return res if ctx.is_main else None
