@@ -55,11 +55,12 @@ def ffmpeg_available() -> bool:
 
 def decode_clip(path: str, size: int, fps: Optional[float] = None, start: Optional[float] = None,
                 duration: Optional[float] = None, crop_only: bool = False, center_crop: bool = True,
-                hflip: bool = False) -> np.ndarray:
+                hflip: bool = False, rng: Optional[random.Random] = None) -> np.ndarray:
     """ffmpeg decode -> uint8 [T, size, size, 3]."""
     if not ffmpeg_available():
         raise RuntimeError("ffmpeg not found: real-video datasets need it; use the synthetic generators")
-    aw, ah = (0.5, 0.5) if center_crop else (random.uniform(0, 1), random.uniform(0, 1))
+    rng = rng or random
+    aw, ah = (0.5, 0.5) if center_crop else (rng.uniform(0, 1), rng.uniform(0, 1))
     filters = []
     if fps:
         filters.append(f"fps={fps}")
@@ -87,10 +88,15 @@ def _fit_frames(v: np.ndarray, n: int, size: int) -> np.ndarray:
 
 
 class HowTo100MDataset(Dataset):
+    """Random choices (caption, seek, crop, flip) are drawn from a generator seeded by
+    (seed, epoch, index) -- not the process-global ``random`` of the reference -- so an item is the
+    same whichever worker loads it and a resumed run sees exactly the data of an uninterrupted one."""
+
     def __init__(self, csv: str, video_root: str, caption_root: str, tokenizer: Tokenizer, min_time: float = 5.0,
                  fps: int = 10, num_frames: int = 32, size: int = 224, crop_only: bool = True,
-                 center_crop: bool = False, random_flip: bool = True, num_candidates: int = 4):
+                 center_crop: bool = False, random_flip: bool = True, num_candidates: int = 4, seed: int = 0):
         import pandas as pd
+        self.seed, self.epoch = int(seed), 0
         self.csv = pd.read_csv(csv)
         self.video_root, self.caption_root, self.tok = video_root, caption_root, tokenizer
         self.min_time, self.fps, self.num_frames, self.size = min_time, fps, num_frames, size
@@ -100,6 +106,9 @@ class HowTo100MDataset(Dataset):
 
     def __len__(self):
         return len(self.csv)
+
+    def set_epoch(self, epoch: int) -> None:
+        self.epoch = int(epoch)
 
     @staticmethod
     def nearest_candidates(starts, ends, ind: int, k: int) -> int:
@@ -117,9 +126,9 @@ class HowTo100MDataset(Dataset):
             n += 1
         return start
 
-    def _text(self, cap: dict):
+    def _text(self, cap: dict, rng: random.Random):
         starts, ends, texts = cap["start"], cap["end"], cap["text"]
-        ind = random.randint(0, len(texts) - 1)
+        ind = rng.randint(0, len(texts) - 1)
         if self.k == 1:
             words = self.tok(texts[ind])
         else:
@@ -139,11 +148,12 @@ class HowTo100MDataset(Dataset):
         vid = vf.split(".")[0]
         with open(os.path.join(self.caption_root, vid + ".json")) as f:
             cap = json.load(f)
-        text, s, e = self._text(cap)
-        seek = random.randint(s, int(max(s, e - self.num_sec)))
-        flip = self.random_flip and random.uniform(0, 1) > 0.5
+        rng = random.Random((self.seed * 1000003 + self.epoch) * 1000003 + int(idx))
+        text, s, e = self._text(cap, rng)
+        seek = rng.randint(s, int(max(s, e - self.num_sec)))
+        flip = self.random_flip and rng.uniform(0, 1) > 0.5
         v = decode_clip(os.path.join(self.video_root, vf), self.size, self.fps, seek, self.num_sec + 0.1,
-                        self.crop_only, self.center_crop, flip)
+                        self.crop_only, self.center_crop, flip, rng=rng)
         return {"video": torch.from_numpy(_fit_frames(v, self.num_frames, self.size).copy()), "text": text}
 
 
@@ -196,6 +206,12 @@ class HMDBDataset(Dataset):
 
     def __len__(self):
         return len(self.data)
+
+    def meta(self, idx):
+        """(label with the ``_test`` suffix stripped, split1, split2, split3) without decoding."""
+        row = self.data.iloc[idx]
+        label = row["label"][:-5] if row["label"].endswith("_test") else row["label"]
+        return label, int(row["split1"]), int(row["split2"]), int(row["split3"])
 
     def __getitem__(self, idx):
         row = self.data.iloc[idx]

@@ -139,6 +139,8 @@ class HowTo100MFeed:
     def epoch(self, epoch: int, start_step: int = 0) -> Iterator[Dict]:
         self.sampler.set_epoch(epoch)
         self.sampler.set_start(start_step * self.b)
+        if hasattr(self.ds, "set_epoch"):
+            self.ds.set_epoch(epoch)  # workers get a fresh copy of the dataset per epoch
         for i, batch in enumerate(DevicePrefetcher(self.loader, self.device), start=start_step):
             if i >= self.steps_per_epoch:
                 break
@@ -184,7 +186,7 @@ def build_train_feed(args, ctx, local_bs: int):
     tok = Tokenizer(getattr(args, "token_to_word_path", ""), max_words=args.max_words)
     ds = HowTo100MDataset(csv, vroot, croot, tok, min_time=args.min_time, fps=args.fps, num_frames=args.num_frames,
                           size=args.video_size, crop_only=bool(args.crop_only), center_crop=bool(args.centercrop),
-                          random_flip=bool(args.random_flip), num_candidates=args.num_candidates)
+                          random_flip=bool(args.random_flip), num_candidates=args.num_candidates, seed=args.seed)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(ctx.world_size)))
     workers = max(0, args.num_thread_reader // max(1, local_world))
     return HowTo100MFeed(ds, local_bs, ctx.rank, ctx.world_size, ctx.device, workers, bool(args.pin_memory),

@@ -51,9 +51,27 @@ def inception(x, sd, p, training):
     return torch.cat(outs, dim=1)
 
 
+def space_to_depth(x):
+    """[B, C, T, H, W] -> [B, 8C, T/2, H/2, W/2], channel = ((dt*2 + dh)*2 + dw)*C + c
+    (the public S3D_HowTo100M weights' input transform)."""
+    b, c, t, h, w = x.shape
+    x = x.reshape(b, c, t // 2, 2, h // 2, 2, w // 2, 2)
+    out = torch.empty(b, 8 * c, t // 2, h // 2, w // 2, dtype=x.dtype)
+    for dt in range(2):
+        for dh in range(2):
+            for dw in range(2):
+                j = (dt * 2 + dh) * 2 + dw
+                out[:, j * c:(j + 1) * c] = x[:, :, :, dt, :, dh, :, dw]
+    return out
+
+
 def s3d_video(sd, video_ncdhw, training=True, mixed5c=False):
     w = sd["conv1.conv1.weight"]
-    x = F.relu(_bn(F.conv3d(video_ncdhw, w, None, 2, (1, 3, 3)), sd, "conv1.bn1", training))
+    if w.shape[1] == 24:  # space-to-depth stem: [2,4,4] conv, pad (1,2,2), BN+ReLU, then crop 1 in T/H/W
+        x = F.relu(_bn(F.conv3d(space_to_depth(video_ncdhw), w, None, 1, (1, 2, 2)), sd, "conv1.bn1", training))
+        x = x[:, :, 1:, 1:, 1:]
+    else:
+        x = F.relu(_bn(F.conv3d(video_ncdhw, w, None, 2, (1, 3, 3)), sd, "conv1.bn1", training))
     x = tf_pool(x, *POOLS["maxpool_2a"])
     x = unit(x, sd, "conv_2b", training=training)
     x = unit(x, sd, "conv_2c", 1, 1, training)

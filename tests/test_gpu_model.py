@@ -138,3 +138,23 @@ def test_full_model_loss_matches_aten_at_batch_32():
             va, ta = m_aten(b["video"], text)
             loss_a = float(ops.milnce_loss(va.float(), ta.float()))
     assert abs(loss - loss_a) < 0.02 * abs(loss_a), (loss, loss_a)
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_space_to_depth_model_on_gpu_matches_fp64(training):
+    """Public-weights variant on the HIP path: the s2d stem conv (Cin=24, [2,4,4], pad (1,2,2))
+    through the implicit-GEMM kernel, crop, and the rest of the tower vs the fp64 NCDHW oracle."""
+    import ref_s3d
+    from mil_nce_howto100m_amd.models import S3D
+    torch.manual_seed(6)
+    m = S3D(512, space_to_depth=True, blocks=["mixed_3b", "mixed_3c"]).cuda().train(training)
+    sd = {k: v.detach().double().cpu().clone() for k, v in m.state_dict().items()}
+    u8 = torch.randint(0, 256, (4, 8, 64, 64, 4), dtype=torch.uint8)
+    u8[..., 3] = 0
+    with torch.no_grad():
+        f = m(u8.cuda(), None, mode="video", mixed5c=True).double().cpu()
+    ref = ref_s3d.s3d_video(sd, u8[..., :3].permute(0, 4, 1, 2, 3).double() / 255.0, training=training,
+                            mixed5c=True)
+    rel = ((f - ref).norm() / ref.norm()).item()
+    print(f"s2d tower rel err vs fp64: {rel:.4f}")
+    assert rel < 0.03, rel

@@ -85,3 +85,18 @@ def test_checkpoint_roundtrip_reference_format():
         # a plain nn.Module with the reference's names loads it strictly (DataParallel-style)
         plain = torch.nn.DataParallel(S3D(512, blocks=["mixed_3b"]))
         plain.load_state_dict(loaded["state_dict"], strict=True)
+
+
+def test_space_to_depth_forward_matches_ncdhw_oracle():
+    """The public-weights (space-to-depth) variant: s2d input transform, [2,4,4] conv1 with pad
+    (1,2,2), BN+ReLU over the uncropped output, crop [1:, 1:, 1:] (s3dg.py:248-253, 267-272);
+    fp64 against an independent NCDHW oracle, train and eval mode."""
+    torch.manual_seed(4)
+    m = S3D(512, space_to_depth=True, blocks=["mixed_3b", "mixed_3c"]).double()
+    v = torch.rand(2, 3, 8, 64, 64, dtype=torch.float64)
+    for training in (True, False):
+        m.train(training)
+        sd = {k: x.clone() for k, x in m.state_dict().items()}
+        f = m(v, None, mode="video", mixed5c=True)
+        ref = ref_s3d.s3d_video(sd, v, training=training, mixed5c=True)
+        assert torch.allclose(f, ref, rtol=1e-8, atol=1e-9), (training, (f - ref).abs().max())
