@@ -1817,6 +1817,16 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
   return (int)hipGetLastError();
 }
 
+// host launcher of the slab reduction for the other translation units (csrc/conv_halo.hip)
+int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int Kpad, int Cout, int Cin,
+                        int Cin_param, int taps, int accumulate, hipStream_t stream) {
+  const long long total = (long long)Cout * taps * Cin;
+  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, slab, dw, splits, Npad, Kpad,
+                     Cout, Cin, Cin_param, taps, accumulate);
+  return (int)hipGetLastError();
+}
+
 MILNCE_API int milnce_pack_weight(const float* w, void* out, int Cout, int Cin, int Cin_p, int KT, int KH,
                                   int KW, int Npad, int Kpad, int mode, hipStream_t stream) {
   const long long total = (long long)Npad * Kpad;

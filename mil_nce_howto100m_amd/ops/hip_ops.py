@@ -504,6 +504,37 @@ def _wgrad_tiles(Cout: int) -> List[int]:
 
 _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
 _W_OCCS = (4, 2)  # split-K occupancy candidates (workgroups per CU)
+_HALO_WGRAD = os.environ.get("MILNCE_HALO_WGRAD", "1") != "0"
+# (3,1,1) is implemented too (csrc/conv_halo.hip) but measures slower than the im2col kernel
+# (3 taps amortise the per-box cost less): tools/halo_bench.py, profiles/r2_halo_wgrad.md
+_HALO_KERNELS = ((1, 3, 3),)
+
+
+def _halo_wgrad_ok(plan: ConvPlan, x: torch.Tensor) -> bool:
+    """Box-tiled wgrad (csrc/conv_halo.hip) covers stride-1 same-padded (1,3,3) / (3,1,1) convs
+    over bf16 activations."""
+    return (_HALO_WGRAD and x.dtype == BF16 and plan.k in _HALO_KERNELS and plan.s == (1, 1, 1)
+            and plan.p == tuple(k // 2 for k in plan.k) and not plan.wo_override and plan.Cin % 8 == 0
+            and plan.Cin == plan.Cin_p)
+
+
+_HALO_SPLITS: Dict[Tuple[int, int], Tuple[int, int]] = {}
+
+
+def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: torch.Tensor, accumulate: int) -> None:
+    kt, kh, kw = plan.k
+    key = (id(plan), cc)
+    geo = _HALO_SPLITS.get(key)
+    if geo is None:
+        floats, splits = ctypes.c_longlong(0), ctypes.c_int(0)
+        rc = lib().milnce_halo_wgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, 64, cc, 0,
+                                          ctypes.byref(floats), ctypes.byref(splits))
+        if rc != 0:
+            raise RuntimeError(f"halo wgrad plan failed ({rc}) for {plan}")
+        geo = _HALO_SPLITS[key] = (int(floats.value), int(splits.value))
+    slab = torch.empty((geo[0],), dtype=F32, device=dy.device)
+    call("milnce_halo_wgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target), accumulate, plan.B, plan.T,
+         plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, 64, cc, geo[1], stream())
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -523,6 +554,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             return dw
 
     def launch_with(tn, impl, occ, target, accumulate):
+        if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
+            return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate)
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
         slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
         call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
@@ -539,6 +572,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 for impl in _WIDE_W_IMPLS.get(tn, _W_IMPLS):
                     for occ in _W_OCCS:
                         cands.append((tn, impl, occ))
+            if _halo_wgrad_ok(plan, x):
+                cands += [(64, 164, 0)]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4)

@@ -45,6 +45,10 @@ def main():
     tr = Trainer(args, build_model(args, ctx.device), ctx, 100)
     tr.train_step(data.batch(0))
     torch.cuda.synchronize()
+    print("plans as tuned inside the training step:")
+    for key, plan in sorted(hip_ops._PLANS.items(), key=lambda kv: -kv[1].M * kv[1].Cout * kv[1].Ktot):
+        print(f"  {key[0]}->{plan.Cout} k{plan.k}: fwd impl {plan.impl} dgrad {plan.d_impl} wgrad {plan.w_impl} "
+              f"(tn {plan.w_tn})", flush=True)
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     flops_tot = 0.0
     print(f"{'shape (B,T,H,W,Cin)->Cout k s':58s} {'GFLOP':>7s} {'fwd ms':>7s} {'TF/s':>6s} {'dgr ms':>7s} "
