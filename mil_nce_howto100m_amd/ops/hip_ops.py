@@ -1404,8 +1404,50 @@ class _MILNCE(torch.autograd.Function):
         return dx.mm(t), dx.t().mm(v)
 
 
-def milnce_loss(video_embd, text_embd):
-    return _MILNCE.apply(video_embd.float().contiguous(), text_embd.float().contiguous())
+class _MILNCEFused(torch.autograd.Function):
+    """MIL-NCE without the [Bg, Bg*K] logits (csrc/milnce_fused.hip): tiled fp32-MFMA logits with
+    row / block-column log-sum-exp partials forward, tile-wise recompute backward."""
+
+    @staticmethod
+    def forward(ctx, v, t):
+        B, D = v.shape
+        K = t.shape[0] // B
+        n_ct, n_rt = _ceil(B * K, 64), _ceil(B, 64)
+        ws = torch.empty((2 * (n_ct * B + n_rt * B) + B,), dtype=F32, device=v.device)
+        den = torch.empty((B,), dtype=F32, device=v.device)
+        nom = torch.empty((B,), dtype=F32, device=v.device)
+        loss = torch.empty((1,), dtype=F32, device=v.device)
+        call("milnce_fused_fwd", ptr(v), ptr(t), B, K, D, ptr(ws), ptr(den), ptr(nom), ptr(loss), stream())
+        ctx.save_for_backward(v, t, den, nom)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        v, t, den, nom = ctx.saved_tensors
+        B, D = v.shape
+        K = t.shape[0] // B
+        dv, dt = torch.empty_like(v), torch.empty_like(t)
+        gg = g.reshape(1).float().contiguous()
+        call("milnce_fused_bwd", ptr(v), ptr(t), B, K, D, ptr(den), ptr(nom), ptr(gg), ptr(dv), ptr(dt), stream())
+        return dv, dt
+
+
+# Fused by default where the tiling applies (K | 64, D a multiple of 64 up to 512); MILNCE_FUSED_LOSS=0
+# selects the logits-materialising path (hipBLASLt GEMMs + LSE kernels).
+_FUSED_LOSS = os.environ.get("MILNCE_FUSED_LOSS", "1") != "0"
+
+
+def milnce_fused_ok(v: torch.Tensor, t: torch.Tensor) -> bool:
+    B, D = v.shape
+    K = t.shape[0] // max(1, B)
+    return K >= 1 and 64 % K == 0 and t.shape[0] == B * K and D % 64 == 0 and D <= 512
+
+
+def milnce_loss(video_embd, text_embd, fused: Optional[bool] = None):
+    v, t = video_embd.float().contiguous(), text_embd.float().contiguous()
+    if (_FUSED_LOSS if fused is None else fused) and milnce_fused_ok(v, t):
+        return _MILNCEFused.apply(v, t)
+    return _MILNCE.apply(v, t)
 
 
 # =========================================================================================

@@ -40,3 +40,50 @@ def test_halo_wgrad_matches_fp32(shape, cc):
     torch.cuda.synchronize()
     err = ((out - 0.5 - ref).norm() / ref.norm()).item()
     assert err < 2e-5, err
+
+
+@pytest.mark.parametrize("B,K,scale", [(8, 4, 1.0), (100, 4, 0.05), (256, 4, 0.05), (256, 1, 0.05), (130, 2, 0.05),
+                                        (96, 8, 0.05), (2048, 4, 0.05)])
+def test_fused_milnce_matches_fp64(B, K, scale):
+    """Fused MIL-NCE (csrc/milnce_fused.hip, no [Bg, Bg*K] tensor) vs the loss.py formula in fp64:
+    loss and both gradients; B not a multiple of the 64-tile, every K that divides 64."""
+    from mil_nce_howto100m_amd.ops import aten
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(B + K)
+    v = (torch.randn(B, 512, device="cuda") * scale).requires_grad_(True)
+    t = (torch.randn(B * K, 512, device="cuda") * scale).requires_grad_(True)
+    assert h.milnce_fused_ok(v, t)
+    loss = h.milnce_loss(v, t, fused=True)
+    (loss * 1.7).backward()
+    vr = v.detach().double().cpu().requires_grad_(True)
+    tr = t.detach().double().cpu().requires_grad_(True)
+    lr = aten.milnce_loss(vr, tr)
+    (lr * 1.7).backward()
+    assert abs(loss.item() - lr.item()) < 1e-5 * max(1.0, abs(lr.item())), (loss.item(), lr.item())
+    rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
+    assert rel(v.grad, vr.grad) < 1e-4 and rel(t.grad, tr.grad) < 1e-4, (rel(v.grad, vr.grad), rel(t.grad, tr.grad))
+
+
+def test_fused_milnce_memory_and_time_at_8192():
+    """BASELINE config 5's global batch (Bg = 8192, K = 4): the fused loss allocates ~1 MiB of
+    workspace instead of two 1 GiB logit / dlogit tensors."""
+    import time
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    B, K = 8192, 4
+    v = (torch.randn(B, 512, device="cuda") * 0.05).requires_grad_(True)
+    t = (torch.randn(B * K, 512, device="cuda") * 0.05).requires_grad_(True)
+    out = {}
+    for fused in (True, False):
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats()
+        base = torch.cuda.memory_allocated()
+        t0 = time.perf_counter()
+        loss = h.milnce_loss(v, t, fused=fused)
+        loss.backward()
+        torch.cuda.synchronize()
+        out[fused] = (float(loss), (torch.cuda.max_memory_allocated() - base) / 2 ** 20, time.perf_counter() - t0)
+        v.grad = t.grad = None
+    print(f"fused: loss {out[True][0]:.5f} peak +{out[True][1]:.0f} MiB {out[True][2] * 1e3:.1f} ms | "
+          f"materialised: loss {out[False][0]:.5f} peak +{out[False][1]:.0f} MiB {out[False][2] * 1e3:.1f} ms")
+    assert abs(out[True][0] - out[False][0]) < 1e-4 * abs(out[False][0])
+    assert out[True][1] < 200 and out[False][1] > 1000
