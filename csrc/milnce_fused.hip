@@ -194,6 +194,8 @@ __global__ __launch_bounds__(256) void milnce_fused_dv_kernel(const float* __res
   float* Tc = Ss + TM * GP;       // [TN][DP]  T chunk for the G GEMM
   const int N = B * K;
   const int r0 = blockIdx.x * TM;
+  const int split = blockIdx.y, splits = gridDim.y;
+  dV += (long long)split * B * D;  // split > 0 (or splits > 1): partial sums, reduced afterwards
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ndc = D / DC;
   f32x4 out[8][4];  // up to D = 512: [d chunk][16-col block] of this wave's 16 rows
@@ -202,7 +204,8 @@ __global__ __launch_bounds__(256) void milnce_fused_dv_kernel(const float* __res
 #pragma unroll
     for (int c = 0; c < 4; ++c) out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int n_ct = (N + TN - 1) / TN;
-  for (int ct = 0; ct < n_ct; ++ct) {
+  const int ct_begin = (int)((long long)split * n_ct / splits), ct_end = (int)((long long)(split + 1) * n_ct / splits);
+  for (int ct = ct_begin; ct < ct_end; ++ct) {
     const int c0 = ct * TN;
     f32x4 acc[4];
     logit_tile(V, T, B, N, D, r0, c0, Vs, Ts, acc);
@@ -257,6 +260,8 @@ __global__ __launch_bounds__(256) void milnce_fused_dt_kernel(const float* __res
   float* Vc = Ss + TM * GP;  // [TM][DP] V chunk
   const int N = B * K;
   const int c0 = blockIdx.x * TN;
+  const int split = blockIdx.y, splits = gridDim.y;
+  dT += (long long)split * N * D;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int ndc = D / DC;
   f32x4 out[8][4];  // this wave's 16 text rows (tile columns 16w..) x D
@@ -265,7 +270,8 @@ __global__ __launch_bounds__(256) void milnce_fused_dt_kernel(const float* __res
 #pragma unroll
     for (int c = 0; c < 4; ++c) out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int n_rt = (B + TM - 1) / TM;
-  for (int rt = 0; rt < n_rt; ++rt) {
+  const int rt_begin = (int)((long long)split * n_rt / splits), rt_end = (int)((long long)(split + 1) * n_rt / splits);
+  for (int rt = rt_begin; rt < rt_end; ++rt) {
     const int r0 = rt * TM;
     f32x4 acc[4];
     logit_tile(V, T, B, N, D, r0, c0, Vs, Ts, acc);
@@ -309,6 +315,28 @@ __global__ __launch_bounds__(256) void milnce_fused_dt_kernel(const float* __res
         }
 }
 
+__global__ void milnce_split_sum_kernel(const float4* __restrict__ part, int splits, long long n4,
+                                        float4* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    float4 a = part[i];
+    for (int s = 1; s < splits; ++s) {
+      const float4 b = part[s * n4 + i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    }
+    out[i] = a;
+  }
+}
+
+// Split counts of the two backward passes: ~2 workgroups per CU over (tiles x reduction ranges).
+MILNCE_API int milnce_fused_bwd_splits(int B, int K, int* s_dv, int* s_dt) {
+  const int N = B * K;
+  const int n_ct = (N + TN - 1) / TN, n_rt = (B + TM - 1) / TM;
+  int a = (512 + n_rt - 1) / n_rt, b = (512 + n_ct - 1) / n_ct;
+  *s_dv = a < n_ct ? a : n_ct;
+  *s_dt = b < n_rt ? b : n_rt;
+  return 0;
+}
+
 // Workspace floats needed by the fused forward (row + column partials).
 MILNCE_API long long milnce_fused_ws_floats(int B, int K) {
   const long long N = (long long)B * K;
@@ -333,15 +361,32 @@ MILNCE_API int milnce_fused_fwd(const float* V, const float* T, int B, int K, in
   return (int)hipGetLastError();
 }
 
+// dV / dT; with s_dv / s_dt > 1 the passes write partial sums to `part` ([s][B][D] then [s][N][D])
+// which are summed into dV / dT.
 MILNCE_API int milnce_fused_bwd(const float* V, const float* T, int B, int K, int D, const float* den, const float* nom,
-                                const float* gup, float* dV, float* dT, hipStream_t stream) {
+                                const float* gup, float* dV, float* dT, int s_dv, int s_dt, float* part,
+                                hipStream_t stream) {
   if (K < 1 || TN % K || D % DC || D > 8 * DC) return (int)hipErrorInvalidValue;
   const int N = B * K;
   const size_t lds = (size_t)(TM * SP + TN * SP + TM * GP + 64 * DP) * sizeof(float);
-  hipLaunchKernelGGL(milnce_fused_dv_kernel, dim3((B + TM - 1) / TM), dim3(256), lds, stream, V, T, B, K, D, den, nom,
-                     gup, dV);
+  float* pv = s_dv > 1 ? part : dV;
+  hipLaunchKernelGGL(milnce_fused_dv_kernel, dim3((B + TM - 1) / TM, s_dv), dim3(256), lds, stream, V, T, B, K, D,
+                     den, nom, gup, pv);
   HIP_RET(hipGetLastError());
-  hipLaunchKernelGGL(milnce_fused_dt_kernel, dim3((N + TN - 1) / TN), dim3(256), lds, stream, V, T, B, K, D, den, nom,
-                     gup, dT);
+  if (s_dv > 1) {
+    const long long n4 = (long long)B * D / 4;
+    hipLaunchKernelGGL(milnce_split_sum_kernel, dim3((int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048)),
+                       dim3(256), 0, stream, (const float4*)pv, s_dv, n4, (float4*)dV);
+    HIP_RET(hipGetLastError());
+  }
+  float* pt = s_dt > 1 ? part : dT;
+  hipLaunchKernelGGL(milnce_fused_dt_kernel, dim3((N + TN - 1) / TN, s_dt), dim3(256), lds, stream, V, T, B, K, D,
+                     den, nom, gup, pt);
+  HIP_RET(hipGetLastError());
+  if (s_dt > 1) {
+    const long long n4 = (long long)N * D / 4;
+    hipLaunchKernelGGL(milnce_split_sum_kernel, dim3((int)((n4 + 255) / 256 < 2048 ? (n4 + 255) / 256 : 2048)),
+                       dim3(256), 0, stream, (const float4*)pt, s_dt, n4, (float4*)dT);
+  }
   return (int)hipGetLastError();
 }

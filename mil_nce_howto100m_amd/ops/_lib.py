@@ -58,7 +58,8 @@ SIGNATURES: Dict[str, list] = {
     "milnce_text_relu_max_bwd": [P, P, P, I, I, I, P, P],
     "milnce_loss_fwd": [P, I, I, P, P, P, P],
     "milnce_fused_fwd": [P, P, I, I, I, P, P, P, P, P],
-    "milnce_fused_bwd": [P, P, I, I, I, P, P, P, P, P, P],
+    "milnce_fused_bwd": [P, P, I, I, I, P, P, P, P, P, I, I, P, P],
+    "milnce_fused_bwd_splits": [I, I, P, P],
     "milnce_loss_bwd": [P, P, P, P, I, I, P, P],
     "milnce_softdtw_fwd": [P, I, I, I, I, I, L, L, F, F, P, P, P],
     "milnce_softdtw_bwd": [P, P, I, I, I, I, I, L, L, F, F, P, P, P],

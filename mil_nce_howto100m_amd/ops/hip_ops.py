@@ -1428,13 +1428,23 @@ class _MILNCEFused(torch.autograd.Function):
         K = t.shape[0] // B
         dv, dt = torch.empty_like(v), torch.empty_like(t)
         gg = g.reshape(1).float().contiguous()
-        call("milnce_fused_bwd", ptr(v), ptr(t), B, K, D, ptr(den), ptr(nom), ptr(gg), ptr(dv), ptr(dt), stream())
+        sv, st = ctypes.c_int(1), ctypes.c_int(1)
+        lib().milnce_fused_bwd_splits(B, K, ctypes.byref(sv), ctypes.byref(st))
+        sv, st = int(sv.value), int(st.value)
+        part = torch.empty((max(sv * B, st * B * K if st > 1 else 0) * D if max(sv, st) > 1 else 1,), dtype=F32,
+                           device=v.device)
+        call("milnce_fused_bwd", ptr(v), ptr(t), B, K, D, ptr(den), ptr(nom), ptr(gg), ptr(dv), ptr(dt), sv, st,
+             ptr(part), stream())
         return dv, dt
 
 
-# Fused by default where the tiling applies (K | 64, D a multiple of 64 up to 512); MILNCE_FUSED_LOSS=0
-# selects the logits-materialising path (hipBLASLt GEMMs + LSE kernels).
-_FUSED_LOSS = os.environ.get("MILNCE_FUSED_LOSS", "1") != "0"
+# Fused where the tiling applies (K | 64, D a multiple of 64 up to 512) and the logits would take
+# >= 4 GiB (Bg >= 16384 at K = 4): the fused path trades time for memory -- steady state on one
+# MI355X, forward + backward: Bg 256 0.27 vs 0.29 ms, 2048 1.67 vs 0.59 ms, 8192 25.4 vs 8.2 ms
+# (fused vs hipBLASLt-materialised), peak +144 MiB vs +2128 MiB at 8192 (tests/test_gpu_halo.py).
+# MILNCE_FUSED_LOSS=0/1 forces either path.
+_FUSED_LOSS = os.environ.get("MILNCE_FUSED_LOSS", "auto")
+_FUSED_MIN_LOGITS = 1 << 30
 
 
 def milnce_fused_ok(v: torch.Tensor, t: torch.Tensor) -> bool:
@@ -1445,7 +1455,9 @@ def milnce_fused_ok(v: torch.Tensor, t: torch.Tensor) -> bool:
 
 def milnce_loss(video_embd, text_embd, fused: Optional[bool] = None):
     v, t = video_embd.float().contiguous(), text_embd.float().contiguous()
-    if (_FUSED_LOSS if fused is None else fused) and milnce_fused_ok(v, t):
+    if fused is None:
+        fused = _FUSED_LOSS == "1" or (_FUSED_LOSS == "auto" and v.shape[0] * t.shape[0] >= _FUSED_MIN_LOGITS)
+    if fused and milnce_fused_ok(v, t):
         return _MILNCEFused.apply(v, t)
     return _MILNCE.apply(v, t)
 

@@ -74,16 +74,37 @@ def test_fused_milnce_memory_and_time_at_8192():
     t = (torch.randn(B * K, 512, device="cuda") * 0.05).requires_grad_(True)
     out = {}
     for fused in (True, False):
-        torch.cuda.synchronize()
-        torch.cuda.reset_peak_memory_stats()
-        base = torch.cuda.memory_allocated()
-        t0 = time.perf_counter()
-        loss = h.milnce_loss(v, t, fused=fused)
-        loss.backward()
-        torch.cuda.synchronize()
-        out[fused] = (float(loss), (torch.cuda.max_memory_allocated() - base) / 2 ** 20, time.perf_counter() - t0)
-        v.grad = t.grad = None
+        for _ in range(3):  # steady state on the last repetition
+            torch.cuda.synchronize()
+            torch.cuda.reset_peak_memory_stats()
+            base = torch.cuda.memory_allocated()
+            t0 = time.perf_counter()
+            loss = h.milnce_loss(v, t, fused=fused)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[fused] = (float(loss.detach()), (torch.cuda.max_memory_allocated() - base) / 2 ** 20,
+                          time.perf_counter() - t0)
+            v.grad = t.grad = None
     print(f"fused: loss {out[True][0]:.5f} peak +{out[True][1]:.0f} MiB {out[True][2] * 1e3:.1f} ms | "
           f"materialised: loss {out[False][0]:.5f} peak +{out[False][1]:.0f} MiB {out[False][2] * 1e3:.1f} ms")
     assert abs(out[True][0] - out[False][0]) < 1e-4 * abs(out[False][0])
-    assert out[True][1] < 200 and out[False][1] > 1000
+    assert out[True][1] < 400 and out[False][1] > 1000
+
+
+@pytest.mark.parametrize("B", [256, 1024, 2048])
+def test_fused_milnce_speed_report(B):
+    """Steady-state time of the fused vs materialising loss (forward + backward) at the global
+    batches of 1, 4 and 8 GPUs (printed; the dispatch threshold in ops/hip_ops.py follows it)."""
+    import time
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    v = (torch.randn(B, 512, device="cuda") * 0.05).requires_grad_(True)
+    t = (torch.randn(B * 4, 512, device="cuda") * 0.05).requires_grad_(True)
+    res = {}
+    for fused in (True, False):
+        for rep in range(5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            h.milnce_loss(v, t, fused=fused).backward()
+            torch.cuda.synchronize()
+            res[fused] = (time.perf_counter() - t0) * 1e3
+    print(f"B {B}: fused {res[True]:.3f} ms, materialised {res[False]:.3f} ms")
