@@ -448,14 +448,17 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   constexpr int STAGE_ELEMS = (BM + BN) * BK;
   constexpr int RING_BYTES = STAGES * STAGE_ELEMS * 2;
   constexpr int EPI_BYTES = BM * LDE * 2;
-  constexpr int TAB_OFF_BYTES = RING_BYTES > EPI_BYTES ? RING_BYTES : EPI_BYTES;
+  // the producer-BN constants (EPI 2) sit behind the epilogue staging, inside the drained ring
+  // when it is large enough: the whole kernel then needs only the ring's LDS (two 80 KiB
+  // workgroups per CU at BN 192 x BK 64 x 2 stages, i.e. two waves per SIMD)
+  constexpr int SSL_BYTES = EPI == 2 ? 16 * BN : 0;
   static_assert(A_INST >= 1 && B_INST >= 1, "tile too small for the DMA mapping");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* ring = (bf16_t*)smem;  // stage s: A [BM][BK] then B [BN][BK]
   bf16_t* Es = (bf16_t*)smem;    // epilogue staging [BM][LDE] (after the ring drained)
-  int2* tab = (int2*)(smem + TAB_OFF_BYTES);
-  float* ssl = (float*)(smem + TAB_OFF_BYTES + 8 * 160);
+  float* ssl = (float*)(smem + EPI_BYTES);  // [4][BN] producer-BN constants (EPI 2), per tile
+  (void)SSL_BYTES;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -476,13 +479,6 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   const int lrow = wave * RPI + lane / CPR;  // row of instruction j: j * 4 * RPI + lrow
   const int src_chunk = swz<BK>(lrow, slot);
 
-  build_tap_table(tab, p.KT, p.KH, p.KW, p.H, p.W, p.Cin);
-  if constexpr (EPI == 2) {
-    for (int t = tid; t < 4 * BN; t += NT) {
-      const int q = t / BN, c = n0 + (t - q * BN);
-      ssl[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
-    }
-  }
   const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long long)p.num_n_tiles * BN * p.Kpad * 2),
                                                      0x00020000);
   // per-thread partial sums of its fixed output chunk column: EPI 1 (sum y, sum y^2) / EPI 2
@@ -530,7 +526,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
 
     // LDS-only barrier: the previous tile's output stores stay in flight (a __syncthreads() would
     // wait for them); the ring's counted vmcnt waits stay exact, older stores only add to the count
-    ring_barrier();  // tap table ready; previous tile's epilogue done with the LDS
+    ring_barrier();  // previous tile's epilogue done with the LDS
 
     auto issue = [&](int kt) {
       bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
@@ -611,6 +607,12 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
         o.y = pack2bf(v[2], v[3]);
         const int col = wc * WN + j * 16 + (lane >> 4) * 4;
         *(uint2*)(Es + row * LDE + col) = o;
+      }
+    }
+    if constexpr (EPI == 2) {
+      for (int t = tid; t < 4 * BN; t += NT) {
+        const int qq = t / BN, c = n0 + (t - qq * BN);
+        ssl[t] = c < p.Cout ? p.bn_ss[qq * p.Cout + c] : 0.f;
       }
     }
     ring_barrier();
@@ -1612,8 +1614,8 @@ template <int BN, int BK, int STAGES, int EPI, int NWM = 2>
 static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
   constexpr int BM = 64 * NWM;
   constexpr size_t ring = (size_t)STAGES * (BM + BN) * BK * 2;
-  constexpr size_t epi = (size_t)BM * (BN + 8) * 2;
-  const size_t lds = (ring > epi ? ring : epi) + 8 * 160 + 16 * BN;
+  constexpr size_t epi = (size_t)BM * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
+  const size_t lds_v3 = ring > epi ? ring : epi;
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>,
@@ -1623,7 +1625,7 @@ static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
   ConvParams q = p;
   q.num_m_tiles = (p.M + BM - 1) / BM;
   const int nblocks = q.num_n_tiles * q.grid_m;
-  hipLaunchKernelGGL((conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>), dim3(nblocks), dim3(128 * NWM), lds, stream, q);
+  hipLaunchKernelGGL((conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>), dim3(nblocks), dim3(128 * NWM), lds_v3, stream, q);
   return (int)hipGetLastError();
 }
 
