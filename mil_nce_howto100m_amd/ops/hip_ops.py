@@ -505,17 +505,22 @@ def _wgrad_tiles(Cout: int) -> List[int]:
 _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
 _W_OCCS = (4, 2)  # split-K occupancy candidates (workgroups per CU)
 _HALO_WGRAD = os.environ.get("MILNCE_HALO_WGRAD", "1") != "0"
-# (3,1,1) is implemented too (csrc/conv_halo.hip) but measures slower than the im2col kernel
-# (3 taps amortise the per-box cost less): tools/halo_bench.py, profiles/r2_halo_wgrad.md
-_HALO_KERNELS = ((1, 3, 3),)
+_HALO_KERNELS = ((1, 3, 3), (3, 1, 1))
+# (3,1,1) is implemented too but measures slower than the im2col kernel (3 taps amortise the
+# per-box cost less: tools/halo_bench.py), so the autotuner only offers the spatial one
+_HALO_TUNED = ((1, 3, 3),)
+
+
+def _halo_wgrad_supported(plan: ConvPlan, x: torch.Tensor) -> bool:
+    """Box-tiled wgrad (csrc/conv_halo.hip) covers stride-1 same-padded (1,3,3) / (3,1,1) convs
+    over bf16 activations."""
+    return (x.dtype == BF16 and plan.k in _HALO_KERNELS and plan.s == (1, 1, 1)
+            and plan.p == tuple(k // 2 for k in plan.k) and not plan.wo_override and plan.Cin % 8 == 0
+            and plan.Cin == plan.Cin_p)
 
 
 def _halo_wgrad_ok(plan: ConvPlan, x: torch.Tensor) -> bool:
-    """Box-tiled wgrad (csrc/conv_halo.hip) covers stride-1 same-padded (1,3,3) / (3,1,1) convs
-    over bf16 activations."""
-    return (_HALO_WGRAD and x.dtype == BF16 and plan.k in _HALO_KERNELS and plan.s == (1, 1, 1)
-            and plan.p == tuple(k // 2 for k in plan.k) and not plan.wo_override and plan.Cin % 8 == 0
-            and plan.Cin == plan.Cin_p)
+    return _HALO_WGRAD and plan.k in _HALO_TUNED and _halo_wgrad_supported(plan, x)
 
 
 _HALO_SPLITS: Dict[Tuple[int, int], Tuple[int, int]] = {}

@@ -32,7 +32,7 @@ def test_halo_wgrad_matches_fp32(shape, cc):
     x = torch.randn(B, T, H, W, Cin, device="cuda").to(torch.bfloat16)
     dy = torch.randn(B, T, H, W, Cout, device="cuda").to(torch.bfloat16)
     plan = h.conv_plan(x.shape, (Cout, Cin) + k, (1, 1, 1), pad)
-    assert h._halo_wgrad_ok(plan, x)
+    assert h._halo_wgrad_supported(plan, x)
     out = torch.full((Cout, Cin) + k, 0.5, device="cuda")
     h._halo_wgrad(dy, x, plan, cc, out, 1)  # accumulate onto 0.5
     ref = torch.nn.grad.conv3d_weight(x.permute(0, 4, 1, 2, 3).float(), (Cout, Cin) + k,
