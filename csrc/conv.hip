@@ -1160,9 +1160,38 @@ constexpr int STW_HR = 2;
 constexpr int STW_KF = 42;           // 672 / 16
 constexpr int STW_KFW = 11;          // K fragments per wave (11, 11, 11, 9)
 
+// 8 uint8 pixel channels (a width pair of RGB0 pixels) -> the same 8 integers as bf16 (exact:
+// 0..255 need 8 significant bits, so the fp32 value's upper half IS the bf16). The stems convert
+// the native clip this way while staging their halo instead of in a separate pass over the clip;
+// the 1/255 scale moves to the other operand / the result (stem_fwd: the LDS weight copy,
+// stem_wgrad: the fp32 partial dW), where it is applied once per workgroup, not per pixel.
+__device__ __forceinline__ uint32_t u8x2_hi_bf16(float a, float b) {
+  return __builtin_amdgcn_perm(__float_as_uint(b), __float_as_uint(a), 0x07060302u);
+}
+__device__ __forceinline__ uint4 u8x8_to_bf16x8(uint2 v) {
+  uint4 o;
+  o.x = u8x2_hi_bf16((float)(v.x & 0xff), (float)((v.x >> 8) & 0xff));
+  o.y = u8x2_hi_bf16((float)((v.x >> 16) & 0xff), (float)(v.x >> 24));
+  o.z = u8x2_hi_bf16((float)(v.y & 0xff), (float)((v.y >> 8) & 0xff));
+  o.w = u8x2_hi_bf16((float)((v.y >> 16) & 0xff), (float)(v.y >> 24));
+  return o;
+}
+
+// one staged halo pixel (8 channels): 16 B of bf16, or 8 B of uint8 converted on the LDS store
+template <bool U8>
+__device__ __forceinline__ auto stem_px_load(__amdgpu_buffer_rsrc_t rs, bool valid, int px) {
+  if constexpr (U8) {
+    const uint32_t off = valid ? (uint32_t)px * 8u : 0x80000000u;  // > num_records: reads 0
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0));
+  } else {
+    const uint32_t off = valid ? (uint32_t)px * 16u : 0x80000000u;
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+  }
+}
+
 struct StemWgradParams {
   const bf16_t* dy;  // [M, 64]
-  const bf16_t* x;   // [B, T, H, W2, 8]
+  const bf16_t* x;   // [B, T, H, W2, 8] bf16 (or uint8 with the U8 kernel)
   float* slab;       // [gridDim][64][672]
   int B, T, H, W2, To, Ho, Wo;
   int nitems;        // B * To * (Ho / HR)
@@ -1181,6 +1210,7 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16_t* a0, const bf16_t* a1) {
 constexpr int STW_HREG = 13;  // halo pixels per thread (<= 3 * 9 * 116 at 224x224)
 constexpr int STW_DREG = 7;   // dY chunks per thread (<= 224 rows x 8 chunks)
 
+template <bool U8>
 __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1195,7 +1225,9 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
 
   // register staging (T14): the next item's halo and dY are loaded into VGPRs while the current
   // item is computed from LDS, then written to the other buffer
-  uint4 hreg[STW_HREG], dreg[STW_DREG];
+  using HReg = typename std::conditional<U8, uint2, uint4>::type;
+  HReg hreg[STW_HREG];
+  uint4 dreg[STW_DREG];
   auto load = [&](int it) {
     const int hg = it % hg_per, q = it / hg_per;
     const int to = q % p.To, b = q / p.To;
@@ -1208,8 +1240,7 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
       const int ti = t0 + tt, hi = h0 + hh, wi = wp - 2;
       const bool v = f < p.halo_px && tt < 3 && (unsigned)ti < (unsigned)p.T && (unsigned)hi < (unsigned)p.H &&
                      (unsigned)wi < (unsigned)p.W2;
-      const uint32_t off = v ? (uint32_t)(((((long long)b * p.T + ti) * p.H + hi) * p.W2 + wi) * 16) : 0x80000000u;
-      hreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      hreg[i] = stem_px_load<U8>(xrs, v, ((b * p.T + ti) * p.H + hi) * p.W2 + wi);
     }
     const long long m0 = ((long long)(b * p.To + to) * p.Ho + hg * STW_HR) * p.Wo;
     const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + m0 * 64), (short)0, real_rows * 128, 0x00020000);
@@ -1224,7 +1255,11 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
 #pragma unroll
     for (int i = 0; i < STW_HREG; ++i) {
       const int f = tid + 256 * i;
-      if (f < p.halo_px) *(uint4*)(base + f * 8) = hreg[i];
+      if constexpr (U8) {  // integer-valued bf16; the 1/255 is applied to the partial dW
+        if (f < p.halo_px) *(uint4*)(base + f * 8) = u8x8_to_bf16x8(hreg[i]);
+      } else {
+        if (f < p.halo_px) *(uint4*)(base + f * 8) = hreg[i];
+      }
     }
     bf16_t* D = base + p.halo_px * 8;
 #pragma unroll
@@ -1317,7 +1352,8 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
       if (kf < STW_KF) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          out[(long long)(nf * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] = acc[nf][j][r];
+          out[(long long)(nf * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] =
+              U8 ? acc[nf][j][r] * (1.0f / 255.0f) : acc[nf][j][r];
       }
     }
 }
@@ -1344,7 +1380,7 @@ struct StemFwdParams {
   long long x_bytes;
 };
 
-template <int W2>
+template <int W2, bool U8>
 __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   constexpr int HR = STW_HR, WO = W2, WPX = W2 + 4, HROWS = 2 * HR + 5;
   constexpr int HALO = 3 * HROWS * WPX;
@@ -1364,14 +1400,32 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, 0x00020000);
   const int hg_per = p.Ho / HR;
 
-  // weight -> LDS (once)
+  // weight -> LDS (once); for the uint8 clip (integer-valued bf16 halo) scaled by 1/255 here
   for (int c = tid; c < 64 * 84; c += 256) {
     const int n = c / 84, k8 = c - n * 84;
-    *(uint4*)(Ws + n * STF_LDW + k8 * 8) = *(const uint4*)(p.w + (long long)n * p.Kpad + k8 * 8);
+    uint4 wv = *(const uint4*)(p.w + (long long)n * p.Kpad + k8 * 8);
+    if constexpr (U8) {
+      float f[8];
+      unpack8(wv, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= 1.0f / 255.0f;
+      wv = pack8(f);
+    }
+    *(uint4*)(Ws + n * STF_LDW + k8 * 8) = wv;
   }
   if (tid < 128) red[tid] = 0.f;
 
-  uint4 hreg[HREG];
+  using HReg = typename std::conditional<U8, uint2, uint4>::type;
+  HReg hreg[HREG];
+  // uint8 clip: converted (integer-valued bf16) part-way through the current item's K loop, where
+  // the VALU work issues between MFMAs and the prefetch has had time to land; store() copies
+  uint4 hcv[U8 ? HREG : 1];
+  auto convert = [&]() {
+    if constexpr (U8) {
+#pragma unroll
+      for (int i = 0; i < HREG; ++i) hcv[i] = u8x8_to_bf16x8(hreg[i]);
+    }
+  };
   // item-invariant part of this thread's halo pixels: (tt, hh, wp) packed, -1 past the halo
   int hgeo[HREG];
 #pragma unroll
@@ -1392,15 +1446,18 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
       const int tt = gq & 3, hh = (gq >> 2) & 63, wp = gq >> 8;
       const bool v = gq >= 0 && (unsigned)(t0 + tt) < (unsigned)p.T && (unsigned)(h0 + hh) < (unsigned)p.H &&
                      (unsigned)(wp - 2) < (unsigned)W2;
-      const uint32_t off = v ? (uint32_t)((base + (tt * p.H + hh) * W2 + wp) * 16) : 0x80000000u;
-      hreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      hreg[i] = stem_px_load<U8>(xrs, v, base + (tt * p.H + hh) * W2 + wp);
     }
   };
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < HREG; ++i) {
       const int f = tid + 256 * i;
-      if (f < HALO) *(uint4*)(X + f * 8) = hreg[i];
+      if constexpr (U8) {
+        if (f < HALO) *(uint4*)(X + f * 8) = hcv[i];
+      } else {
+        if (f < HALO) *(uint4*)(X + f * 8) = hreg[i];
+      }
     }
   };
 
@@ -1433,6 +1490,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   int it = blockIdx.x;
   if (it < p.nitems) {
     load(it);
+    convert();
     store();
   }
   if (it + (int)gridDim.x < p.nitems) load(it + gridDim.x);
@@ -1445,8 +1503,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
       for (int j = 0; j < PFW; ++j) acc[nf][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 21; ++ks) {
-      constexpr int dummy = 0;
-      (void)dummy;
+      if (U8 && ks == 12 && it + (int)gridDim.x < p.nitems) convert();
       const int dt = ks / 7, dh = ks % 7;
       const uint32_t boff = (uint32_t)(((dt * HROWS + dh) * WPX) * 16);
       bf16x8 af[2], bf[PFW];
@@ -1506,17 +1563,17 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   if (tid < 128) p.stats[(long long)blockIdx.x * 128 + tid] = red[tid];
 }
 
-template <int W2>
+template <int W2, bool U8>
 static int launch_stem_fwd(StemFwdParams& p, int grid, hipStream_t stream) {
   constexpr int HALO = 3 * (2 * STW_HR + 5) * (W2 + 4);
   const size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + 128 * 4;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_fwd_kernel<W2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_fwd_kernel<W2, U8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL(stem_fwd_kernel<W2>, dim3(grid), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((stem_fwd_kernel<W2, U8>), dim3(grid), dim3(256), lds, stream, p);
   return (int)hipGetLastError();
 }
 
@@ -1839,9 +1896,10 @@ MILNCE_API int milnce_pack_weight(const float* w, void* out, int Cout, int Cin, 
 }
 
 // Stem wgrad (see stem_wgrad_kernel): dW2 [64][8][3][7][4] (accumulated if `accumulate`).
+// x2 is the bf16 clip as width pairs [B,T,H,W2,8], or (x_u8) the native uint8 clip read the same way.
 // Returns hipErrorInvalidValue for geometries it does not cover (caller falls back).
-MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, float* slab, long long slab_floats, float* dw,
-                                 int B, int T, int H, int W2, int accumulate, hipStream_t stream) {
+MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float* slab, long long slab_floats,
+                                 float* dw, int B, int T, int H, int W2, int accumulate, hipStream_t stream) {
   StemWgradParams p;
   p.dy = (const bf16_t*)dy; p.x = (const bf16_t*)x2; p.slab = slab;
   p.B = B; p.T = T; p.H = H; p.W2 = W2;
@@ -1853,21 +1911,24 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, float* slab, lo
   p.halo_px = 3 * (2 * STW_HR + 5) * (W2 + 4);
   if (p.halo_px > 256 * STW_HREG || STW_HR * p.Wo > 32 * STW_DREG) return (int)hipErrorInvalidValue;
   p.dy_rows = (STW_HR * p.Wo + 31) / 32 * 32;
-  p.x_bytes = (long long)B * T * H * W2 * 16;
+  p.x_bytes = (long long)B * T * H * W2 * (x_u8 ? 8 : 16);
   p.dy_bytes = (long long)B * p.To * p.Ho * p.Wo * 128;
   if (p.x_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
   const size_t lds = (size_t)2 * (p.halo_px + p.dy_rows * 8) * 16;
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024));
     attr_set = true;
   }
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
   if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(stem_wgrad_kernel, dim3(grid), dim3(256), lds, stream, p);
+  if (x_u8) hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(256), lds, stream, p);
+  else hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(grid), dim3(256), lds, stream, p);
   HIP_RET(hipGetLastError());
   const long long total = 64LL * 672;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, slab, dw, grid,
@@ -1876,9 +1937,10 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, float* slab, lo
 }
 
 // Stem forward (see stem_fwd_kernel): y [M, 64] bf16 and BN partials stats[nparts][2][64];
+// x2 as for milnce_stem_wgrad (bf16, or uint8 scaled by 1/255 while staged);
 // returns the number of partial rows written (> 0), or a negative value for geometries it does
 // not cover (the caller falls back to the generic implicit GEMM).
-MILNCE_API int milnce_stem_fwd(const void* x2, const void* wpacked, int Kpad, void* y, float* stats,
+MILNCE_API int milnce_stem_fwd(const void* x2, int x_u8, const void* wpacked, int Kpad, void* y, float* stats,
                                long long stats_floats, int B, int T, int H, int W2, hipStream_t stream) {
   StemFwdParams p;
   p.x = (const bf16_t*)x2; p.w = (const bf16_t*)wpacked; p.y = (bf16_t*)y; p.stats = stats;
@@ -1887,15 +1949,15 @@ MILNCE_API int milnce_stem_fwd(const void* x2, const void* wpacked, int Kpad, vo
   p.Ho = (H + 6 - 7) / 2 + 1;
   if (p.Ho % STW_HR || Kpad < 672) return -1;
   p.nitems = B * p.To * (p.Ho / STW_HR);
-  p.x_bytes = (long long)B * T * H * W2 * 16;
+  p.x_bytes = (long long)B * T * H * W2 * (x_u8 ? 8 : 16);
   if (p.x_bytes > 0x7FFFFFF0LL) return -1;
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
   if ((long long)grid * 128 > stats_floats) return -1;
   int rc;
-  if (W2 == 100) rc = launch_stem_fwd<100>(p, grid, stream);
-  else if (W2 == 112) rc = launch_stem_fwd<112>(p, grid, stream);
-  else if (W2 == 32) rc = launch_stem_fwd<32>(p, grid, stream);
+  if (W2 == 100) rc = x_u8 ? launch_stem_fwd<100, true>(p, grid, stream) : launch_stem_fwd<100, false>(p, grid, stream);
+  else if (W2 == 112) rc = x_u8 ? launch_stem_fwd<112, true>(p, grid, stream) : launch_stem_fwd<112, false>(p, grid, stream);
+  else if (W2 == 32) rc = x_u8 ? launch_stem_fwd<32, true>(p, grid, stream) : launch_stem_fwd<32, false>(p, grid, stream);
   else return -1;
   return rc ? -rc - 1000 : grid;
 }

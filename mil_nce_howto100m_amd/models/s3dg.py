@@ -204,8 +204,9 @@ class S3D(nn.Module):
 
         Accepted: reference float ``[B,3,T,H,W]`` in [0,1]; uint8 ``[B,3,T,H,W]`` (raw loader
         output); native uint8 ``[B,T,H,W,4]`` (RGB + zero pad channel, from the synthetic
-        generator). GPU stem input: bf16 ``[B,T,H,W,4]`` (channel 3 zero, read as width pairs by
-        the stem); CPU: float ``[B,T,H,W,3]``.
+        generator). GPU stem input: ``[B,T,H,W,4]`` (channel 3 zero, read as width pairs by the
+        stem), uint8 for uint8 clips (the stem kernels scale by 1/255 while staging) else bf16;
+        CPU: float ``[B,T,H,W,3]``.
         """
         native = video.dim() == 5 and video.shape[-1] == 4 and video.shape[1] != 3
         if video.is_cuda and ops.use_hip(video) and not self.space_to_depth:

@@ -551,10 +551,10 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     acc = int(out is not None)
     dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
-    if _STEM_WGRAD and _is_paired_stem(plan) and x.dtype == BF16:
+    if _STEM_WGRAD and _is_paired_stem(plan) and x.dtype in (BF16, torch.uint8):
         slab = torch.empty((256 * 64 * 672,), dtype=F32, device=dy.device)
-        rc = lib().milnce_stem_wgrad(ptr(dy), ptr(x), ptr(slab), slab.numel(), ptr(dw), plan.B, plan.T, plan.H,
-                                     plan.W, acc, stream())
+        rc = lib().milnce_stem_wgrad(ptr(dy), ptr(x), int(x.dtype == torch.uint8), ptr(slab), slab.numel(), ptr(dw),
+                                     plan.B, plan.T, plan.H, plan.W, acc, stream())
         if rc == 0:
             return dw
 
@@ -604,12 +604,12 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     wp = _pack(weight, plan, 0)
     nparts = plan.grid_m
     y = None
-    if _STEM_FWD and _is_paired_stem(plan) and x.dtype == BF16:
+    if _STEM_FWD and _is_paired_stem(plan) and x.dtype in (BF16, torch.uint8):
         # halo-tiled stem kernel (csrc/conv.hip stem_fwd_kernel); its statistics rows are per workgroup
         y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=dev)
         stats = torch.empty((256 * 128,), dtype=F32, device=dev)
-        rc = lib().milnce_stem_fwd(ptr(x), ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
-                                   plan.H, plan.W, stream())
+        rc = lib().milnce_stem_fwd(ptr(x), int(x.dtype == torch.uint8), ptr(wp), plan.Kpad, ptr(y), ptr(stats),
+                                   stats.numel(), plan.B, plan.T, plan.H, plan.W, stream())
         if rc > 0:
             nparts = rc
         else:
@@ -802,8 +802,9 @@ def stem_conv_bn_relu_pool(x, weight, bn, training: bool, pool_k, pool_s):
     """The stem unit followed by its TF-SAME max pool (maxpool_2a), fused: see
     ``_ConvBNReLUPool`` and ``stem_conv_bn_relu``."""
     B, T, H, W, C = x.shape
-    if C != 4 or W % 2 or tuple(weight.shape) != (64, 3, 3, 7, 7) or x.dtype != BF16:
-        raise ValueError(f"stem expects bf16 [B,T,H,W even,4] and a (64,3,3,7,7) weight, got {tuple(x.shape)}")
+    if C != 4 or W % 2 or tuple(weight.shape) != (64, 3, 3, 7, 7) or x.dtype not in (BF16, torch.uint8):
+        raise ValueError(f"stem expects bf16/uint8 [B,T,H,W even,4] and a (64,3,3,7,7) weight, got "
+                         f"{tuple(x.shape)} {x.dtype}")
     idx, mask = _stem_pair_map(x.device)
     cout = weight.shape[0]
     w2 = (weight.reshape(cout, -1).index_select(1, idx) * mask).view(cout, 8, 3, 7, 4)
@@ -816,13 +817,15 @@ def stem_conv_bn_relu_pool(x, weight, bn, training: bool, pool_k, pool_s):
 
 
 def stem_conv_bn_relu(x, weight, bn, training: bool):
-    """S3D-G conv1 (``s3dg.py:226``: 3->64, k (3,7,7), s 2, p (1,3,3)) + BN + ReLU on the bf16
-    clip ``[B,T,H,W,4]`` (channel 3 zero) via the paired-width formulation above."""
+    """S3D-G conv1 (``s3dg.py:226``: 3->64, k (3,7,7), s 2, p (1,3,3)) + BN + ReLU on the clip
+    ``[B,T,H,W,4]`` (channel 3 zero) via the paired-width formulation above. The clip is bf16, or
+    the native uint8 clip, which the stem kernels scale by 1/255 while staging it (no separate
+    conversion pass)."""
     B, T, H, W, C = x.shape
     if C != 4 or W % 2 or tuple(weight.shape) != (64, 3, 3, 7, 7):
         raise ValueError(f"stem expects [B,T,H,W even,4] bf16 and a (64,3,3,7,7) weight, got {tuple(x.shape)}")
-    if x.dtype != BF16:
-        raise TypeError("stem input must be bf16 (see prepare_stem_input)")
+    if x.dtype not in (BF16, torch.uint8):
+        raise TypeError("stem input must be bf16 or uint8 (see prepare_stem_input)")
     idx, mask = _stem_pair_map(x.device)
     cout = weight.shape[0]
     w2 = (weight.reshape(cout, -1).index_select(1, idx) * mask).view(cout, 8, 3, 7, 4)
@@ -1482,15 +1485,23 @@ def synth_video(labels_i32, ids_i32, T, S, seed):
     return out
 
 
-def prepare_stem_input(video, native: bool):
-    """Any accepted clip format -> the stem's bf16 ``[B,T,H,W,4]`` operand (values /255 for
-    uint8 input; channel 3 zero). Native clips are uint8 ``[B,T,H,W,4]`` already."""
+_STEM_U8 = os.environ.get("MILNCE_STEM_U8", "1") != "0"
+
+
+def prepare_stem_input(video, native: bool, keep_u8: Optional[bool] = None):
+    """Any accepted clip format -> the stem's ``[B,T,H,W,4]`` operand (channel 3 zero).
+    uint8 clips stay uint8 (``keep_u8``, default on): the stem kernels convert them (x/255 in
+    bf16) while staging their halo, so the clip is never materialised in bf16. Otherwise the
+    result is bf16 (values /255 for uint8). Native clips are uint8 ``[B,T,H,W,4]`` already."""
+    keep_u8 = _STEM_U8 if keep_u8 is None else keep_u8
     if native:
         v = video.contiguous()
         if v.dtype == BF16:
             return v
         if v.dtype != torch.uint8:
             return v.to(BF16)
+        if keep_u8:
+            return v
     else:
         B, C, T, H, W = video.shape
         assert C == 3
@@ -1498,6 +1509,8 @@ def prepare_stem_input(video, native: bool):
         if video.dtype == torch.uint8:
             v = torch.empty((B, T, H, W, 4), dtype=torch.uint8, device=video.device)
             call("milnce_stem_prep", ptr(video), 0, B, T, H, W, ptr(v), stream())
+            if keep_u8:
+                return v
         else:
             if video.dtype not in (F32, BF16):
                 video = video.float()

@@ -458,8 +458,11 @@ def test_synth_video_matches_torch():
 def test_stem_prep_reference_layout():
     h = hip()
     v = torch.randint(0, 256, (2, 3, 4, 6, 6), dtype=torch.uint8, device=DEV)
-    o = h.prepare_stem_input(v, native=False)
+    o = h.prepare_stem_input(v, native=False, keep_u8=False)
     assert o.shape == (2, 4, 6, 6, 4) and o.dtype == torch.bfloat16
+    ou = h.prepare_stem_input(v, native=False, keep_u8=True)
+    assert ou.dtype == torch.uint8 and torch.equal(ou[..., :3], v.permute(0, 2, 3, 4, 1))
+    assert int(ou[..., 3].sum()) == 0
     ref = (v.permute(0, 2, 3, 4, 1).float() / 255.0).to(torch.bfloat16)
     assert torch.equal(o[..., :3], ref)
     assert int(o[..., 3].float().abs().sum()) == 0
@@ -476,7 +479,7 @@ def test_paired_width_stem(S):
     B, T = 2, 6
     u8 = torch.randint(0, 256, (B, T, S, S, 4), dtype=torch.uint8, device=DEV)
     u8[..., 3] = 0
-    x = h.prepare_stem_input(u8, native=True)
+    x = h.prepare_stem_input(u8, native=True, keep_u8=False)
     conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
     bn = nn.BatchNorm3d(64).to(DEV)
     bn_ref = nn.BatchNorm3d(64).to(DEV)
@@ -501,7 +504,7 @@ def test_stem_bn_relu_pool_fused_matches_unfused():
     h = hip()
     u8 = torch.randint(0, 256, (2, 6, 24, 24, 4), dtype=torch.uint8, device=DEV)
     u8[..., 3] = 0
-    x = h.prepare_stem_input(u8, native=True)
+    x = h.prepare_stem_input(u8, native=True, keep_u8=False)
     conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
     bns = [nn.BatchNorm3d(64).to(DEV) for _ in range(2)]
     bns[1].load_state_dict(bns[0].state_dict())
@@ -517,6 +520,52 @@ def test_stem_bn_relu_pool_fused_matches_unfused():
     assert rel_err(bns[0].weight.grad, bns[1].weight.grad) < 1e-3
     assert rel_err(bns[0].bias.grad, bns[1].bias.grad) < 1e-3
     assert torch.equal(bns[0].running_mean, bns[1].running_mean)
+
+
+@pytest.mark.parametrize("S,fused", [(64, True), (64, False), (20, False), (200, True)])
+def test_stem_uint8_input(S, fused):
+    """The stem on the native uint8 clip (no bf16 copy of the clip: the kernels stage it as
+    integer-valued bf16 and apply the 1/255 to the LDS weight copy / the fp32 partial dW) ==
+    the stem on the bf16 clip x/255 up to bf16 rounding: output, BN statistics, weight grad.
+    S 64 / 200 run the halo-tiled stem kernels (W2 32 / 100), S 20 the generic implicit GEMM
+    (uint8 operand scaled by 1/255 on its LDS store)."""
+    torch.manual_seed(12)
+    h = hip()
+    B, T = 2, 4
+    u8 = torch.randint(0, 256, (B, T, S, S, 4), dtype=torch.uint8, device=DEV)
+    u8[..., 3] = 0
+    xu = h.prepare_stem_input(u8, native=True, keep_u8=True)
+    xb = h.prepare_stem_input(u8, native=True, keep_u8=False)
+    assert xu.dtype == torch.uint8 and xb.dtype == torch.bfloat16
+    conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
+    bns = [nn.BatchNorm3d(64).to(DEV) for _ in range(2)]
+    bns[1].load_state_dict(bns[0].state_dict())
+    ws = [conv.weight.detach().clone().requires_grad_(True) for _ in range(2)]
+    outs = []
+    for x, w, bn in zip((xu, xb), ws, bns):
+        if fused:
+            outs.append(h.stem_conv_bn_relu_pool(x, w, bn, True, (1, 3, 3), (1, 2, 2)))
+        else:
+            outs.append(h.stem_conv_bn_relu(x, w, bn, True))
+    assert rel_err(outs[0], outs[1]) < 1e-2
+    assert torch.allclose(bns[0].running_var, bns[1].running_var, rtol=1e-2, atol=1e-4)
+    assert torch.allclose(bns[0].running_mean, bns[1].running_mean, rtol=1e-2, atol=1e-4)
+    # weight gradient kernels on the same dY (through BN backward the bf16 rounding differences
+    # of the two forwards are amplified by the mean/variance cancellation; compare the wgrad itself)
+    x2u, x2b = xu.view(B, T, S, S // 2, 8), xb.view(B, T, S, S // 2, 8)
+    plan = h.conv_plan(x2u.shape, (64, 8, 3, 7, 4), (2, 2, 1), (1, 3, 2), S // 2)
+    dy = torch.randn((plan.B, plan.To, plan.Ho, plan.Wo, 64), device=DEV).to(torch.bfloat16)
+    dwu, dwb = h.conv_wgrad(dy, x2u, plan), h.conv_wgrad(dy, x2b, plan)
+    # fp32 reference: the paired conv has W2 + 1 output columns, the stem keeps W2 (zero dY column)
+    dyf = F.pad(dy.float().permute(0, 4, 1, 2, 3), (0, 1))
+    ref = torch.nn.grad.conv3d_weight((u8.float() / 255.0).view(B, T, S, S // 2, 8).permute(0, 4, 1, 2, 3),
+                                      (64, 8, 3, 7, 4), dyf, (2, 2, 1), (1, 3, 2))
+    assert rel_err(dwu, ref) < 1e-2 and rel_err(dwb, ref) < 1e-2
+    assert rel_err(dwu, dwb) < 5e-3
+    g = torch.randn_like(outs[0].float()).to(torch.bfloat16)
+    for o in outs:
+        o.backward(g)
+    assert torch.isfinite(ws[0].grad).all()
 
 
 @pytest.mark.parametrize("dist", ["cosine", "negative_dot", None])
@@ -652,7 +701,7 @@ def test_stem_fwd_halo_kernel(B, T, S):
     wp = h._pack(w2, plan, 0)
     y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, 64), dtype=torch.bfloat16, device=DEV)
     stats = torch.empty((256 * 128,), device=DEV)
-    n = lib().milnce_stem_fwd(ptr(x2), ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
+    n = lib().milnce_stem_fwd(ptr(x2), 0, ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
                               plan.H, plan.W, stream())
     assert n > 0
     xr = x2.float().permute(0, 4, 1, 2, 3)
