@@ -64,6 +64,10 @@ def main():
     agg_bytes = 0.0
     for k, t in sorted(dur.items(), key=lambda kv: -kv[1])[:a.top]:
         mf = avg(k, "MfmaUtil")
+        busy, grbm = ctr[k].get("SQ_VALU_MFMA_BUSY_CYCLES"), ctr[k].get("GRBM_GUI_ACTIVE")
+        if mf is None and busy is not None and grbm:
+            # busy cycles summed over SIMDs / (GPU-active cycles per XCD x 256 CUs x 4 SIMDs)
+            mf = 100.0 * busy / (grbm / 8 * 256 * 4)
         bc, li = ctr[k].get("SQ_LDS_BANK_CONFLICT"), ctr[k].get("SQ_LDS_IDX_ACTIVE")
         conf = bc / li if bc is not None and li else None
         fb = ctr[k].get("FETCH_SIZE", 0.0) + ctr[k].get("WRITE_SIZE", 0.0)   # KiB over the step
