@@ -453,6 +453,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   // workgroups per CU at BN 192 x BK 64 x 2 stages, i.e. two waves per SIMD)
   constexpr int SSL_BYTES = EPI == 2 ? 16 * BN : 0;
   static_assert(A_INST >= 1 && B_INST >= 1, "tile too small for the DMA mapping");
+  static_assert(BM % (RPI * NWAVES) == 0 && BN % (RPI * NWAVES) == 0, "tile rows must split evenly over the DMAs");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* ring = (bf16_t*)smem;  // stage s: A [BM][BK] then B [BN][BK]
@@ -1697,13 +1698,22 @@ static int launch_v3_epi(ConvParams& p, hipStream_t stream) {
 }
 
 //   6: 256-row tiles (8 waves), BK as planned, 3 stages; 7: same, 2 stages.
+// A variant exists for an N tile only if its B rows split evenly into the 1-KiB DMA pieces of
+// all waves (rows per piece 512 / BK, times the wave count); other requests run variant 3.
+template <int BN, int BK, int NWAVES>
+constexpr bool v3_fits() { return BN % ((512 / BK) * NWAVES) == 0; }
+
 template <int BN, int BK>
 static int launch_v3_impl(ConvParams& p, int impl, hipStream_t stream) {
-  if constexpr (BN * BK >= 64 * 64) {  // >= one 1-KiB DMA piece of B per wave with 8 waves
+  if constexpr (v3_fits<BN, BK, 8>()) {
     if (impl == 7) return launch_v3_epi<BN, BK, 2, 4>(p, stream);
-    if (impl == 6) return launch_v3_epi<BN, BK, 3, 4>(p, stream);
+    if constexpr (3 * (256 + BN) * BK * 2 <= 160 * 1024) {  // 3-stage ring within the LDS
+      if (impl == 6) return launch_v3_epi<BN, BK, 3, 4>(p, stream);
+    }
   }
-  if (impl == 5) return launch_v3_epi<BN, 32, 4>(p, stream);
+  if constexpr (v3_fits<BN, 32, 4>()) {
+    if (impl == 5) return launch_v3_epi<BN, 32, 4>(p, stream);
+  }
   if (impl == 4) return launch_v3_epi<BN, BK, 2>(p, stream);
   return launch_v3_epi<BN, BK, 3>(p, stream);
 }
@@ -1758,7 +1768,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
     // wide / odd N tiles: LDS-DMA ring variants only, BK 64
     if (bk != 64) return (int)hipErrorInvalidValue;
-    const int im = impl == 3 ? 3 : 4;
+    const int im = impl >= 3 ? impl : 4;
     if (bn == 96) return launch_v3_impl<96, 64>(p, im, stream);
     if (bn == 160) return launch_v3_impl<160, 64>(p, im, stream);
     return launch_v3_impl<192, 64>(p, im, stream);

@@ -802,8 +802,15 @@ __device__ __forceinline__ S1Geo s1_geo(const PoolParams& p, int G, int nchunk) 
   return s;
 }
 
+// Buffer descriptor of a workgroup-uniform range. The operands are passed through readfirstlane:
+// the compiler cannot always prove them uniform (then it wraps EVERY buffer access in a
+// readfirstlane "waterfall" loop, which also defeats the counted vmcnt waits of the sweeps).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t clip_rsrc(const void* base, int nbytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, nbytes, 0x00020000);
+  const unsigned long long a = (unsigned long long)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  void* ub = (void*)(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, __builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
 }
 
 __device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t rs, uint32_t byte_off) {
@@ -835,6 +842,9 @@ __device__ __forceinline__ void max3(const float* a, bool va, const float* b, bo
   }
 }
 
+constexpr int S1_PF = 8;  // forward sweep: register ring of input columns (6 loads in flight)
+
+template <int WT>  // WT = W when specialised (the sweep is then fully unrolled), 0 = runtime W
 __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, int nchunk, const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
   extern __shared__ uint4 s1_lds[];  // m1 [rows+1][G], m2 [rows+1][G] (bf16 x 8); row `rows`: idle lanes
@@ -854,37 +864,48 @@ __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, i
   const int ihm = vhm ? me - G : me, ihp = vhp ? me + G : me;
   const int itm = vtm ? me - p.H * G : me, itp = vtp ? me + p.H * G : me;
   auto col = [&](int w) { return (w >= 0 && w < p.W) ? (s.e0 + (uint32_t)w * ecol) : oob; };
-  uint4 xp = make_uint4(0, 0, 0, 0), xc = bld16(xr, col(0) * 2), xn = bld16(xr, col(1) * 2);
-  for (int w = 0; w < p.W; ++w) {
-    const uint4 xnn = bld16(xr, col(w + 2) * 2);  // prefetch
-    float fa[8], fb[8], fc[8], m1[8], m2[8], o[8];
-    uint32_t cw[8], ch[8], ct[8];
-    unpack8(xp, fa);
-    unpack8(xc, fb);
-    unpack8(xn, fc);
-    max3(fa, w > 0, fb, true, fc, w + 1 < p.W, m1, cw);
-    m1s[me] = pack8(m1);  // exact: maxima of bf16 values
-    lds_barrier();
-    unpack8(m1s[ihm], fa);
-    unpack8(m1s[ihp], fc);
-    max3(fa, vhm, m1, true, fc, vhp, m2, ch);
-    m2s[me] = pack8(m2);
-    lds_barrier();
-    unpack8(m2s[itm], fa);
-    unpack8(m2s[itp], fc);
-    max3(fa, vtm, m2, true, fc, vtp, o, ct);
-    const uint32_t off = col(s.active ? w : -1);
-    bst16(yr, off * 2, pack8(o));
-    uint32_t cb[8];
+  // register ring of input columns, slot = column % S1_PF (column -1 reads as zeros): the loop is
+  // unrolled by the ring size so a pending load is never copied between registers (a copy would
+  // make the compiler wait for it), i.e. S1_PF - 2 columns stay in flight across the barriers
+  uint4 ring[S1_PF];
+  ring[S1_PF - 1] = make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) cb[k] = cw[k] | (ch[k] << 2) | (ct[k] << 4);
-    uint2 a;
-    a.x = cb[0] | (cb[1] << 8) | (cb[2] << 16) | (cb[3] << 24);
-    a.y = cb[4] | (cb[5] << 8) | (cb[6] << 16) | (cb[7] << 24);
-    bst8(ar, off, a);
-    xp = xc;
-    xc = xn;
-    xn = xnn;
+  for (int k = 0; k < S1_PF - 1; ++k) ring[k] = bld16(xr, col(k) * 2);
+  const int W = WT > 0 ? WT : p.W;
+#pragma unroll
+  for (int w0 = 0; w0 < W; w0 += S1_PF) {
+#pragma unroll
+    for (int u = 0; u < S1_PF; ++u) {
+      const int w = w0 + u;
+      if (w >= W) break;
+      const int sp = (u + S1_PF - 1) % S1_PF, sc = u, sn = (u + 1) % S1_PF;
+      float fa[8], fb[8], fc[8], m1[8], m2[8], o[8];
+      uint32_t cw[8], ch[8], ct[8];
+      unpack8(ring[sp], fa);
+      unpack8(ring[sc], fb);
+      unpack8(ring[sn], fc);
+      ring[sp] = bld16(xr, col(w - 1 + S1_PF) * 2);  // column w-1's slot takes column w-1+S1_PF
+      max3(fa, w > 0, fb, true, fc, w + 1 < W, m1, cw);
+      m1s[me] = pack8(m1);  // exact: maxima of bf16 values
+      lds_barrier();
+      unpack8(m1s[ihm], fa);
+      unpack8(m1s[ihp], fc);
+      max3(fa, vhm, m1, true, fc, vhp, m2, ch);
+      m2s[me] = pack8(m2);
+      lds_barrier();
+      unpack8(m2s[itm], fa);
+      unpack8(m2s[itp], fc);
+      max3(fa, vtm, m2, true, fc, vtp, o, ct);
+      const uint32_t off = col(s.active ? w : -1);
+      bst16(yr, off * 2, pack8(o));
+      uint32_t cb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) cb[k] = cw[k] | (ch[k] << 2) | (ct[k] << 4);
+      uint2 a;
+      a.x = cb[0] | (cb[1] << 8) | (cb[2] << 16) | (cb[3] << 24);
+      a.y = cb[4] | (cb[5] << 8) | (cb[6] << 16) | (cb[7] << 24);
+      bst8(ar, off, a);
+    }
   }
 }
 
@@ -896,6 +917,7 @@ __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, i
 // otherwise): acc_in  dx += acc_in (the other gradient of the pool input: the Inception 1x1
 // GEMM's dX); x, gs  gs[b, c] = sum_thw dx * x (the SelfGating reduction of the block that
 // produced x, from the final bf16 dx), written directly (the workgroup owns the plane).
+template <int WT>
 __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, int nchunk,
                                                           const bf16_t* __restrict__ dy,
                                                           const uint8_t* __restrict__ arg,
@@ -925,13 +947,14 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
   auto code = [](const uint2& a, int k, int sh) {
     return ((((k < 4 ? a.x : a.y) >> (8 * (k & 3))) >> sh) & 3u);
   };
+  const int W = WT > 0 ? WT : p.W;
   float sacc[8], dA[8], dB[8];  // dm1 of columns wo-2 (A), wo-1 (B)
   uint2 cA = make_uint2(0, 0), cB = make_uint2(0, 0);
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sacc[k] = 0.f; dA[k] = 0.f; dB[k] = 0.f; }
   uint4 gcur = bld16(dyr, col(0) * 2);
   uint2 acur = bld8(agr, col(0));
-  for (int wo = 0; wo <= p.W; ++wo) {
+  for (int wo = 0; wo <= W; ++wo) {
     // emit operands of column wo-1 first, then the next column's gradient and codes
     const uint32_t ep = col(wo - 1);
     const uint4 ein = bld16(inr, ep * 2), xin = bld16(xr, ep * 2);
@@ -939,7 +962,7 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
     const uint2 anext = bld8(agr, col(wo + 1));
     float dC[8];  // dm1 of column wo
     uint2 cC = acur;
-    if (wo < p.W) {
+    if (wo < W) {
       const int buf = (wo & 1) * n;
       dys[buf + me] = gcur;
       cds[buf + me] = acur;
@@ -1044,13 +1067,41 @@ static size_t s1_fwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 32; 
 static size_t s1_bwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 80; }
 
 // Stride-1 pool implementation: 1 = LDS plane sweeps (default), 0 = global-memory sliding
-// kernels (A/B benchmarks only; milnce_set_pool_s1_impl).
+// kernels (A/B benchmarks only; milnce_set_pool_s1_impl). A tiled forward (band + halo rows in
+// LDS, one barrier, all loads in flight) measured 1.6-2.4 TB/s against the sweep's 2.6-3.4: its
+// h stage is recomputed per t and the VALU work, not memory, bound it (tools/ew_bench.py).
 static int g_s1_impl = 1;
+static int g_s1_maxthr = 512;  // workgroup size cap of the plane sweeps (G = cap / rows groups)
+MILNCE_API int milnce_set_pool_s1_maxthr(int n) {
+  const int old = g_s1_maxthr;
+  if (n >= 64 && n <= 1024) g_s1_maxthr = n;
+  return old;
+}
 static bool s1_use_lds(const PoolParams& p) { return g_s1_impl == 1 && p.T * p.H <= 512; }
 MILNCE_API int milnce_set_pool_s1_impl(int impl) {
   const int old = g_s1_impl;
   g_s1_impl = impl;
   return old;
+}
+
+// the sweeps, fully unrolled for the S3D-G widths (56 / 28 / 14 / 7 at 224 input; 25 / 13 / 7 at 200)
+template <typename... A>
+static void launch_s1_fwd(int W, dim3 grid, dim3 block, size_t lds, hipStream_t s, A... args) {
+  switch (W) {
+    case 25: hipLaunchKernelGGL((maxpool_s1_fwd_sep<25>), grid, block, lds, s, args...); break;
+    case 28: hipLaunchKernelGGL((maxpool_s1_fwd_sep<28>), grid, block, lds, s, args...); break;
+    case 13: hipLaunchKernelGGL((maxpool_s1_fwd_sep<13>), grid, block, lds, s, args...); break;
+    case 14: hipLaunchKernelGGL((maxpool_s1_fwd_sep<14>), grid, block, lds, s, args...); break;
+    case 7: hipLaunchKernelGGL((maxpool_s1_fwd_sep<7>), grid, block, lds, s, args...); break;
+    default: hipLaunchKernelGGL((maxpool_s1_fwd_sep<0>), grid, block, lds, s, args...);
+  }
+}
+// (the backward keeps its runtime-W loop: unrolled or with deeper register rings its carried
+// columns exceed the VGPR budget and it ran 25 % slower; tools/ew_bench.py)
+template <typename... A>
+static void launch_s1_bwd(int W, dim3 grid, dim3 block, size_t lds, hipStream_t s, A... args) {
+  (void)W;
+  hipLaunchKernelGGL((maxpool_s1_bwd_sep<0>), grid, block, lds, s, args...);
 }
 
 static int s1_threads(int rows, int G) {
@@ -1101,9 +1152,9 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
   }
   if (is_s1_333(p) && s1_use_lds(p)) {
     const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
-    const int rows = p.T * p.H, G = s1_groups(rows, p.C, 512, B), nchunk = (p.C / 8 + G - 1) / G;
-    hipLaunchKernelGGL(maxpool_s1_fwd_sep, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)),
-                       s1_fwd_lds(rows, G), s, p, G, nchunk, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg);
+    const int rows = p.T * p.H, G = s1_groups(rows, p.C, g_s1_maxthr, B), nchunk = (p.C / 8 + G - 1) / G;
+    launch_s1_fwd(p.W, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)), s1_fwd_lds(rows, G), s, p, G,
+                  nchunk, (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg);
     return true;
   }
   if (is_s1_333(p)) {
@@ -1143,10 +1194,10 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   const PoolDivs d = make_divs(p);
   if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
     const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
-    const int rows = p.T * p.H, G = s1_groups(rows, p.C, 512, B), nchunk = (p.C / 8 + G - 1) / G;
-    hipLaunchKernelGGL(maxpool_s1_bwd_sep, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)),
-                       s1_bwd_lds(rows, G), s, p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg,
-                       (const bf16_t*)nullptr, (const bf16_t*)nullptr, (float*)nullptr, (bf16_t*)dx);
+    const int rows = p.T * p.H, G = s1_groups(rows, p.C, g_s1_maxthr, B), nchunk = (p.C / 8 + G - 1) / G;
+    launch_s1_bwd(p.W, dim3((unsigned)(B * nchunk)), dim3(s1_threads(rows, G)), s1_bwd_lds(rows, G), s, p, G,
+                  nchunk, (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)nullptr, (const bf16_t*)nullptr,
+                  (float*)nullptr, (bf16_t*)dx);
     return true;
   }
   if (is_s1_333(p) && bn_y == nullptr) {
@@ -1272,10 +1323,10 @@ MILNCE_API int milnce_maxpool_s1_bwd_fused(const void* dy, const void* arg, cons
   const int rows = T * H;
   // the separable code layout must match the forward that produced arg (milnce_maxpool_fwd)
   if (!s1_use_lds(p) || (gs != nullptr && x == nullptr)) return (int)hipErrorInvalidValue;
-  const int G = s1_groups(rows, C, 512, B), nchunk = (C / 8 + G - 1) / G;
-  hipLaunchKernelGGL(maxpool_s1_bwd_sep, dim3((unsigned)((long long)B * nchunk)), dim3(s1_threads(rows, G)),
-                     s1_bwd_lds(rows, G), stream, p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg,
-                     (const bf16_t*)acc_in, (const bf16_t*)x, gs, (bf16_t*)dx);
+  const int G = s1_groups(rows, C, g_s1_maxthr, B), nchunk = (C / 8 + G - 1) / G;
+  launch_s1_bwd(W, dim3((unsigned)((long long)B * nchunk)), dim3(s1_threads(rows, G)), s1_bwd_lds(rows, G), stream,
+                p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)acc_in, (const bf16_t*)x, gs,
+                (bf16_t*)dx);
   return (int)hipGetLastError();
 }
 

@@ -138,6 +138,10 @@ _NUM_CU = 256
 
 
 _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (csrc/conv.hip)
+# their variants: 3 / 4 (128-row tiles, 3 / 2 stages); 192 also splits into the BK-32 4-stage
+# ring (5) (csrc/conv.hip v3_fits). Its 256-row 8-wave tiles (7) win the isolated timing of the
+# conv_2c dgrad but run 2.1 ms instead of 0.9 ms inside the step, so the tuner does not offer them.
+_WIDE_IMPLS = {96: (3, 4), 160: (3, 4), 192: (3, 4, 5)}
 
 
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
@@ -329,7 +333,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
              plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, impl, stream())
 
     if plan.impl == 0:
-        plan.impl = (_tune(launch, (3, 4) if plan.bn in _WIDE_BN else _IMPLS) if x.dtype != torch.uint8 else 2)
+        plan.impl = (_tune(launch, _WIDE_IMPLS.get(plan.bn, _IMPLS)) if x.dtype != torch.uint8 else 2)
     launch(plan.impl)
     return y
 
@@ -354,7 +358,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl = _tune(launch, (3, 4) if plan.d_bn in _WIDE_BN else _IMPLS)
+        plan.d_impl = _tune(launch, _WIDE_IMPLS.get(plan.d_bn, _IMPLS))
     launch(plan.d_impl)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)

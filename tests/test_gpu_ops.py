@@ -956,3 +956,4 @@ def test_step_weight_prepack_matches_per_call_pack():
         h.zero_arena_end()
         h._PACKER.entries.clear()
         h._PACKER.descs = None
+
