@@ -23,8 +23,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+// Two floats -> a packed bf16 pair in ONE v_cvt_pk_bf16_f32 (RNE, same bits as two f2bf): the
+// scalar form compiles to two converts plus a shift and an OR, i.e. 4 VALU per pair in every
+// epilogue and streaming kernel.
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack2bf(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  const f32x2_t f = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
 }
 
 // Unpack 8 bf16 held in a uint4 to floats.
