@@ -234,6 +234,105 @@ MILNCE_API int milnce_text_relu_max(const void* h, int N, int Wd, int F, float* 
   return (int)hipGetLastError();
 }
 
+// Text tower fc1 fused with its gather and the ReLU-max over words (s3dg.py:196-204):
+//   out[n, f] = max_w relu(bf16(table[tok[n, w]] . w1[f] + b1[f])),  arg = first arg-max word
+// Workgroup = 8 sentences x 64 features: the W1 tile [64][kp] is staged in LDS once and shared by
+// the 8 waves; wave = one sentence (its <= 32 words as two 16-row MFMA fragments, rows gathered
+// straight from the embedding table into the A operand, issued before the W1 staging) x the 64
+// features (four 16-column fragments). K = kp (table and W1 zero-padded to a multiple of 32 bf16). The
+// [N*Wd, F] fc1 output is never stored: the max runs on the accumulators (per lane over its
+// words, then across the four row groups by shuffles).
+constexpr int TXT_FT = 64;  // features per workgroup (41 KiB of W1 in LDS: 3 workgroups per CU)
+template <int KS>  // K steps of 32 (kp / 32), compile time: every A fragment is loaded up front
+__global__ __launch_bounds__(512) void text_fc1_max_kernel(const long long* __restrict__ tok, int N, int Wd,
+                                                           const bf16_t* __restrict__ table,
+                                                           const bf16_t* __restrict__ w1, const float* __restrict__ b1,
+                                                           int F, int kp, float* __restrict__ out,
+                                                           uint8_t* __restrict__ arg) {
+  extern __shared__ __attribute__((aligned(16))) bf16_t ws[];  // [TXT_FT][kp + 8]
+  const int ldw = kp + 8;
+  const int f0 = blockIdx.y * TXT_FT;
+  const int lane = threadIdx.x & 63;
+  const int n = blockIdx.x * 8 + (threadIdx.x >> 6);
+  const bool live = n < N;  // wave-uniform
+  const int li = lane & 15, g = lane >> 4;
+  // the sentence's gathered rows first (all K steps in flight), then the shared W1 tile
+  bf16x8 a[KS][2];
+#pragma unroll
+  for (int rf = 0; rf < 2; ++rf) {
+    const int w = rf * 16 + li;
+    const long long t = (live && w < Wd) ? tok[(long long)n * Wd + w] : 0;  // rows past Wd: masked below
+    const bf16_t* arow = table + t * kp + g * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a[ks][rf] = *(const bf16x8*)(arow + ks * 32);
+  }
+  const int cpr = kp / 8;
+  for (int i = threadIdx.x; i < TXT_FT * cpr; i += blockDim.x) {
+    const int r = i / cpr, c = i - r * cpr;
+    *(uint4*)(ws + r * ldw + c * 8) = *(const uint4*)(w1 + (long long)(f0 + r) * kp + c * 8);
+  }
+  __syncthreads();
+  if (!live) return;
+  const bf16_t* bl = ws + li * ldw + g * 8;
+  f32x4 acc[2][TXT_FT / 16];
+#pragma unroll
+  for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+    for (int cf = 0; cf < TXT_FT / 16; ++cf) acc[rf][cf] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int cf = 0; cf < TXT_FT / 16; ++cf) {
+      const bf16x8 b = *(const bf16x8*)(bl + cf * 16 * ldw + ks * 32);
+#pragma unroll
+      for (int rf = 0; rf < 2; ++rf)
+        acc[rf][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks][rf], b, acc[rf][cf], 0, 0, 0);
+    }
+  }
+  // C[i = word][j = feature]: this lane holds feature li of each fragment and words rf*16 + 4g + r
+#pragma unroll
+  for (int cf = 0; cf < TXT_FT / 16; ++cf) {
+    const int f = f0 + cf * 16 + li;
+    const float bias = b1[f];
+    float best = -INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int rf = 0; rf < 2; ++rf)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int w = rf * 16 + 4 * g + r;  // ascending per lane
+        const float v = fmaxf(bf2f(f2bf(acc[rf][cf][r] + bias)), 0.f);  // relu(bf16 fc1 output)
+        if (w < Wd && v > best) { best = v; bi = w; }
+      }
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {  // the 4 row groups: larger value, ties to the earlier word
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (g == 0) {
+      out[(long long)n * F + f] = best;
+      arg[(long long)n * F + f] = (uint8_t)bi;
+    }
+  }
+}
+
+MILNCE_API int milnce_text_fc1_max(const long long* tok, int N, int Wd, const void* table, const void* w1,
+                                   const float* b1, int F, int kp, float* out, void* arg, hipStream_t stream) {
+  if (Wd > 32 || Wd < 1 || F % TXT_FT || kp != 320) return (int)hipErrorInvalidValue;  // 300-d word2vec
+  const size_t lds = (size_t)TXT_FT * (kp + 8) * 2;
+  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    HIP_RET(hipFuncSetAttribute((const void*)text_fc1_max_kernel<10>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(text_fc1_max_kernel<10>, dim3((N + 7) / 8, F / TXT_FT), dim3(512), lds, stream, tok, N, Wd,
+                     (const bf16_t*)table, (const bf16_t*)w1, b1, F, kp, out, (uint8_t*)arg);
+  return (int)hipGetLastError();
+}
+
 MILNCE_API int milnce_text_relu_max_bwd(const float* dout, const float* out, const void* arg, int N, int Wd, int F,
                                         void* dh, hipStream_t stream) {
   const long long n = (long long)N * Wd * (F / 8);

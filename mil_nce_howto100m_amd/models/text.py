@@ -5,8 +5,9 @@
 ``word2vec_path=''`` gives a random-init frozen table (the reference joins '' with its
 directory and then fails to load it, ``s3dg.py:158, 238``), which the synthetic benchmark needs.
 
-On GPU the gather + fc1 run as one bf16 GEMM over the gathered rows (hipBLASLt), and
-ReLU + max-over-words is a HIP kernel that also records the arg-max word for the backward.
+On GPU the embedding gather, fc1, its bias, the ReLU and the max over words run as ONE HIP
+MFMA kernel (``ops.hip_ops.text_tower``) over a bf16 copy of the table padded to 320 columns;
+it also records the arg-max word for the backward.
 """
 from __future__ import annotations
 
@@ -41,6 +42,7 @@ class SentenceEmbedding(nn.Module):
             for i, t in enumerate(token_to_word):
                 self.word_to_token[str(t)] = i + 1  # token id = index + 1; 0 is padding
         self._bf16_table: Optional[torch.Tensor] = None
+        self._bf16_key: Optional[tuple] = None
 
     # --- raw-text tokenisation (s3dg.py:166-194) -----------------------------------------
     @staticmethod
@@ -59,22 +61,23 @@ class SentenceEmbedding(nn.Module):
         return torch.stack([self._words_to_token(self._split_text(s)) for s in sentences], dim=0)
 
     # --- forward (s3dg.py:196-204) --------------------------------------------------------
-    def _table(self, dtype: torch.dtype) -> torch.Tensor:
+    def _table(self) -> torch.Tensor:
+        """bf16, 32-column-padded copy of the frozen table for the fused GPU kernel; rebuilt when
+        the table is replaced or modified in place (e.g. ``load_state_dict``)."""
         w = self.word_embd.weight
-        if dtype == w.dtype:
-            return w
-        t = self._bf16_table
-        if t is None or t.device != w.device or t.data_ptr() == 0 or t.shape != w.shape:
-            t = w.detach().to(dtype)
-            self._bf16_table = t
-        return t
+        key = (w.device, w.data_ptr(), w._version, tuple(w.shape))
+        if self._bf16_table is None or self._bf16_key != key:
+            from ..ops import hip_ops
+            self._bf16_table = hip_ops.text_table_padded(w)
+            self._bf16_key = key
+        return self._bf16_table
 
     def forward(self, x, raw_text=False):
         if raw_text:
             x = self.words_to_ids(x).to(self.fc1.weight.device)
         if x.is_cuda and ops.use_hip(x):
             from ..ops import hip_ops
-            return hip_ops.text_tower(x, self._table(torch.bfloat16), self.fc1.weight, self.fc1.bias,
+            return hip_ops.text_tower(x, self._table(), self.fc1.weight, self.fc1.bias,
                                       self.fc2.weight, self.fc2.bias)
         with torch.no_grad():
             e = F.embedding(x, self.word_embd.weight)

@@ -57,6 +57,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_u8_to_bf16": [P, P, L, P],
     "milnce_text_relu_max": [P, I, I, I, P, P, P],
     "milnce_text_relu_max_bwd": [P, P, P, I, I, I, P, P],
+    "milnce_text_fc1_max": [P, I, I, P, P, P, I, I, P, P, P],
     "milnce_loss_fwd": [P, I, I, P, P, P, P],
     "milnce_fused_fwd": [P, P, I, I, I, P, P, P, P, P],
     "milnce_fused_bwd": [P, P, I, I, I, P, P, P, P, P, I, I, P, P],

@@ -1346,24 +1346,32 @@ def global_avgpool(x):
 # Text tower
 # =========================================================================================
 class _TextTower(torch.autograd.Function):
+    """fc2(max_w relu(fc1(table[tokens]))) (``s3dg.py:196-204``). Forward: the gather, fc1, bias,
+    ReLU and the max over words run in ONE MFMA kernel (csrc/misc.hip text_fc1_max_kernel), so
+    neither the gathered embeddings [N*Wd, 300] nor the fc1 output [N*Wd, 2048] is stored.
+    ``table`` is the bf16 embedding table zero-padded to ``kp`` (multiple of 32) columns."""
+
     @staticmethod
     def forward(ctx, tokens, table, w1, b1, w2, b2):
         N, Wd = tokens.shape
-        e = table.index_select(0, tokens.reshape(-1))                     # [N*Wd, 300] bf16
-        h = torch.addmm(b1.to(BF16), e, w1.to(BF16).t())                   # [N*Wd, 2048] bf16 (hipBLASLt)
-        F_ = h.shape[1]
-        hm = torch.empty((N, F_), dtype=F32, device=h.device)
-        arg = torch.empty((N, F_), dtype=torch.uint8, device=h.device)
-        call("milnce_text_relu_max", ptr(h), N, Wd, F_, ptr(hm), ptr(arg), stream())
+        F_, D = w1.shape
+        kp = table.shape[1]
+        w1p = torch.zeros((F_, kp), dtype=BF16, device=w1.device)
+        w1p[:, :D] = w1
+        hm = torch.empty((N, F_), dtype=F32, device=w1.device)
+        arg = torch.empty((N, F_), dtype=torch.uint8, device=w1.device)
+        tok = tokens.to(torch.int64).contiguous()
+        call("milnce_text_fc1_max", ptr(tok), N, Wd, ptr(table), ptr(w1p), ptr(b1.float().contiguous()), F_, kp,
+             ptr(hm), ptr(arg), stream())
         out = torch.addmm(b2, hm, w2.t())
-        ctx.save_for_backward(e, hm, arg, w2)
-        ctx.dims = (N, Wd, F_)
+        ctx.save_for_backward(tok, table, hm, arg, w2)
+        ctx.dims = (N, Wd, F_, D)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        e, hm, arg, w2 = ctx.saved_tensors
-        N, Wd, F_ = ctx.dims
+        tok, table, hm, arg, w2 = ctx.saved_tensors
+        N, Wd, F_, D = ctx.dims
         dout = dout.contiguous().float()
         dw2 = dout.t().mm(hm)
         db2 = dout.sum(0)
@@ -1371,13 +1379,26 @@ class _TextTower(torch.autograd.Function):
         dh = torch.empty((N * Wd, F_), dtype=BF16, device=dout.device)
         call("milnce_text_relu_max_bwd", ptr(dhm), ptr(hm), ptr(arg), N, Wd, F_, ptr(dh), stream())
         dhf = dh.float()
+        e = table.index_select(0, tok.reshape(-1))[:, :D]  # re-gathered (not kept from the forward)
         dw1 = dhf.t().mm(e.float())
         db1 = dhf.sum(0)
         return None, None, dw1, db1, dw2, db2
 
 
-def text_tower(tokens, table_bf16, w1, b1, w2, b2):
-    return _TextTower.apply(tokens.contiguous(), table_bf16, w1, b1, w2, b2)
+def text_table_padded(weight: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of the embedding table with its rows zero-padded to a multiple of 32 columns
+    (the K step of the fused text kernel; 300 -> 320)."""
+    V, D = weight.shape
+    kp = _ceil(D, 32) * 32
+    t = torch.zeros((V, kp), dtype=BF16, device=weight.device)
+    t[:, :D] = weight.detach()
+    return t
+
+
+def text_tower(tokens, table_padded, w1, b1, w2, b2):
+    if tokens.shape[1] > 32:
+        raise ValueError(f"fused text tower supports up to 32 words per sentence, got {tokens.shape[1]}")
+    return _TextTower.apply(tokens.contiguous(), table_padded, w1, b1, w2, b2)
 
 
 def text_relu_max(h):

@@ -382,17 +382,23 @@ def test_avgpool():
     assert torch.allclose(x.grad.float(), torch.full_like(x.float(), 1 / 98.0), rtol=1e-2)
 
 
-def test_text_tower():
+@pytest.mark.parametrize("Wd", [20, 7, 32])
+def test_text_tower(Wd):
+    """Fused gather + fc1 + ReLU + max-over-words kernel (csrc/misc.hip text_fc1_max_kernel)
+    and the fc2 / backward around it vs an fp32 reference on the same bf16 operands."""
     torch.manual_seed(4)
     h = hip()
-    N, Wd, V = 16, 20, 1000
+    N, V = 18, 1000  # 18 sentences: a partial last workgroup (4 sentences per workgroup)
     tok = torch.randint(0, V, (N, Wd), device=DEV)
+    tok[:, Wd // 2:] = 0  # padded word slots hold token 0, as the tokenizer writes them
     table = torch.randn(V, 300, device=DEV)
     fc1, fc2 = nn.Linear(300, 2048).to(DEV), nn.Linear(2048, 512).to(DEV)
-    out = h.text_tower(tok, table.to(torch.bfloat16), fc1.weight, fc1.bias, fc2.weight, fc2.bias)
+    tp = h.text_table_padded(table)
+    assert tp.shape == (V, 320) and int(tp[:, 300:].float().abs().sum()) == 0
+    out = h.text_tower(tok, tp, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
     e = F.embedding(tok, table.to(torch.bfloat16).float())
     w1 = nn.Parameter(fc1.weight.detach().to(torch.bfloat16).float())
-    b1 = nn.Parameter(fc1.bias.detach().to(torch.bfloat16).float())
+    b1 = nn.Parameter(fc1.bias.detach().clone())  # the kernel adds the fp32 bias
     w2 = nn.Parameter(fc2.weight.detach().clone())
     b2 = nn.Parameter(fc2.bias.detach().clone())
     # h is stored in bf16 by the kernel path; round the reference h the same way so the

@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Time every forward / dgrad kernel variant of one conv shape in isolation (csrc/conv.hip
+launch_v3_impl ids), with the BN-statistics epilogue the training step uses.
+
+    python tools/conv_impls.py [--cin 64 --cout 192 --k 1 3 3 --t 8 --hw 50 --batch 256 --impls 3 4 5 7]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from mil_nce_howto100m_amd.ops import hip_ops as h  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cin", type=int, default=64)
+    ap.add_argument("--cout", type=int, default=192)
+    ap.add_argument("--k", type=int, nargs=3, default=[1, 3, 3])
+    ap.add_argument("--t", type=int, default=8)
+    ap.add_argument("--hw", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--impls", type=int, nargs="+", default=[3, 4, 5, 7])
+    o = ap.parse_args()
+    k = tuple(o.k)
+    pad = tuple(kk // 2 for kk in k)
+    x = torch.randn(o.batch, o.t, o.hw, o.hw, o.cin, device="cuda").to(torch.bfloat16)
+    w = torch.randn(o.cout, o.cin, *k, device="cuda") * 0.05
+    plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), pad)
+    wp, wd = h._pack(w, plan, 0), h._pack(w, plan, 1)
+    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device="cuda")
+    dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, o.cout, device="cuda").to(torch.bfloat16)
+    fl = 2.0 * plan.M * plan.Cout * plan.Ktot
+    print(f"{tuple(x.shape)} -> {o.cout} k{k}: fwd tile bn {plan.bn} bk {plan.bk}, dgrad tile bn {plan.d_bn} "
+          f"bk {plan.d_bk}; {fl / 1e9:.0f} GFLOP", flush=True)
+    for impl in o.impls:
+        plan.impl = plan.d_impl = impl
+        try:
+            tf = timeit(lambda: h.conv_forward_raw(x, wp, plan, stats))
+            td = timeit(lambda: h.conv_dgrad(dy, wd, plan))
+        except Exception as e:  # variant not available for this tile
+            print(f"impl {impl}: {e}")
+            continue
+        print(f"impl {impl}: fwd {tf:7.3f} ms {fl / tf / 1e9:6.0f} TF/s   dgrad {td:7.3f} ms {fl / td / 1e9:6.0f} TF/s",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
