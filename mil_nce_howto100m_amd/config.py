@@ -109,6 +109,9 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
                    help="HIP-event timers per step phase, reported in the JSONL metrics")
     g.add_argument("--fault_at_step", type=int, default=-1,
                    help="fault injection: raise on this global step (tests kill-and-resume)")
+    g.add_argument("--verify_buckets", type=int, default=0,
+                   help="debug: check every gradient bucket is unchanged between its all-reduce launch and "
+                        "the end of backward (comm/compute ordering verifier; 2 extra gradient copies)")
     return p
 
 

@@ -21,15 +21,30 @@ sized design:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 
+class BucketOrderError(RuntimeError):
+    """A gradient slice changed after its bucket's all-reduce was issued (verify mode)."""
+
+
 class GradBucketer:
+    """See the module docstring. ``verify`` (or ``MILNCE_VERIFY_BUCKETS=1``) turns on the
+    comm/compute ordering verifier: each bucket is all-reduced from a private copy taken on the
+    compute stream at launch, and ``finish`` checks that the local gradient slice still equals
+    that copy after backward (any later write, e.g. a kernel that accumulated into a parameter
+    after reporting it ready, would silently be lost in normal mode) before installing the
+    reduced copy. Costs two extra gradient copies; for debugging only."""
+
     def __init__(self, params: Sequence[torch.nn.Parameter], world_size: int,
-                 bucket_bytes: int = 8 << 20, process_group=None):
+                 bucket_bytes: int = 8 << 20, process_group=None, verify: Optional[bool] = None):
+        self.verify = (os.environ.get("MILNCE_VERIFY_BUCKETS", "0") == "1") if verify is None else bool(verify)
+        self._snap: Dict[int, torch.Tensor] = {}
+        self._comm: Dict[int, torch.Tensor] = {}
         self.params = [p for p in params if p.requires_grad]
         self.world_size = world_size
         self.group = process_group
@@ -83,8 +98,11 @@ class GradBucketer:
 
     def _launch(self, b: int) -> None:
         s, e = self.buckets[b]
-        self._handles[b] = dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.group,
-                                           async_op=True)
+        buf = self.flat[s:e]
+        if self.verify:  # reduce a private copy; keep another to check the slice against later
+            self._snap[b] = buf.clone()
+            buf = self._comm[b] = buf.clone()
+        self._handles[b] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def _on_grad(self, p: torch.Tensor) -> None:
         """A parameter's gradient for this step is complete (enqueued on the compute stream).
@@ -117,6 +135,18 @@ class GradBucketer:
                 self._launch(b)
         for h in self._handles:
             h.wait()
+        if self.verify:
+            bad = []
+            for b, (s, e) in enumerate(self.buckets):
+                d = (self.flat[s:e] - self._snap[b]).abs().max().item() if e > s else 0.0
+                if d != 0.0:
+                    bad.append((b, d))
+                self.flat[s:e].copy_(self._comm[b])
+            self._snap.clear()
+            self._comm.clear()
+            if bad:
+                raise BucketOrderError("gradient written after its bucket's all-reduce was issued "
+                                       f"(bucket, max |change|): {bad}")
 
 
 class BufferBroadcaster:

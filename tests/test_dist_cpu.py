@@ -265,3 +265,39 @@ def test_bench_contract_two_ranks_cpu():
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
     assert r["config"]["global_batch"] == 4 and r["config"]["parallelism"] == "dp2"
     assert abs(r["value"] - 4 * 1000.0 / r["ms_per_step"]) / r["value"] < 1e-2
+
+
+def _worker_verify(rank, world, port, outdir, late_write):
+    _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.ddp import BucketOrderError, GradBucketer
+    torch.manual_seed(0)
+    lin = torch.nn.Sequential(torch.nn.Linear(8, 8), torch.nn.Linear(8, 4))
+    bk = GradBucketer(list(lin.parameters()), world, bucket_bytes=64, verify=True)
+    bk.zero()
+    x = torch.full((3, 8), 1.0 + rank)
+    lin(x).sum().backward()  # every bucket launches from its post-accumulate hooks
+    if late_write:
+        lin[0].weight.grad.add_(1.0)  # a write after the bucket was issued: lost in normal mode
+    err = None
+    try:
+        bk.finish()
+    except BucketOrderError as e:
+        err = str(e)
+    _put(outdir, rank, (err, bk.flat.clone()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("late_write", [False, True])
+def test_bucket_order_verifier(late_write):
+    """GradBucketer(verify=True): clean steps pass and still all-reduce; a gradient written after
+    its bucket launched is reported (parallel/ddp.py BucketOrderError)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_verify, args=(world, _port(), d, late_write), nprocs=world, join=True)
+        res = _collect(d, world)
+    for err, flat in res:
+        if late_write:
+            assert err is not None and "bucket" in err
+        else:
+            assert err is None
+    assert torch.equal(res[0][1], res[1][1])  # the reduced gradient was installed on both ranks
