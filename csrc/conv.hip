@@ -529,9 +529,13 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
     // wait for them); the ring's counted vmcnt waits stay exact, older stores only add to the count
     ring_barrier();  // previous tile's epilogue done with the LDS
 
-    auto issue = [&](int kt) {
-      bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
-      bf16_t* sb = sa + BM * BK;
+    // DMA source offsets of stage kt's pieces (pure ALU: computed before the wait / barrier that
+    // precedes the issue, so the issue itself is just the buffer_load ... lds instructions)
+    // DMA source offsets of the next stage to issue. Fixed bounds: arrays sized by A_INST / B_INST
+    // here make clang's host pass silently drop the kernel's launch stub (undefined symbol)
+    static_assert(A_INST <= 4 && B_INST <= 8, "offset arrays");
+    uint32_t oa[4], ob[8];
+    auto offsets = [&](int kt) {
       // (tap, c) of this lane's chunk by arithmetic: an LDS table read here would make the
       // compiler drain every LDS-DMA in flight (it cannot prove the read does not alias them)
       const int k = kt * BK + src_chunk * 8;
@@ -548,29 +552,43 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
         const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
         const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                        ((unsigned)wi < (unsigned)p.W);
-        const uint32_t off = v ? rowoff[i] + koff : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * BK), 16, off,
-                                                 0, 0, 0);
+        oa[i] = v ? rowoff[i] + koff : 0x80000000u;
       }
 #pragma unroll
       for (int i = 0; i < B_INST; ++i) {
         const int n = n0 + i * NWAVES * RPI + lrow;
-        const uint32_t off = (uint32_t)(((long long)n * p.Kpad + kt * BK + src_chunk * 8) * 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, off,
-                                                 0, 0, 0);
+        ob[i] = (uint32_t)(((long long)n * p.Kpad + kt * BK + src_chunk * 8) * 2);
       }
+    };
+    auto fire = [&](int kt) {
+      bf16_t* sa = ring + (kt % STAGES) * STAGE_ELEMS;
+      bf16_t* sb = sa + BM * BK;
+#pragma unroll
+      for (int i = 0; i < A_INST; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * BK), 16,
+                                                 oa[i], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < B_INST; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16,
+                                                 ob[i], 0, 0, 0);
     };
 
 #pragma unroll
-    for (int s = 0; s < STAGES - 1; ++s)
-      if (s < nk) issue(s);
+    for (int s = 0; s < STAGES - 1; ++s) {
+      if (s < nk) {
+        offsets(s);
+        fire(s);
+      }
+    }
 
     for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + STAGES - 1 < nk;
+      if (more) offsets(kt + STAGES - 1);
       // stage kt must have landed: later stages (issued: min(nk-1, kt+STAGES-2) - kt of them) may stay in flight
       const int ahead = min(nk - 1, kt + STAGES - 2) - kt;
       wait_stages<NDMA, STAGES - 2>(ahead);
       ring_barrier();
-      if (kt + STAGES - 1 < nk) issue(kt + STAGES - 1);
+      if (more) fire(kt + STAGES - 1);
       const bf16_t* a = ring + (kt % STAGES) * STAGE_ELEMS;
       const bf16_t* bsh = a + BM * BK;
 #pragma unroll

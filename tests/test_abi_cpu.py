@@ -4,6 +4,8 @@ import glob
 import os
 import re
 
+import pytest
+
 from mil_nce_howto100m_amd.ops import _lib
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -42,3 +44,18 @@ def test_signatures_match_c_declarations():
         if want != have:
             bad.append((name, "".join(have), "".join(want)))
     assert not bad, bad
+
+
+def test_library_has_no_undefined_kernel_stubs():
+    """Every kernel's host launch stub is defined in libmilnce_hip.so: clang's host pass can drop a
+    template kernel's stub without an error (seen with a lambda-captured array sized by a
+    template-dependent constant), which only fails at dlopen time on the GPU box."""
+    import shutil
+    import subprocess
+    from mil_nce_howto100m_amd.ops._lib import LIB_PATH
+    nm = shutil.which("nm") or "/opt/rocm/lib/llvm/bin/llvm-nm"
+    if not os.path.exists(LIB_PATH):
+        pytest.skip("library not built")
+    out = subprocess.run([nm, "-D", "--undefined-only", LIB_PATH], capture_output=True, text=True).stdout
+    bad = [ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith("_Z")]
+    assert not bad, bad[:10]
