@@ -15,7 +15,8 @@ from typing import Dict
 import torch  # noqa: F401  (must precede the library load)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_native", "libmilnce_hip.so")
+# MILNCE_LIB_PATH: an alternative build of the same sources (A/B of compile-time kernel options)
+LIB_PATH = os.environ.get("MILNCE_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "_native", "libmilnce_hip.so")
 
 P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
 

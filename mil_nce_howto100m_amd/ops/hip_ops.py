@@ -142,6 +142,16 @@ _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (cs
 # ring (5) (csrc/conv.hip v3_fits). Its 256-row 8-wave tiles (7) win the isolated timing of the
 # conv_2c dgrad but run 2.1 ms instead of 0.9 ms inside the step, so the tuner does not offer them.
 _WIDE_IMPLS = {96: (3, 4), 160: (3, 4), 192: (3, 4, 5)}
+_V4 = os.environ.get("MILNCE_CONV_V4", "1") != "0"
+
+
+def _fwd_impls(bn: int, kpad: int) -> Tuple[int, ...]:
+    """Forward / dgrad variants the tuner tries for an N tile: the v3 family, plus v4 (impl 9:
+    256-row tiles, 8 waves, half-tile LDS-DMA ring) for 128 / 192 tiles with Kpad % 64 == 0."""
+    base = _WIDE_IMPLS.get(bn, _IMPLS)
+    if _V4 and bn in (128, 192) and kpad % 64 == 0:
+        base = base + (9,)
+    return base
 
 
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
@@ -333,7 +343,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
              plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, impl, stream())
 
     if plan.impl == 0:
-        plan.impl = (_tune(launch, _WIDE_IMPLS.get(plan.bn, _IMPLS)) if x.dtype != torch.uint8 else 2)
+        plan.impl = (_tune(launch, _fwd_impls(plan.bn, plan.Kpad)) if x.dtype != torch.uint8 else 2)
     launch(plan.impl)
     return y
 
@@ -358,7 +368,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl = _tune(launch, _WIDE_IMPLS.get(plan.d_bn, _IMPLS))
+        plan.d_impl = _tune(launch, _fwd_impls(plan.d_bn, plan.d_Kpad))
     launch(plan.d_impl)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
