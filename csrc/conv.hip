@@ -707,267 +707,6 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
 }
 
 // ---------------------------------------------------------------------------------------
-// v4 forward / dgrad: 256-row x BN tiles, 8 waves (2 along M x 4 along N, wave tile 128 x BN/4),
-// one workgroup per CU. The K loop runs over HALF tiles of 32 k (a 64-k tile = two halves) held
-// in a 4-slot LDS-DMA ring (slot = half % 4):
-//   half-step h: counted vmcnt (h landed; h+1, h+2 may stay in flight) -> one LDS barrier (h is
-//   readable everywhere, h-1 is no longer read by anyone) -> DMA of half h+3 into h-1's slot ->
-//   B fragments of h -> two phases of (A fragments of 64 rows, 4 x TN MFMAs at raised priority).
-// Three half-tiles (1.5 k-tiles of MFMA work) cover each DMA's latency, with one barrier per 32 k
-// and 8 waves per CU (two per SIMD) instead of v3's two 4-wave workgroups each waiting on its own
-// barrier. Same operand images (16-B XOR swizzle, source-permuted LDS-DMA), accumulator layout
-// and epilogues (EPI 0/1/2) as v3.
-template <int BN, int EPI>
-__global__ __launch_bounds__(512, 1) void conv_fwd_v4_kernel(ConvParams p) {
-  constexpr int BM = 256, NT = 512, NWAVES = 8;
-  constexpr int HK = 32;                    // k per half tile
-  constexpr int CPR = HK / 8;               // 16-B chunks per row of a half
-  constexpr int RPI = 64 / CPR;             // rows per 1-KiB DMA instruction
-  constexpr int A_INST = BM / RPI / NWAVES;  // 2
-  constexpr int B_PIECES = BN / RPI;         // 8 / 12 / 16 DMA instructions for the B half
-  constexpr int B_MAX = (B_PIECES + NWAVES - 1) / NWAVES;
-  constexpr int WM = 128, WN = BN / 4;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int LDE = BN + 8;
-  constexpr int SLOT_ELEMS = (BM + BN) * HK;
-  constexpr int EPI_BYTES = BM * LDE * 2;
-  static_assert(B_PIECES * RPI == BN && TN * 16 == WN && A_INST == 2, "v4 tile");
-  static_assert(B_MAX <= 2, "v4 DMA split");
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* ring = (bf16_t*)smem;  // slot s: A [BM][HK] then B [BN][HK]
-  bf16_t* Es = (bf16_t*)smem;    // epilogue staging [BM][LDE]
-  float* ssl = (float*)(smem + EPI_BYTES);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 2, wc = wave & 3;
-  // B DMA pieces of this wave: piece j = i * 8 + wave (i < B_MAX), when j < B_PIECES
-  const int nb = (B_PIECES - wave + NWAVES - 1) / NWAVES;  // 1 or 2 (wave-uniform)
-  const int nblocks = p.num_n_tiles * p.grid_m;
-  const int logical = xcd_remap(blockIdx.x, nblocks);
-  const int n_tile = logical % p.num_n_tiles;
-  const int m_slot = logical / p.num_n_tiles;
-  const int n0 = n_tile * BN;
-  const int nh = 2 * (p.Kpad / 64);  // half tiles (Kpad is a multiple of 64)
-  const int taps = p.KT * p.KH * p.KW;
-  const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
-  const uint32_t clip_bytes = (uint32_t)(p.x_bstride * 2);
-
-  const int dslot = lane % CPR;
-  const int lrow = wave * RPI + lane / CPR;  // row of DMA instruction i: i * 8 * RPI + lrow
-  const int src_chunk = swz<HK>(lrow, dslot);
-
-  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0,
-                                                     (int)((long long)p.num_n_tiles * BN * p.Kpad * 2), 0x00020000);
-  float e_s[8], e_q[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
-
-  for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
-    const int m0 = m_tile * BM;
-    const uint32_t b0 = (uint32_t)m0 / thw;
-    const char* base = (const char*)p.x + (long long)b0 * p.x_bstride * 2;
-    const long long remain = p.x_total_bytes - (long long)b0 * p.x_bstride * 2;
-    const uint32_t nrec = remain > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)remain;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)nrec, 0x00020000);
-
-    int rt[2], rh[2], rw[2];
-    uint32_t rowoff[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + i * NWAVES * RPI + lrow;
-      if (m < p.M) {
-        uint32_t q = fdiv((uint32_t)m, p.fWo);
-        const int wo = m - q * p.Wo;
-        uint32_t q2 = fdiv(q, p.fHo);
-        const int ho = q - q2 * p.Ho;
-        uint32_t b = fdiv(q2, p.fTo);
-        const int to = q2 - b * p.To;
-        rt[i] = to * p.st - p.pt;
-        rh[i] = ho * p.sh - p.ph;
-        rw[i] = wo * p.sw - p.pw;
-        rowoff[i] = (b - b0) * clip_bytes + (uint32_t)(((rt[i] * p.H + rh[i]) * p.W + rw[i]) * p.Cin * 2);
-      } else {
-        rt[i] = -(1 << 28);
-        rh[i] = 0;
-        rw[i] = 0;
-        rowoff[i] = 0;
-      }
-    }
-
-    f32x4 acc[TN][TM];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int i = 0; i < TM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-    ring_barrier();  // previous tile's epilogue done with the LDS
-
-    auto issue = [&](int h) {
-      bf16_t* sa = ring + (h & 3) * SLOT_ELEMS;
-      bf16_t* sb = sa + BM * HK;
-      const int k = h * HK + src_chunk * 8;
-      const int tap = (int)fdiv((uint32_t)k, p.fCin);
-      const int c = k - tap * p.Cin;
-      const bool kval = tap < taps;
-      const int tq = (int)fdiv((uint32_t)tap, p.fKW);
-      const int dw = tap - tq * p.KW;
-      const int dt = (int)fdiv((uint32_t)tq, p.fKH);
-      const int dh = tq - dt * p.KH;
-      const uint32_t koff = (uint32_t)((((dt * p.H + dh) * p.W + dw) * p.Cin + c) * 2);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int ti = rt[i] + dt, hi = rh[i] + dh, wi = rw[i] + dw;
-        const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
-                       ((unsigned)wi < (unsigned)p.W);
-        const uint32_t off = v ? rowoff[i] + koff : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * HK), 16, off,
-                                                 0, 0, 0);
-      }
-#pragma unroll
-      for (int i = 0; i < B_MAX; ++i) {
-        if (i < nb) {
-          const int n = n0 + i * NWAVES * RPI + lrow;
-          const uint32_t off = (uint32_t)(((long long)n * p.Kpad + h * HK + src_chunk * 8) * 2);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * HK), 16,
-                                                   off, 0, 0, 0);
-        }
-      }
-    };
-    // exact counted waits: this wave issues 2 + nb DMA instructions per half (nb wave-uniform)
-    auto wait_half = [&](int ahead) {  // ahead = halves issued after the one needed (0..2)
-      if (nb == 2) {
-        if (ahead >= 2) wait_vmcnt<8>();
-        else if (ahead == 1) wait_vmcnt<4>();
-        else wait_vmcnt<0>();
-      } else {
-        if (ahead >= 2) wait_vmcnt<6>();
-        else if (ahead == 1) wait_vmcnt<3>();
-        else wait_vmcnt<0>();
-      }
-    };
-
-    for (int h = 0; h < 3 && h < nh; ++h) issue(h);
-
-    for (int h = 0; h < nh; ++h) {
-      const int ahead = min(nh - 1, h + 2) - h;
-      wait_half(ahead);
-      ring_barrier();
-      if (h + 3 < nh) issue(h + 3);
-      const bf16_t* a = ring + (h & 3) * SLOT_ELEMS;
-      const bf16_t* bsh = a + BM * HK;
-      const int chunk = lane >> 4;
-      bf16x8 wf[TN];
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wc * WN + j * 16 + (lane & 15);
-        wf[j] = *(const bf16x8*)(bsh + row * HK + swz<HK>(row, chunk) * 8);
-      }
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph) {
-        bf16x8 xf[TM / 2];
-#pragma unroll
-        for (int i = 0; i < TM / 2; ++i) {
-          const int row = wr * WM + (ph * (TM / 2) + i) * 16 + (lane & 15);
-          xf[i] = *(const bf16x8*)(a + row * HK + swz<HK>(row, chunk) * 8);
-        }
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM / 2; ++i)
-            acc[j][ph * (TM / 2) + i] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][ph * (TM / 2) + i], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ring_barrier();  // every wave done reading the ring before the epilogue reuses it
-
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wr * WM + i * 16 + (lane & 15);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const f32x4 v = acc[j][i];
-        uint2 o;
-        o.x = pack2bf(v[0], v[1]);
-        o.y = pack2bf(v[2], v[3]);
-        const int col = wc * WN + j * 16 + (lane >> 4) * 4;
-        *(uint2*)(Es + row * LDE + col) = o;
-      }
-    }
-    if constexpr (EPI == 2) {
-      for (int t = tid; t < 4 * BN; t += NT) {
-        const int qq = t / BN, c = n0 + (t - qq * BN);
-        ssl[t] = c < p.Cout ? p.bn_ss[qq * p.Cout + c] : 0.f;
-      }
-    }
-    ring_barrier();
-    constexpr int OCPR = BN / 8;
-    constexpr int RPP = NT / OCPR;  // rows per pass
-    const int cc = tid % OCPR;
-    if (tid < RPP * OCPR) {
-#pragma unroll 4
-      for (int row = tid / OCPR; row < BM; row += RPP) {
-        const int m = m0 + row, n = n0 + cc * 8;
-        const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
-        const bool ok = (m < p.M) & (n < p.Cout);
-        if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
-        if constexpr (EPI == 1) {
-          if (ok) {
-            float d8[8];
-            unpack8(dv, d8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              e_s[k] += d8[k];
-              e_q[k] += d8[k] * d8[k];
-            }
-          }
-        }
-        if constexpr (EPI == 2) {
-          if (ok) {
-            float d8[8], y8[8];
-            unpack8(dv, d8);
-            unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const int cl = cc * 8 + k;
-              const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
-              e_s[k] += gm;
-              e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
-            }
-          }
-        }
-      }
-    }
-  }
-
-  if constexpr (EPI != 0) {
-    constexpr int OCPR = BN / 8;
-    __syncthreads();
-    float* red = (float*)smem;  // [2][8][NT]
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { red[k * NT + tid] = e_s[k]; red[(8 + k) * NT + tid] = e_q[k]; }
-    __syncthreads();
-    if (tid < OCPR) {
-      const int npad = p.num_n_tiles * BN;
-      constexpr int ACT = (NT / OCPR) * OCPR;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int j = tid; j < ACT; j += OCPR) { s1 += red[k * NT + j]; s2 += red[(8 + k) * NT + j]; }
-        const int col = n0 + tid * 8 + k;
-        p.stats[(long long)m_slot * 2 * npad + col] = s1;
-        p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------
 // wgrad: dW[n, k] partial over an m-range -> slab[split][Npad][Kpad] (fp32)
 struct WgradParams {
   const bf16_t* dy;    // [M, ldd] bf16
@@ -1973,32 +1712,6 @@ static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-template <int BN, int EPI>
-static int launch_fwd_v4(ConvParams& p, hipStream_t stream) {
-  constexpr size_t ring = (size_t)4 * (256 + BN) * 32 * 2;
-  constexpr size_t epi = (size_t)256 * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
-  const size_t lds = ring > epi ? ring : epi;
-  if (p.Kpad % 64) return (int)hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v4_kernel<BN, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-    attr_set = true;
-  }
-  ConvParams q = p;
-  q.num_m_tiles = (p.M + 255) / 256;
-  const int nblocks = q.num_n_tiles * q.grid_m;
-  hipLaunchKernelGGL((conv_fwd_v4_kernel<BN, EPI>), dim3(nblocks), dim3(512), lds, stream, q);
-  return (int)hipGetLastError();
-}
-
-template <int BN>
-static int launch_v4_epi(ConvParams& p, hipStream_t stream) {
-  if (p.bn_mode == 0) return launch_fwd_v4<BN, 0>(p, stream);
-  if (p.bn_mode == 1) return launch_fwd_v4<BN, 1>(p, stream);
-  return launch_fwd_v4<BN, 2>(p, stream);
-}
-
 // Kernel variants (the host autotunes per conv shape, ops/hip_ops.py):
 //   2: register-staged double buffer; 3: LDS-DMA ring, BK as planned, 3 stages;
 //   4: LDS-DMA ring, 2 stages (2 blocks/CU at BN 128); 5: LDS-DMA ring, BK 32, 4 stages.
@@ -2015,12 +1728,8 @@ static int launch_v3_epi(ConvParams& p, hipStream_t stream) {
 template <int BN, int BK, int NWAVES>
 constexpr bool v3_fits() { return BN % ((512 / BK) * NWAVES) == 0; }
 
-//   9: v4 (256-row tiles, 8 waves, half-tile ring; N tiles 128 / 192, Kpad a multiple of 64).
 template <int BN, int BK>
 static int launch_v3_impl(ConvParams& p, int impl, hipStream_t stream) {
-  if constexpr (BN == 128 || BN == 192) {
-    if (impl == 9) return launch_v4_epi<BN>(p, stream);
-  }
   if constexpr (v3_fits<BN, BK, 8>()) {
     if (impl == 7) return launch_v3_epi<BN, BK, 2, 4>(p, stream);
     if constexpr (3 * (256 + BN) * BK * 2 <= 160 * 1024) {  // 3-stage ring within the LDS

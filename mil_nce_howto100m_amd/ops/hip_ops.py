@@ -142,16 +142,11 @@ _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (cs
 # ring (5) (csrc/conv.hip v3_fits). Its 256-row 8-wave tiles (7) win the isolated timing of the
 # conv_2c dgrad but run 2.1 ms instead of 0.9 ms inside the step, so the tuner does not offer them.
 _WIDE_IMPLS = {96: (3, 4), 160: (3, 4), 192: (3, 4, 5)}
-_V4 = os.environ.get("MILNCE_CONV_V4", "1") != "0"
 
 
 def _fwd_impls(bn: int, kpad: int) -> Tuple[int, ...]:
-    """Forward / dgrad variants the tuner tries for an N tile: the v3 family, plus v4 (impl 9:
-    256-row tiles, 8 waves, half-tile LDS-DMA ring) for 128 / 192 tiles with Kpad % 64 == 0."""
-    base = _WIDE_IMPLS.get(bn, _IMPLS)
-    if _V4 and bn in (128, 192) and kpad % 64 == 0:
-        base = base + (9,)
-    return base
+    """Forward / dgrad variants the tuner tries for an N tile (csrc/conv.hip launch_v3_impl)."""
+    return _WIDE_IMPLS.get(bn, _IMPLS)
 
 
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:

@@ -91,8 +91,7 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
     stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device=DEV)
     outs = {}
-    impls = sorted(set(h._IMPLS) | {9})  # 9 = v4 where the tile allows it (else the C side runs v3 3)
-    for impl in impls:
+    for impl in h._IMPLS:
         plan.impl = plan.d_impl = impl
         for rep in range(2):
             y = h.conv_forward_raw(x, wp, plan, stats)
