@@ -5,7 +5,8 @@
   zero-logit level log(2B) (SURVEY.md §7.3 exit criterion 1);
 * the soft-DTW SDTW_3 loss (BASELINE config 4) and the GradCache micro-batched MIL-NCE loss
   (config 5): the HIP path equals the ATen/MIOpen path on the same weights and batch in
-  train-mode BN (embeddings, loss, loss gradient w.r.t. the embeddings, step loss).
+  train-mode BN (embeddings, loss, loss gradient w.r.t. the embeddings, step loss);
+* the same comparison at the flagship layer shapes (16 x 200^2, K = 4; 64 clips).
 """
 import math
 
@@ -155,3 +156,17 @@ def test_gradcache_loss_hip_matches_aten():
 
     _compare(["--batch_size", "32", "--num_frames", "16", "--video_size", "96", "--num_candidates", "4",
               "--grad_cache_chunks", "4"], mk, chunks=4)
+
+
+def test_flagship_shapes_hip_matches_aten():
+    """The BASELINE config-2 layer shapes (16 x 200^2 clips, K = 4 captions; 64 clips instead of 256
+    to keep the ATen/MIOpen reference quick): every conv / pool / gate runs at its production
+    spatial size and channel count with the kernel variants the autotuner picks for it, and the
+    whole HIP step equals the ATen one (embeddings to bf16 accuracy, loss and embedding gradient
+    to fp32 accuracy, step loss)."""
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+
+    def mk(args):
+        return SyntheticClips(64, 16, 200, 4, args.max_words, args.vocab_size, device=torch.device("cuda")).batch(0)
+
+    _compare(["--batch_size", "64", "--num_frames", "16", "--video_size", "200", "--num_candidates", "4"], mk)
