@@ -16,6 +16,25 @@ typedef short s16x8 __attribute__((ext_vector_type(8)));
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
+// Kernel invariant checks, compiled in only by the checking build (python csrc/build.py --check,
+// -DMILNCE_KCHECK, loaded with MILNCE_LIB_PATH=.../libmilnce_hip_check.so): a failed check prints
+// the condition and traps the wave, so an out-of-range tile / index shows up at its source
+// instead of as a silently dropped (out-of-range buffer) access or a later fault.
+#ifdef MILNCE_KCHECK
+#define KASSERT(cond)                                                                              \
+  do {                                                                                             \
+    if (!(cond)) {                                                                                 \
+      printf("KASSERT failed %s:%d block %d thread %d: %s\n", __FILE__, __LINE__, (int)blockIdx.x, \
+             (int)threadIdx.x, #cond);                                                             \
+      __builtin_trap();                                                                            \
+    }                                                                                              \
+  } while (0)
+#else
+#define KASSERT(cond) \
+  do {                \
+  } while (0)
+#endif
+
 __device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
 
 __device__ __forceinline__ uint16_t f2bf(float f) {

@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
   const int m_slot = logical / p.num_n_tiles;
   const int n0 = n_tile * BN;
   const int nk = p.Kpad / BK;
+  KASSERT(nk * BK == p.Kpad && (int)blockIdx.x < p.num_n_tiles * p.grid_m);
   const int a_ccol = tid % A_CPR;
   const int b_ccol = tid % B_CPR;
   const int taps = p.KT * p.KH * p.KW;
@@ -476,6 +477,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   const int m_slot = logical / p.num_n_tiles;
   const int n0 = n_tile * BN;
   const int nk = p.Kpad / BK;
+  KASSERT(nk * BK == p.Kpad && (int)blockIdx.x < p.num_n_tiles * p.grid_m);
   const int taps = p.KT * p.KH * p.KW;
   const uint32_t thw = (uint32_t)p.To * p.Ho * p.Wo;
   const uint32_t clip_bytes = (uint32_t)(p.x_bstride * 2);
@@ -653,6 +655,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
         const int m = m0 + row, n = n0 + cc * 8;
         const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
         const bool ok = (m < p.M) & (n < p.Cout);
+        KASSERT(!ok || n + 8 <= p.ldy);
         if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
         if constexpr (EPI == 1) {
           // BN statistics of the values actually stored (bf16), as a bf16 BN layer would see them
