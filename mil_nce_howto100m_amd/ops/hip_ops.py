@@ -512,7 +512,10 @@ def _wgrad_tiles(Cout: int) -> List[int]:
 
 
 _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
-_W_OCCS = (4, 2)  # split-K occupancy candidates (workgroups per CU)
+# split-K occupancy candidates (workgroups per CU; more splits hide the wgrad kernels' latency at the
+# price of bigger slabs: same-box bench 66.45 ms with (4, 2), 66.05 with (4, 2, 8), 65.72 with
+# (4, 2, 8, 16)); MILNCE_W_OCCS overrides (A/B runs)
+_W_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_W_OCCS", "4,2,8,16").split(","))
 _HALO_WGRAD = os.environ.get("MILNCE_HALO_WGRAD", "1") != "0"
 _HALO_KERNELS = ((1, 3, 3), (3, 1, 1))
 # (3,1,1) is implemented too but measures slower than the im2col kernel (3 taps amortise the
