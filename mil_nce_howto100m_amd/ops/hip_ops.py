@@ -138,6 +138,10 @@ _NUM_CU = 256
 
 
 _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (csrc/conv.hip)
+# persistent forward / dgrad workgroups per CU (each loops over M tiles). 2 = exactly the residency
+# of the usual 2-stage ring variant (no second partial round of workgroups, half the BN partial
+# rows): same-box bench 65.3 ms at 4, 64.4 at 2, 66.3 at 3, 69.6 at 1. MILNCE_FWD_WGS overrides.
+_FWD_WGS_PER_CU = int(os.environ.get("MILNCE_FWD_WGS", "2"))
 # their variants: 3 / 4 (128-row tiles, 3 / 2 stages); 192 also splits into the BK-32 4-stage
 # ring (5) (csrc/conv.hip v3_fits). Its 256-row 8-wave tiles (7) win the isolated timing of the
 # conv_2c dgrad but run 2.1 ms instead of 0.9 ms inside the step, so the tuner does not offer them.
@@ -165,7 +169,7 @@ def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
     kpad = _ceil(K, bk) * bk
     m_tiles = _ceil(M, 128)
     n_tiles = npad // bn
-    grid_m = max(1, min(m_tiles, _ceil(4 * _NUM_CU, n_tiles)))
+    grid_m = max(1, min(m_tiles, _ceil(_FWD_WGS_PER_CU * _NUM_CU, n_tiles)))
     return bn, bk, npad, kpad, grid_m
 
 
