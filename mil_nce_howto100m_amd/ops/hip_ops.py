@@ -539,17 +539,22 @@ def _halo_wgrad_ok(plan: ConvPlan, x: torch.Tensor) -> bool:
     return _HALO_WGRAD and plan.k in _HALO_TUNED and _halo_wgrad_supported(plan, x)
 
 
-_HALO_SPLITS: Dict[Tuple[int, int], Tuple[int, int]] = {}
+_HALO_SPLITS: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
 
 
-def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: torch.Tensor, accumulate: int) -> None:
+# halo wgrad split targets to tune over, in workgroups per CU (same-box bench: 64.4 ms with 2 only,
+# 63.7 with 1, 2, 4, 8); MILNCE_HALO_OCCS overrides
+_HALO_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_HALO_OCCS", "1,2,4,8").split(","))
+
+
+def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: torch.Tensor, accumulate: int, occ: int = 2) -> None:
     kt, kh, kw = plan.k
-    key = (id(plan), cc)
+    key = (id(plan), cc, occ)
     geo = _HALO_SPLITS.get(key)
     if geo is None:
         floats, splits = ctypes.c_longlong(0), ctypes.c_int(0)
-        rc = lib().milnce_halo_wgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, 64, cc, 0,
-                                          ctypes.byref(floats), ctypes.byref(splits))
+        rc = lib().milnce_halo_wgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, 64, cc,
+                                          occ * _NUM_CU, ctypes.byref(floats), ctypes.byref(splits))
         if rc != 0:
             raise RuntimeError(f"halo wgrad plan failed ({rc}) for {plan}")
         geo = _HALO_SPLITS[key] = (int(floats.value), int(splits.value))
@@ -576,7 +581,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
 
     def launch_with(tn, impl, occ, target, accumulate):
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
-            return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate)
+            return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
         slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
         call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
@@ -594,7 +599,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                     for occ in _W_OCCS:
                         cands.append((tn, impl, occ))
             if _halo_wgrad_ok(plan, x):
-                cands += [(64, 164, 0)]
+                cands += [(64, 164, occ) for occ in _HALO_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4)
