@@ -298,6 +298,7 @@ _IMPLS = (2, 3, 4, 5, 6, 7)
 _W_IMPLS = (2, 3, 4, 5)  # wgrad: register-staged, LDS-DMA 3/2 stages, register-staged 2-deep
 _AUTOTUNE = os.environ.get("MILNCE_CONV_AUTOTUNE", "1") != "0"
 _DEFAULT_IMPL = int(os.environ.get("MILNCE_CONV_IMPL", "2"))
+_TUNE_MARGIN = float(os.environ.get("MILNCE_TUNE_MARGIN", "0.97"))  # another variant must beat the default by 3 %
 
 
 def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
@@ -325,7 +326,7 @@ def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
         times[impl] = timed(impl, max(2, min(50, int(0.5 / max(t0, 1e-3)))))
     best = min(times, key=times.get)
     default = _DEFAULT_IMPL if default is None else default
-    if default in times and times[best] > 0.97 * times[default]:
+    if default in times and times[best] > _TUNE_MARGIN * times[default]:
         best = default
     return best
 
