@@ -1862,6 +1862,9 @@ static int launch_wgrad_impl(WgradParams& p, int impl, hipStream_t stream) {
   }
 }
 
+int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int Kpad, int Cout, int Cin,
+                        int Cin_param, int taps, int accumulate, hipStream_t stream);
+
 MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u8, float* slab, float* dw,
                                  int B, int T, int H, int W, int Cin, int Cin_param, int Cout,
                                  int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
@@ -1906,15 +1909,11 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
     else rc = (int)hipErrorInvalidValue;
   }
   if (rc) return rc;
-  const int taps = KT * KH * KW;
-  const long long total = (long long)Cout * taps * Cin;
-  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, slab, dw, splits, Npad, Kpad,
-                     Cout, Cin, Cin_param, taps, accumulate);
-  return (int)hipGetLastError();
+  if (dw == nullptr) return 0;  // the caller reduces the slab itself (milnce_wgrad_reduce, e.g. on a side stream)
+  return launch_wgrad_reduce(slab, dw, splits, Npad, Kpad, Cout, Cin, Cin_param, KT * KH * KW, accumulate, stream);
 }
 
-// host launcher of the slab reduction for the other translation units (csrc/conv_halo.hip)
+// host launcher of the slab reduction, shared with csrc/conv_halo.hip
 int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int Kpad, int Cout, int Cin,
                         int Cin_param, int taps, int accumulate, hipStream_t stream) {
   const long long total = (long long)Cout * taps * Cin;
@@ -1922,6 +1921,13 @@ int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int 
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, slab, dw, splits, Npad, Kpad,
                      Cout, Cin, Cin_param, taps, accumulate);
   return (int)hipGetLastError();
+}
+
+// dW (+)= sum over the split slabs [splits][Npad][Kpad] of a wgrad (milnce_conv_wgrad /
+// milnce_halo_wgrad called with dw == nullptr), into the parameter layout [Cout][Cin_param][taps].
+MILNCE_API int milnce_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int Kpad, int Cout, int Cin,
+                                   int Cin_param, int taps, int accumulate, hipStream_t stream) {
+  return launch_wgrad_reduce(slab, dw, splits, Npad, Kpad, Cout, Cin, Cin_param, taps, accumulate, stream);
 }
 
 MILNCE_API int milnce_pack_weight(const float* w, void* out, int Cout, int Cin, int Cin_p, int KT, int KH,

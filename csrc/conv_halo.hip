@@ -388,5 +388,6 @@ MILNCE_API int milnce_halo_wgrad(const void* dy, int ldd, const void* x, float* 
     else return (int)hipErrorInvalidValue;
   }
   if (rc) return rc;
+  if (dw == nullptr) return 0;  // the caller reduces the slab (milnce_wgrad_reduce; Npad = ceil(Cout / bn) * bn, Kpad = taps * Cin)
   return launch_wgrad_reduce(slab, dw, splits, p.Npad, p.Kdim, Cout, Cin, Cin_param, KT * KH * KW, accumulate, stream);
 }

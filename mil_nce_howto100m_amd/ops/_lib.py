@@ -26,6 +26,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],
     "milnce_halo_wgrad_plan": [I] * 12 + [P, P],
     "milnce_halo_wgrad": [P, I, P, P, P, I] + [I] * 13 + [P],
+    "milnce_wgrad_reduce": [P, P] + [I] * 8 + [P],
     "milnce_pack_weights_multi": [P, I, I, P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],

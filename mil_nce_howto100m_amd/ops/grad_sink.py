@@ -1,7 +1,15 @@
 """Who to tell when a kernel wrote a parameter's gradient in place (see hip_ops "Direct
 gradient writes"). The data-parallel bucketer registers itself here; pure Python, so it can be
-imported on CPU-only hosts without loading the HIP library."""
+imported on CPU-only hosts without loading the HIP library.
+
+Deferred writes: a gradient whose final write runs on a side stream (the split-K wgrad slab
+reduction, hip_ops.conv_wgrad(defer=True)) registers that stream's completion event with
+``defer``; ``drain`` makes the current stream wait for all of them. Every consumer of the flat
+gradient buffer drains first: the bucketer before each all-reduce and in ``finish`` (which the
+trainer calls before the optimizer step); the first deferral of a backward pass also queues a
+drain as an autograd end-of-pass callback."""
 _SINK = None
+_PENDING = []
 
 
 def set_sink(fn) -> None:
@@ -12,3 +20,29 @@ def set_sink(fn) -> None:
 def notify(param) -> None:
     if _SINK is not None:
         _SINK(param)
+
+
+def defer(event) -> None:
+    if not _PENDING:
+        # join at the end of the running backward pass too, so gradients are complete when
+        # .backward() returns whoever reads them (a no-op if a bucket launch drained already)
+        try:
+            import torch
+            torch.autograd.Variable._execution_engine.queue_callback(drain)
+        except RuntimeError:  # not inside a backward pass: the explicit drain() points remain
+            pass
+    _PENDING.append(event)
+
+
+def drain() -> None:
+    if not _PENDING:
+        return
+    import torch
+    s = torch.cuda.current_stream()
+    for e in _PENDING:
+        s.wait_event(e)
+    _PENDING.clear()
+
+
+def pending() -> int:
+    return len(_PENDING)

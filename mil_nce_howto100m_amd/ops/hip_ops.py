@@ -517,6 +517,23 @@ def _wgrad_tiles(Cout: int) -> List[int]:
 
 
 _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: register-staged only
+
+
+def _wide_w_impls(tn: int, tk: int) -> Tuple[int, ...]:
+    if tn == 192 and tk == 64:  # the 2-deep register-staged 192 x 64 tile fits (192 x 128 would spill)
+        return (2, 5)
+    return _WIDE_W_IMPLS.get(tn, _W_IMPLS)
+
+
+# K-tile candidates: 64 besides the default 128 where 128 pads the reduction width (e.g. a
+# (3,1,1) conv over 192 channels: Ktot 576 -> 640 with 128-wide tiles); MILNCE_W_TK64=0 disables
+_W_TK64 = os.environ.get("MILNCE_W_TK64", "1") != "0"
+
+
+def _wgrad_tks(plan: "ConvPlan") -> Tuple[int, ...]:
+    if _W_TK64 and plan.w_tk == 128 and plan.Ktot % 128 != 0:
+        return (128, 64)
+    return (plan.w_tk,)
 # split-K occupancy candidates (workgroups per CU; more splits hide the wgrad kernels' latency at the
 # price of bigger slabs: same-box bench 66.45 ms with (4, 2), 66.05 with (4, 2, 8), 65.72 with
 # (4, 2, 8, 16)); MILNCE_W_OCCS overrides (A/B runs)
@@ -548,7 +565,10 @@ _HALO_SPLITS: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
 _HALO_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_HALO_OCCS", "1,2,4,8").split(","))
 
 
-def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: torch.Tensor, accumulate: int, occ: int = 2) -> None:
+def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: Optional[torch.Tensor], accumulate: int,
+                occ: int = 2):
+    """Box-tiled wgrad; with ``target`` None the kernel only fills the split slab and the
+    (slab, splits, Npad, Kpad) of the pending reduction is returned."""
     kt, kh, kw = plan.k
     key = (id(plan), cc, occ)
     geo = _HALO_SPLITS.get(key)
@@ -560,13 +580,49 @@ def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: torch.Tensor, accumulate
             raise RuntimeError(f"halo wgrad plan failed ({rc}) for {plan}")
         geo = _HALO_SPLITS[key] = (int(floats.value), int(splits.value))
     slab = torch.empty((geo[0],), dtype=F32, device=dy.device)
-    call("milnce_halo_wgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target), accumulate, plan.B, plan.T,
-         plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, 64, cc, geo[1], stream())
+    call("milnce_halo_wgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target) if target is not None else None,
+         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, 64, cc, geo[1],
+         stream())
+    return slab, geo[1], _ceil(plan.Cout, 64) * 64, kt * kh * kw * plan.Cin
 
 
-def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+# Deferred slab reductions (conv_wgrad(defer=True)): the split-K reduce of a parameter's wgrad is
+# a small latency-bound kernel (~17 us, 58 per flagship step) that nothing in the backward pass
+# waits for, so it can run on a side stream overlapping the next layer's kernels; grad_sink.drain()
+# joins it before the gradients are read (all-reduce, optimizer). Opt-in (MILNCE_DEFER_WGRAD=1):
+# same-box bench A/B 4012 pairs/s inline vs 4003 deferred -- the big kernels it would overlap
+# already fill the chip, so there is no idle gap for the reduce to hide in.
+_DEFER_WGRAD = os.environ.get("MILNCE_DEFER_WGRAD", "0") == "1"
+_SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE_STREAMS.get(idx)
+    if s is None:
+        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def _reduce_on_side(slab: torch.Tensor, dw: torch.Tensor, splits: int, npad: int, kpad: int, plan: ConvPlan,
+                    accumulate: int) -> None:
+    main = torch.cuda.current_stream(slab.device)
+    side = _side_stream(slab.device)
+    side.wait_stream(main)
+    call("milnce_wgrad_reduce", ptr(slab), ptr(dw), splits, npad, kpad, plan.Cout, plan.Cin, plan.Cin_p,
+         plan.k[0] * plan.k[1] * plan.k[2], accumulate, side.cuda_stream)
+    slab.record_stream(side)  # the allocator must not hand the slab to the main stream before the reduce ran
+    ev = torch.cuda.Event()
+    ev.record(side)
+    grad_sink.defer(ev)
+
+
+def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None,
+               defer: bool = False) -> torch.Tensor:
     """dW of the conv; with ``out`` the result is accumulated into it (a parameter's grad).
-    The first call of a plan tunes over (N tile, kernel variant) pairs on the real operands."""
+    The first call of a plan tunes over (N tile, kernel variant) pairs on the real operands.
+    ``defer`` (with ``out``): the final split-K reduction into ``out`` runs on a side stream and
+    is only complete after grad_sink.drain() (see _reduce_on_side)."""
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
@@ -580,14 +636,18 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         if rc == 0:
             return dw
 
-    def launch_with(tn, impl, occ, target, accumulate):
+    def launch_with(tn, impl, occ, tk, target, accumulate):
+        """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
+        (slab, splits, Npad, Kpad) returned for the caller's reduction."""
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
             return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
-        npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
+        npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, tk, occ)
         slab = torch.empty((splits, npad, kpad), dtype=F32, device=dy.device)
-        call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab), ptr(target),
+        call("milnce_conv_wgrad", ptr(dy), ldd, ptr(x), int(x.dtype == torch.uint8), ptr(slab),
+             ptr(target) if target is not None else None,
              plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-             kpad, npad, tn, plan.w_tk, splits, accumulate, plan.wo_override, impl, stream())
+             kpad, npad, tn, tk, splits, accumulate, plan.wo_override, impl, stream())
+        return slab, splits, npad, kpad
 
     if plan.w_impl == 0:
         if x.dtype == torch.uint8 or not _AUTOTUNE:
@@ -595,21 +655,28 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         else:
             scratch = torch.empty_like(dw)  # tune on a scratch output: the real one may accumulate
             cands = []
-            for tn in _wgrad_tiles(plan.Cout):
-                for impl in _WIDE_W_IMPLS.get(tn, _W_IMPLS):
-                    for occ in _W_OCCS:
-                        cands.append((tn, impl, occ))
+            for tk in _wgrad_tks(plan):
+                for tn in _wgrad_tiles(plan.Cout):
+                    for impl in _wide_w_impls(tn, tk):
+                        for occ in _W_OCCS:
+                            cands.append((tn, impl, occ, tk))
             if _halo_wgrad_ok(plan, x):
-                cands += [(64, 164, occ) for occ in _HALO_OCCS]
+                cands += [(64, 164, occ, 0) for occ in _HALO_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
-            default = (plan.w_tn, _DEFAULT_IMPL, 4)
+            default = (plan.w_tn, _DEFAULT_IMPL, 4, plan.w_tk)
             best = _tune(lambda c: launch_with(*inv[c], scratch, 0), tuple(code.values()),
                          default=code.get(default))
-            tn, impl, occ = inv[best]
+            tn, impl, occ, tk = inv[best]
             plan.w_tn, plan.w_impl, plan.w_occ = tn, impl, occ
+            if impl < 100:
+                plan.w_tk = tk
             plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
-    launch_with(plan.w_tn, plan.w_impl, plan.w_occ, dw, acc)
+    if defer and out is not None and _DEFER_WGRAD:
+        slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, acc)
+        _reduce_on_side(slab, dw, splits, npad, kpad, plan, acc)
+    else:
+        launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
     return dw
 
 
@@ -692,7 +759,7 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     dw = None
     if ctx.needs_input_grad[1]:
         w_direct = _direct_grad(weight)
-        dw = conv_wgrad(dy, x, plan, out=w_direct)
+        dw = conv_wgrad(dy, x, plan, out=w_direct, defer=True)
         if w_direct is not None:
             _grad_done(weight)
             dw = None

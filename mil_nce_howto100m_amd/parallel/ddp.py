@@ -117,6 +117,8 @@ class GradBucketer:
         b = self.bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0 and self._handles[b] is None:
+            from ..ops import grad_sink
+            grad_sink.drain()  # gradients still being reduced on a side stream land first
             self._launch(b)
 
     def set_sync(self, enabled: bool) -> None:
@@ -127,7 +129,12 @@ class GradBucketer:
         self._ready = set()
 
     def finish(self) -> None:
-        """Issue buckets whose params got no gradient this step, then wait for all."""
+        """Issue buckets whose params got no gradient this step, then wait for all. Also the
+        point where deferred (side-stream) gradient writes are joined into the compute stream,
+        so it must run before anything reads the gradients (the trainer calls it before the
+        optimizer step, at every world size)."""
+        from ..ops import grad_sink
+        grad_sink.drain()
         if self.world_size <= 1:
             return
         for b in range(len(self.buckets)):

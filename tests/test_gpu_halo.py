@@ -108,3 +108,39 @@ def test_fused_milnce_speed_report(B):
             torch.cuda.synchronize()
             res[fused] = (time.perf_counter() - t0) * 1e3
     print(f"B {B}: fused {res[True]:.3f} ms, materialised {res[False]:.3f} ms")
+
+
+@pytest.mark.parametrize("k,halo", [((1, 3, 3), True), ((1, 3, 3), False), ((3, 1, 1), False), ((1, 1, 1), False)])
+def test_deferred_wgrad_reduce_matches_inline(k, halo, monkeypatch):
+    """conv_wgrad(defer=True): the split-K slab reduction runs on a side stream and lands in the
+    accumulated gradient once grad_sink.drain() joined it -- same values as the inline reduce,
+    also when the main stream immediately reuses freed memory for new work."""
+    from mil_nce_howto100m_amd.ops import grad_sink
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    monkeypatch.setattr(h, "_DEFER_WGRAD", True)
+    torch.manual_seed(7)
+    B, T, H, W, Cin, Cout = 4, 8, 25, 25, 64, 192
+    pad = tuple(kk // 2 for kk in k)
+    x = torch.randn(B, T, H, W, Cin, device="cuda").to(torch.bfloat16)
+    dy = torch.randn(B, T, H, W, Cout, device="cuda").to(torch.bfloat16)
+    plan = h.conv_plan(x.shape, (Cout, Cin) + k, (1, 1, 1), pad)
+    if halo:
+        if not h._halo_wgrad_supported(plan, x):
+            pytest.skip("no halo kernel for this shape")
+        plan.w_tn, plan.w_impl, plan.w_occ = 64, 164, 2
+    else:
+        plan.w_tn, plan.w_impl, plan.w_occ = 128, 2, 4
+    ref = torch.full((Cout, Cin) + k, 0.25, device="cuda")
+    h.conv_wgrad(dy, x, plan, out=ref)
+    out = torch.full((Cout, Cin) + k, 0.25, device="cuda")
+    for _ in range(3):  # three deferred accumulations, each followed by main-stream allocations
+        h.conv_wgrad(dy, x, plan, out=out, defer=True)
+        junk = [torch.full((1 << 20,), 9.0, device="cuda") for _ in range(8)]
+        del junk
+    assert grad_sink.pending() == 3
+    grad_sink.drain()
+    assert grad_sink.pending() == 0
+    expect = (ref - 0.25) * 3 + 0.25
+    torch.cuda.synchronize()
+    err = ((out - expect).norm() / (expect - 0.25).norm()).item()
+    assert err < 1e-6, err
