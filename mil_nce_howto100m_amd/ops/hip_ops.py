@@ -526,12 +526,13 @@ def _wide_w_impls(tn: int, tk: int) -> Tuple[int, ...]:
 
 
 # K-tile candidates: 64 besides the default 128 where 128 pads the reduction width (e.g. a
-# (3,1,1) conv over 192 channels: Ktot 576 -> 640 with 128-wide tiles); MILNCE_W_TK64=0 disables
-_W_TK64 = os.environ.get("MILNCE_W_TK64", "1") != "0"
+# (3,1,1) conv over 192 channels: Ktot 576 -> 640 with 128-wide tiles; same-box bench 4010 ->
+# 4050 pairs/s); MILNCE_W_TK64=0 disables, =2 offers 64 for every layer
+_W_TK64 = int(os.environ.get("MILNCE_W_TK64", "1"))
 
 
 def _wgrad_tks(plan: "ConvPlan") -> Tuple[int, ...]:
-    if _W_TK64 and plan.w_tk == 128 and plan.Ktot % 128 != 0:
+    if _W_TK64 and plan.w_tk == 128 and (plan.Ktot % 128 != 0 or _W_TK64 == 2):
         return (128, 64)
     return (plan.w_tk,)
 # split-K occupancy candidates (workgroups per CU; more splits hide the wgrad kernels' latency at the
