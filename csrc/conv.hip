@@ -730,6 +730,9 @@ struct WgradParams {
 constexpr int WG_R = 64;  // reduction rows (m) per LDS stage = two 32-deep MFMA k-steps
 constexpr int WG_R_MAX = 64;
 
+template <int TK>
+constexpr int wg_xpad() { return TK == 192 ? 8 : 16; }
+
 // Per-stage row table (one decomposition per row instead of one per row and chunk column):
 // .x = element offset of the row's unshifted input origin relative to the split's first clip,
 // .y = (rt + 64) | (rh + 64) << 10 | (rw + 64) << 20 (rows past m_end: all fields 0 -> invalid).
@@ -753,12 +756,27 @@ __device__ __forceinline__ void wgrad_row_table(int2* tab, const WgradParams& p,
   }
 }
 
+// The im2col (tap, channel) of a thread's X chunks. A thread's chunk i sits in column
+// (tid + 256 i) % XCPR: one fixed column when XCPR divides 256, else XP = XCPR / gcd(256, XCPR)
+// columns used cyclically (TK = 192: 24 chunks per row, columns repeat every 3 chunks).
+// Fixed-size arrays (see the note on launch stubs in conv_fwd_v3_kernel).
+struct XCols {
+  int tapoff[4], dt[4], dh[4], dw[4], col[4];
+  bool kval[4];
+};
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+template <int XCPR>
+constexpr int x_period() { return XCPR / cgcd(256, XCPR); }
+
 // Stage this thread's chunks of dY rows [mb, mb+R) and of the im2col X rows.
 template <int DCH, int XCH, int DCPR, int XCPR, int VEC, int ESZ, bool U8, typename XReg>
 __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH], __amdgpu_buffer_rsrc_t drs,
                                            __amdgpu_buffer_rsrc_t xrs, const WgradParams& p, const int2* tab,
-                                           int mb, int m_end, int m_base, int tid, int n0, int d_ccol, bool kval,
-                                           int dt, int dh, int dw, int tapoff) {
+                                           int mb, int m_end, int m_base, int tid, int n0, int d_ccol,
+                                           const XCols& xc) {
+  constexpr int XP = x_period<XCPR>();
 #pragma unroll
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
@@ -772,10 +790,12 @@ __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH]
   for (int i = 0; i < XCH; ++i) {
     const int row = (tid + i * 256) / XCPR;
     const int2 e = tab[row];
-    const int ti = (e.y & 1023) - 64 + dt, hi = ((e.y >> 10) & 1023) - 64 + dh, wi = (e.y >> 20) - 64 + dw;
-    const bool v = kval & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
+    const int j = i % XP;
+    const int ti = (e.y & 1023) - 64 + xc.dt[j], hi = ((e.y >> 10) & 1023) - 64 + xc.dh[j],
+              wi = (e.y >> 20) - 64 + xc.dw[j];
+    const bool v = xc.kval[j] & ((unsigned)ti < (unsigned)p.T) & ((unsigned)hi < (unsigned)p.H) &
                    ((unsigned)wi < (unsigned)p.W);
-    const uint32_t off = v ? (uint32_t)((e.x + tapoff) * ESZ) : 0x80000000u;
+    const uint32_t off = v ? (uint32_t)((e.x + xc.tapoff[j]) * ESZ) : 0x80000000u;
     if constexpr (U8) {
       xreg[i] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0);
     } else {
@@ -786,7 +806,8 @@ __device__ __forceinline__ void wgrad_load(uint4 (&dreg)[DCH], XReg (&xreg)[XCH]
 
 template <int DCH, int XCH, int DCPR, int XCPR, int LDN, int LDK, bool U8, typename XReg>
 __device__ __forceinline__ void wgrad_store(const uint4 (&dreg)[DCH], const XReg (&xreg)[XCH], bf16_t* d, bf16_t* x,
-                                            int tid, int d_ccol, int x_ccol, float in_scale) {
+                                            int tid, int d_ccol, const XCols& xc, float in_scale) {
+  constexpr int XP = x_period<XCPR>();
 #pragma unroll
   for (int i = 0; i < DCH; ++i) {
     const int row = (tid + i * 256) / DCPR;
@@ -795,6 +816,7 @@ __device__ __forceinline__ void wgrad_store(const uint4 (&dreg)[DCH], const XReg
 #pragma unroll
   for (int i = 0; i < XCH; ++i) {
     const int row = (tid + i * 256) / XCPR;
+    const int x_ccol = xc.col[i % XP];
     if constexpr (U8) {
       const uint32_t v = xreg[i];
       uint2 o;
@@ -826,7 +848,8 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
   constexpr int R = WG_R;
   constexpr int VEC = U8 ? 4 : 8;
   constexpr int ESZ = U8 ? 1 : 2;
-  constexpr int LDN = TN_ + 16, LDK = TK_ + 16;  // padded rows: conflict-free transposed reads
+  // padded rows: conflict-free transposed reads (TK 192: pad 8 keeps two workgroups per CU)
+  constexpr int LDN = TN_ + 16, LDK = TK_ + wg_xpad<TK_>();
   constexpr int DCPR = TN_ / 8, XCPR = TK_ / VEC;
   constexpr int DCH = R * DCPR / 256, XCH = R * XCPR / 256;
   constexpr int WN = TN_ / 2, WK = TK_ / 2;
@@ -852,16 +875,23 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
   const int m_begin = split * p.rows_per_split;
   const int m_end = min(p.M, m_begin + p.rows_per_split);
 
-  // fixed (tap, c) of this thread's X chunk column
-  const int x_ccol = tid % XCPR;
-  const int kk = k0 + x_ccol * VEC;
-  const int tap = (int)fdiv((uint32_t)kk, p.fCin);
-  const int c = kk - tap * p.Cin;
-  const bool kval = kk < p.Ktot;
-  const int dw = tap % p.KW;
-  const int dh = (tap / p.KW) % p.KH;
-  const int dt = tap / (p.KW * p.KH);
-  const int tapoff = ((dt * p.H + dh) * p.W + dw) * p.Cin + c;
+  // fixed (tap, c) of this thread's X chunk column(s)
+  constexpr int XP = x_period<XCPR>();
+  static_assert(XP <= 4 && XCH % XP == 0, "X chunk column period");
+  XCols xc;
+#pragma unroll
+  for (int j = 0; j < XP; ++j) {
+    const int col = (tid + j * 256) % XCPR;
+    const int kk = k0 + col * VEC;
+    const int tap = (int)fdiv((uint32_t)kk, p.fCin);
+    const int c = kk - tap * p.Cin;
+    xc.col[j] = col;
+    xc.kval[j] = kk < p.Ktot;
+    xc.dw[j] = tap % p.KW;
+    xc.dh[j] = (tap / p.KW) % p.KH;
+    xc.dt[j] = tap / (p.KW * p.KH);
+    xc.tapoff[j] = ((xc.dt[j] * p.H + xc.dh[j]) * p.W + xc.dw[j]) * p.Cin + c;
+  }
   const int d_ccol = tid % DCPR;
 
   // Descriptors based at this split's first row / first clip: offsets stay 32-bit whatever the
@@ -914,20 +944,20 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
       wgrad_row_table(rtab + R, p, m_begin + R, m_end, b_first, tid);
       __syncthreads();
       wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
-                                                      n0, d_ccol, kval, dt, dh, dw, tapoff);
-      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+                                                      n0, d_ccol, xc);
+      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, xc, p.in_scale);
     }
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
       const int buf = s & 1;
       const int sn = min(s + 1, nsteps - 1);  // unconditional prefetch (the last one is a harmless repeat)
       wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sn & 1) * R, m_begin + sn * R,
-                                                      m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+                                                      m_end, m_clamped, tid, n0, d_ccol, xc);
       // row table of stage s + 2 into the slot stage s used (its last reader was iteration s - 1)
       if (s + 2 < nsteps) wgrad_row_table(rtab + buf * R, p, m_begin + (s + 2) * R, m_end, b_first, tid);
       compute(buf);
       wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds + (buf ^ 1) * R * LDN, Xs + (buf ^ 1) * R * LDK,
-                                                       tid, d_ccol, x_ccol, p.in_scale);
+                                                       tid, d_ccol, xc, p.in_scale);
       __syncthreads();
     }
   } else {
@@ -938,10 +968,10 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
       for (int st = 0; st < 3; ++st) wgrad_row_table(rtab + (st & 3) * R, p, m_begin + st * R, m_end, b_first, tid);
       __syncthreads();
       wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab, m_begin, m_end, m_clamped, tid,
-                                                      n0, d_ccol, kval, dt, dh, dw, tapoff);
-      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+                                                      n0, d_ccol, xc);
+      wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, xc, p.in_scale);
       wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg2, xreg2, drs, xrs, p, rtab + R, m_begin + R, m_end,
-                                                      m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+                                                      m_clamped, tid, n0, d_ccol, xc);
     }
     __syncthreads();
     for (int s = 0; s < nsteps; s += 2) {
@@ -949,12 +979,12 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
       {
         const int sl = min(s + 2, nsteps - 1);
         wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg, xreg, drs, xrs, p, rtab + (sl & 3) * R, m_begin + sl * R,
-                                                        m_end, m_clamped, tid, n0, d_ccol, kval, dt, dh, dw, tapoff);
+                                                        m_end, m_clamped, tid, n0, d_ccol, xc);
         if (s + 3 < nsteps)
           wgrad_row_table(rtab + ((s + 3) & 3) * R, p, m_begin + (s + 3) * R, m_end, b_first, tid);
         compute(0);
-        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg2, xreg2, Ds + R * LDN, Xs + R * LDK, tid, d_ccol,
-                                                         x_ccol, p.in_scale);
+        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg2, xreg2, Ds + R * LDN, Xs + R * LDK, tid, d_ccol, xc,
+                                                         p.in_scale);
         lds_barrier();  // LDS only: the loads of stage s + 2 stay in flight across the barrier
       }
       if (s + 1 >= nsteps) break;
@@ -962,12 +992,11 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
       {
         const int sl = min(s + 3, nsteps - 1);
         wgrad_load<DCH, XCH, DCPR, XCPR, VEC, ESZ, U8>(dreg2, xreg2, drs, xrs, p, rtab + (sl & 3) * R,
-                                                        m_begin + sl * R, m_end, m_clamped, tid, n0, d_ccol, kval, dt,
-                                                        dh, dw, tapoff);
+                                                        m_begin + sl * R, m_end, m_clamped, tid, n0, d_ccol, xc);
         if (s + 4 < nsteps)
           wgrad_row_table(rtab + ((s + 4) & 3) * R, p, m_begin + (s + 4) * R, m_end, b_first, tid);
         compute(1);
-        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, x_ccol, p.in_scale);
+        wgrad_store<DCH, XCH, DCPR, XCPR, LDN, LDK, U8>(dreg, xreg, Ds, Xs, tid, d_ccol, xc, p.in_scale);
         lds_barrier();
       }
     }
@@ -1817,7 +1846,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 
 template <int TN_, int TK_, bool U8, bool DEEP = false>
 static int launch_wgrad(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + 16)) * 2 + 4 * WG_R * sizeof(int2);
+  const size_t lds = (size_t)2 * WG_R * ((TN_ + 16) + (TK_ + wg_xpad<TK_>())) * 2 + 4 * WG_R * sizeof(int2);
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_kernel<TN_, TK_, U8, DEEP>,
@@ -1845,7 +1874,16 @@ static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
 
 template <int TN_, int TK_>
 static int launch_wgrad_impl(WgradParams& p, int impl, hipStream_t stream) {
-  if constexpr (TN_ % 64 != 0) {
+  if constexpr (TK_ == 192) {
+    // 192-wide K tiles (Ktot = 576, 1152, ...: a third of the dY re-reads of 64-wide tiles)
+    // exist only register-staged (the LDS-DMA mapping needs TK / 8 to divide 64); the 2-deep
+    // variant fits the 256 VGPRs of two waves per SIMD only at TN 64
+    if constexpr (TN_ == 64) {
+      if (impl == 5) return launch_wgrad<TN_, TK_, false, true>(p, stream);
+    }
+    if (impl == 2) return launch_wgrad<TN_, TK_, false>(p, stream);
+    return (int)hipErrorInvalidValue;
+  } else if constexpr (TN_ % 64 != 0) {
     // wide N tiles (96 / 192: Cout = 96, 192, 288, 384, ... without padding) exist only as the
     // register-staged kernels (the LDS-DMA mapping needs TN / 8 to divide 64); the 2-deep
     // variant of 192 x 128 would spill
@@ -1906,6 +1944,9 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
     else if (tn == 96 && tk == 128) rc = launch_wgrad_impl<96, 128>(p, impl, stream);
     else if (tn == 192 && tk == 64) rc = launch_wgrad_impl<192, 64>(p, impl, stream);
     else if (tn == 192 && tk == 128) rc = launch_wgrad_impl<192, 128>(p, impl, stream);
+    else if (tn == 96 && tk == 192) rc = launch_wgrad_impl<96, 192>(p, impl, stream);
+    else if (tn == 128 && tk == 192) rc = launch_wgrad_impl<128, 192>(p, impl, stream);
+    else if (tn == 64 && tk == 192) rc = launch_wgrad_impl<64, 192>(p, impl, stream);
     else rc = (int)hipErrorInvalidValue;
   }
   if (rc) return rc;

@@ -520,6 +520,8 @@ _WIDE_W_IMPLS = {96: (2, 5), 192: (2,)}  # csrc/conv.hip launch_wgrad_impl: regi
 
 
 def _wide_w_impls(tn: int, tk: int) -> Tuple[int, ...]:
+    if tk == 192:  # register-staged only; 2-deep fits at tn 64 (csrc/conv.hip launch_wgrad_impl)
+        return (2, 5) if tn == 64 else (2,)
     if tn == 192 and tk == 64:  # the 2-deep register-staged 192 x 64 tile fits (192 x 128 would spill)
         return (2, 5)
     return _WIDE_W_IMPLS.get(tn, _W_IMPLS)
@@ -532,9 +534,24 @@ _W_TK64 = int(os.environ.get("MILNCE_W_TK64", "1"))
 
 
 def _wgrad_tks(plan: "ConvPlan") -> Tuple[int, ...]:
+    tks = [plan.w_tk]
     if _W_TK64 and plan.w_tk == 128 and (plan.Ktot % 128 != 0 or _W_TK64 == 2):
-        return (128, 64)
-    return (plan.w_tk,)
+        tks.append(64)
+    if _W_TK192 and plan.Ktot % 192 == 0 and plan.Cin % 8 == 0:
+        tks.append(192)
+    return tuple(tks)
+
+
+# 192-wide K tiles where they divide the reduction width (Ktot 576 = 3 x 192: a (3,1,1) or
+# (1,3,3) conv over 192 / 64 channels): each dY tile is re-read Ktot / 192 times instead of
+# Ktot / 64; N tiles 64 / 96 / 128 (csrc/conv.hip). MILNCE_W_TK192=0 disables
+_W_TK192 = os.environ.get("MILNCE_W_TK192", "1") != "0"
+
+
+def _wgrad_tiles_for(Cout: int, tk: int) -> List[int]:
+    if tk == 192:
+        return [t for t in (64, 96, 128) if t <= max(64, _ceil(Cout, 32) * 32)]
+    return _wgrad_tiles(Cout)
 # split-K occupancy candidates (workgroups per CU; more splits hide the wgrad kernels' latency at the
 # price of bigger slabs: same-box bench 66.45 ms with (4, 2), 66.05 with (4, 2, 8), 65.72 with
 # (4, 2, 8, 16)); MILNCE_W_OCCS overrides (A/B runs)
@@ -657,7 +674,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             scratch = torch.empty_like(dw)  # tune on a scratch output: the real one may accumulate
             cands = []
             for tk in _wgrad_tks(plan):
-                for tn in _wgrad_tiles(plan.Cout):
+                for tn in _wgrad_tiles_for(plan.Cout, tk):
                     for impl in _wide_w_impls(tn, tk):
                         for occ in _W_OCCS:
                             cands.append((tn, impl, occ, tk))

@@ -120,7 +120,8 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
 
 
 @pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 176, (1, 1, 1), (0, 0, 0)),
-                                          (96, 288, (3, 1, 1), (1, 0, 0))])
+                                          (96, 288, (3, 1, 1), (1, 0, 0)), (192, 192, (3, 1, 1), (1, 0, 0)),
+                                          (128, 96, (3, 1, 1), (1, 0, 0))])
 def test_wgrad_every_tile_and_variant(cin, cout, k, p):
     """Every (N tile, kernel variant) the wgrad tuner may pick, incl. the wide 96/192 register-staged
     tiles, against fp32 autograd."""
@@ -133,15 +134,18 @@ def test_wgrad_every_tile_and_variant(cin, cout, k, p):
     xr = x.float().requires_grad_(True)
     wr = w.to(torch.bfloat16).float().requires_grad_(True)
     F.conv3d(xr.permute(0, 4, 1, 2, 3), wr, None, 1, p).permute(0, 2, 3, 4, 1).backward(dy.float())
-    tiles = h._wgrad_tiles(cout)
-    assert len(tiles) > 1
-    for tn in tiles:
-        for impl in h._WIDE_W_IMPLS.get(tn, h._W_IMPLS):
-            plan.w_tn, plan.w_impl = tn, impl
-            plan.w_Npad, plan.w_Kpad, plan.w_splits = h._wgrad_geom(cout, plan.Ktot, plan.M, tn, plan.w_tk)
-            dw = h.conv_wgrad(dy, x, plan)
-            assert rel_err(dw, wr.grad) < 1e-2, (tn, impl)
-    plan.w_impl = 0
+    assert len(h._wgrad_tiles(cout)) > 1
+    tk0 = plan.w_tk
+    tks = h._wgrad_tks(plan)
+    assert (192 in tks) == (plan.Ktot % 192 == 0)
+    for tk in tks:  # incl. the 64- and 192-wide K tiles (192: per-chunk X columns, see XCols)
+        for tn in h._wgrad_tiles_for(cout, tk):
+            for impl in h._wide_w_impls(tn, tk):
+                plan.w_tn, plan.w_impl, plan.w_tk = tn, impl, tk
+                plan.w_Npad, plan.w_Kpad, plan.w_splits = h._wgrad_geom(cout, plan.Ktot, plan.M, tn, tk)
+                dw = h.conv_wgrad(dy, x, plan)
+                assert rel_err(dw, wr.grad) < 1e-2, (tn, impl, tk)
+    plan.w_impl, plan.w_tk = 0, tk0
 
 
 def test_stem_uint8():
