@@ -76,7 +76,7 @@ def test_conv_fwd_dgrad_wgrad(case):
 
 
 @pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 192, (3, 1, 1), (1, 0, 0)),
-                                          (256, 288, (1, 1, 1), (0, 0, 0))])
+                                          (256, 288, (1, 1, 1), (0, 0, 0)), (192, 64, (1, 3, 3), (0, 1, 1))])
 def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     """Every forward / dgrad / wgrad kernel variant the autotuner may pick computes the same sums
     in the same order: outputs must be bitwise identical, on a problem large enough (8 clips of
@@ -108,7 +108,9 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
         # group rows differently), their column sums must agree
         sums = val[1].view(-1, 2, npad).double().sum(0)
         # (the LDS-DMA variants sum the stored bf16 outputs, the register-staged one the fp32 ones)
-        assert torch.allclose(sums, ref_sums, rtol=5e-3, atol=5e-2), ("stats", key)
+        # (sum y cancels to ~0 over 160k rows: its absolute tolerance scales with sqrt(sum y^2))
+        atol = (5e-3 * ref_sums[1].sqrt() + 5e-2).expand_as(ref_sums)
+        assert ((sums - ref_sums).abs() <= atol + 5e-3 * ref_sums.abs()).all(), ("stats", key)
     dws = []
     for impl in h._W_IMPLS:
         plan.w_impl = impl
