@@ -1,0 +1,66 @@
+"""Autotuner candidate sets and split-K geometry (pure Python, ops/hip_ops.py): which wgrad K / N
+tiles and kernel variants the tuner may try for the S3D-G layer shapes, and the grad_sink
+deferral bookkeeping used by the side-stream slab reduction."""
+import os
+
+from mil_nce_howto100m_amd.ops import grad_sink
+from mil_nce_howto100m_amd.ops import hip_ops as h
+
+
+def _plan(x_shape, cout, k):
+    pad = tuple(kk // 2 for kk in k)
+    return h.conv_plan(x_shape, (cout, x_shape[-1]) + k, (1, 1, 1), pad)
+
+
+def test_wgrad_k_tiles_follow_the_reduction_width():
+    # (3,1,1) over 192 channels: Ktot 576 -> 128 pads (640), 64 and 192 divide it
+    p = _plan((4, 8, 25, 25, 192), 192, (3, 1, 1))
+    assert p.Ktot == 576 and p.w_tk == 128
+    assert set(h._wgrad_tks(p)) == {128, 64, 192}
+    # 1x1 over 256 channels: 128 divides, 192 does not -> the default only
+    p = _plan((4, 8, 25, 25, 256), 288, (1, 1, 1))
+    assert h._wgrad_tks(p) == (128,)
+    # (1,3,3) over 64 channels: Ktot 576 again
+    p = _plan((4, 8, 50, 50, 64), 192, (1, 3, 3))
+    assert 192 in h._wgrad_tks(p)
+
+
+def test_wgrad_variants_per_tile():
+    # 192-wide K tiles: register-staged only, the 2-deep variant only at N tile 64 (VGPR budget)
+    assert h._wide_w_impls(64, 192) == (2, 5)
+    assert h._wide_w_impls(96, 192) == (2,)
+    assert h._wide_w_impls(128, 192) == (2,)
+    assert h._wide_w_impls(192, 64) == (2, 5)
+    assert h._wide_w_impls(192, 128) == (2,)
+    assert h._wide_w_impls(128, 128) == h._W_IMPLS
+    assert h._wgrad_tiles_for(192, 192) == [64, 96, 128]
+    assert h._wgrad_tiles_for(64, 192) == [64]
+
+
+def test_wgrad_split_geometry():
+    for occ in h._W_OCCS:
+        npad, kpad, splits = h._wgrad_geom(192, 576, 5_120_000, 96, 192, occ)
+        assert npad == 192 and kpad == 576
+        tiles = (npad // 96) * (kpad // 192)
+        # enough workgroups for `occ` per CU, never more splits than 256-row chunks
+        assert splits * tiles >= min(occ * h._NUM_CU, tiles * (5_120_000 // 256))
+        assert splits <= h._ceil(5_120_000, 256)
+    # tiny reduction: one split
+    assert h._wgrad_geom(64, 64, 100, 64, 64, 4)[2] == 1
+
+
+def test_grad_sink_deferral_bookkeeping():
+    class _Ev:
+        pass
+
+    assert grad_sink.pending() == 0
+    grad_sink.defer(_Ev())  # outside a backward pass: no end-of-pass callback, still tracked
+    grad_sink.defer(_Ev())
+    assert grad_sink.pending() == 2
+    grad_sink._PENDING.clear()  # drain() needs a HIP stream; on CPU just reset
+    grad_sink.drain()  # nothing pending: no stream access
+    assert grad_sink.pending() == 0
+
+
+def test_deferred_reduce_is_opt_in():
+    assert h._DEFER_WGRAD == (os.environ.get("MILNCE_DEFER_WGRAD") == "1")
