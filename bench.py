@@ -27,6 +27,12 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 
+def _native_lib() -> str:
+    """File name of the HIP kernel library this process loaded (there is no fallback path)."""
+    from mil_nce_howto100m_amd.ops import _lib
+    return os.path.basename(_lib.LIB_PATH)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +114,14 @@ def main():
     dt = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt)
     final_loss = float(losses[-1].item()) if losses else float("nan")
+    comm = None
+    if ctx.world_size > 1:
+        # after the timed region: the step's collectives alone at the step's sizes (xGMI record)
+        from mil_nce_howto100m_amd.parallel.comm_probe import probe
+        net = trainer.model.module if hasattr(trainer.model, "module") else trainer.model
+        # packed [b video + b*K text] fp32 rows of the embedding width (models/s3dg.py fc)
+        comm = probe(trainer.bucketer.flat.numel(), trainer.bucketer.buckets, b * (1 + opts.num_candidates),
+                     net.fc.out_features, net.fc.weight.dtype, ctx.device)
     if opts.profile_steps and cuda:
         from torch.profiler import ProfilerActivity, profile
         with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
@@ -157,6 +171,10 @@ def main():
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
         }
+        if comm is not None:
+            out["comm"] = comm
+        if cuda:
+            out["kernel_lib"] = _native_lib()
         print(json.dumps(out), flush=True)
     pdist.destroy()
     return 0

@@ -50,6 +50,11 @@ def test_bench_self_launches_n_ranks():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
     assert r["config"]["backend"] == "gloo" and r["config"]["global_batch"] == 4
+    # the step's collectives timed after the timed region (parallel/comm_probe.py)
+    c = r["comm"]
+    assert c["world_size"] == 2 and c["buckets"] >= 1 and c["grad_mib"] > 0
+    assert c["allreduce_ms"] > 0 and c["bucketed_allreduce_ms"] > 0 and c["allgather_ms"] > 0
+    assert c["allgather_kib"] == 2 * 2 * (1 + 4) * 512 * 4 / 1024  # W * b(1+K) rows * 512 fp32
 
 
 def test_bench_world_size_mismatch_fails():
