@@ -1268,11 +1268,18 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16_t* a0, const bf16_t* a1) {
 constexpr int STW_HREG = 13;  // halo pixels per thread (<= 3 * 9 * 116 at 224x224)
 constexpr int STW_DREG = 7;   // dY chunks per thread (<= 224 rows x 8 chunks)
 
-template <bool U8>
-__global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
+// NH output-channel groups: 4 * NH waves, wave = (channel group, K quarter); NH 2 = 8 waves (two
+// per SIMD, 4 x 32 x (11 x 16) accumulator tiles each) so fragment reads overlap another wave's MFMAs.
+template <bool U8, int NH>
+__global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams p) {
+  constexpr int NT = 256 * NH;
+  constexpr int NAF = 4 / NH;                              // dY (A) fragments per wave
+  constexpr int HREG = (STW_HREG * 256 + NT - 1) / NT;     // halo pixels per thread
+  constexpr int DREG = (STW_DREG * 256 + NT - 1) / NT;     // dY chunks per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave % NH, wq = wave / NH;  // channel group, K quarter
   const int hrows = 2 * STW_HR + 5, wpx = p.W2 + 4;
   const int buf_elems = (p.halo_px + p.dy_rows * 8) * 8;  // halo pixels, then dY rows (8 chunks each)
   bf16_t* const buf0 = (bf16_t*)smem;
@@ -1284,15 +1291,15 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
   // register staging (T14): the next item's halo and dY are loaded into VGPRs while the current
   // item is computed from LDS, then written to the other buffer
   using HReg = typename std::conditional<U8, uint2, uint4>::type;
-  HReg hreg[STW_HREG];
-  uint4 dreg[STW_DREG];
+  HReg hreg[HREG];
+  uint4 dreg[DREG];
   auto load = [&](int it) {
     const int hg = it % hg_per, q = it / hg_per;
     const int to = q % p.To, b = q / p.To;
     const int t0 = 2 * to - 1, h0 = 2 * hg * STW_HR - 3;
 #pragma unroll
-    for (int i = 0; i < STW_HREG; ++i) {
-      const int f = tid + 256 * i;
+    for (int i = 0; i < HREG; ++i) {
+      const int f = tid + NT * i;
       const int tt = f / (hrows * wpx), rem = f - tt * (hrows * wpx);
       const int hh = rem / wpx, wp = rem - hh * wpx;
       const int ti = t0 + tt, hi = h0 + hh, wi = wp - 2;
@@ -1303,16 +1310,16 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
     const long long m0 = ((long long)(b * p.To + to) * p.Ho + hg * STW_HR) * p.Wo;
     const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + m0 * 64), (short)0, real_rows * 128, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < STW_DREG; ++i) {
-      const int ch = tid + 256 * i;  // chunk = row * 8 + logical column chunk
+    for (int i = 0; i < DREG; ++i) {
+      const int ch = tid + NT * i;  // chunk = row * 8 + logical column chunk
       const uint32_t off = ch < real_rows * 8 ? (uint32_t)(ch * 16) : 0x80000000u;
       dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
     }
   };
   auto store = [&](bf16_t* base) {
 #pragma unroll
-    for (int i = 0; i < STW_HREG; ++i) {
-      const int f = tid + 256 * i;
+    for (int i = 0; i < HREG; ++i) {
+      const int f = tid + NT * i;
       if constexpr (U8) {  // integer-valued bf16; the 1/255 is applied to the partial dW
         if (f < p.halo_px) *(uint4*)(base + f * 8) = u8x8_to_bf16x8(hreg[i]);
       } else {
@@ -1321,32 +1328,32 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
     }
     bf16_t* D = base + p.halo_px * 8;
 #pragma unroll
-    for (int i = 0; i < STW_DREG; ++i) {
-      const int ch = tid + 256 * i;
+    for (int i = 0; i < DREG; ++i) {
+      const int ch = tid + NT * i;
       const int row = ch >> 3, c = ch & 7;
       if (row < p.dy_rows) *(uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8) = dreg[i];  // tail rows: zeros
     }
   };
 
-  f32x4 acc[4][STW_KFW];
+  f32x4 acc[NAF][STW_KFW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NAF; ++i)
 #pragma unroll
     for (int j = 0; j < STW_KFW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
-  const int kf0 = wave * STW_KFW;
+  const int kf0 = wq * STW_KFW;
   const int nchunks = p.dy_rows / 32;
   // fragments of one 32-position chunk: 4 dY (A) fragments and this wave's 11 X (B) fragments;
   // chunk c + 1's are read while chunk c's 44 MFMAs run (two register sets)
   struct Frags {
-    bf16x8 a[4], b[STW_KFW];
+    bf16x8 a[NAF], b[STW_KFW];
   };
   auto read_frags = [&](const bf16_t* X, int c, Frags& f) {
     const bf16_t* D = X + p.halo_px * 8;
     const int p0 = c * 32;
 #pragma unroll
-    for (int nf = 0; nf < 4; ++nf) f.a[nf] = tr_frag_sw(D, 64, 8, p0, nf * 16, g, qq, pp);
+    for (int nf = 0; nf < NAF; ++nf) f.a[nf] = tr_frag_sw(D, 64, 8, p0, (wn * NAF + nf) * 16, g, qq, pp);
     int pb[2];  // this lane's two positions (rows of the transposed reads): halo pixel bases
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1369,13 +1376,20 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
     for (int j = 0; j < STW_KFW; ++j) {
       if (kf0 + j < STW_KF) {
 #pragma unroll
-        for (int nf = 0; nf < 4; ++nf)
+        for (int nf = 0; nf < NAF; ++nf)
           acc[nf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[nf], f.b[j], acc[nf][j], 0, 0, 0);
       }
     }
   };
   auto compute = [&](const bf16_t* X) {
     Frags f0, f1;
+    if constexpr (NH > 1) {  // one fragment set: the SIMD's other wave covers the read latency
+      for (int c = 0; c < nchunks; ++c) {
+        read_frags(X, c, f0);
+        mfmas(f0);
+      }
+      return;
+    }
     read_frags(X, 0, f0);
     int c = 0;
     for (; c + 2 <= nchunks; c += 2) {
@@ -1403,14 +1417,14 @@ __global__ __launch_bounds__(256, 1) void stem_wgrad_kernel(StemWgradParams p) {
   // partial dW[n][k] of this workgroup: C[i = n][j = k], row n = 4*(lane>>4) + r, col k = lane & 15
   float* out = p.slab + (long long)blockIdx.x * 64 * 672;
 #pragma unroll
-  for (int nf = 0; nf < 4; ++nf)
+  for (int nf = 0; nf < NAF; ++nf)
 #pragma unroll
     for (int j = 0; j < STW_KFW; ++j) {
       const int kf = kf0 + j;
       if (kf < STW_KF) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          out[(long long)(nf * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] =
+          out[(long long)((wn * NAF + nf) * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] =
               U8 ? acc[nf][j][r] * (1.0f / 255.0f) : acc[nf][j][r];
       }
     }
@@ -1438,14 +1452,17 @@ struct StemFwdParams {
   long long x_bytes;
 };
 
-template <int W2, bool U8>
-__global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
-  constexpr int HR = STW_HR, WO = W2, WPX = W2 + 4, HROWS = 2 * HR + 5;
+// HR output rows per item, NPG position groups: 2 * NPG waves (two channel halves per group).
+// NPG 4 = two waves per SIMD, so one wave's fragment reads overlap the other's MFMAs.
+template <int W2, bool U8, int HR, int NPG>
+__global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p) {
+  constexpr int NT = 128 * NPG;
+  constexpr int WO = W2, WPX = W2 + 4, HROWS = 2 * HR + 5;
   constexpr int HALO = 3 * HROWS * WPX;
   constexpr int ROWS = HR * WO;                    // positions per item
   constexpr int PF = (ROWS + 15) / 16;             // 16-position fragments
-  constexpr int PFW = (PF + 1) / 2;                // per wave (position half 0 takes the extra one)
-  constexpr int HREG = (HALO + 255) / 256;
+  constexpr int PFW = (PF + NPG - 1) / NPG;        // per wave (at most)
+  constexpr int HREG = (HALO + NT - 1) / NT;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ws = (bf16_t*)smem;                      // [64][STF_LDW]
   bf16_t* X = Ws + 64 * STF_LDW;                   // [HALO][8]
@@ -1459,7 +1476,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   const int hg_per = p.Ho / HR;
 
   // weight -> LDS (once); for the uint8 clip (integer-valued bf16 halo) scaled by 1/255 here
-  for (int c = tid; c < 64 * 84; c += 256) {
+  for (int c = tid; c < 64 * 84; c += NT) {
     const int n = c / 84, k8 = c - n * 84;
     uint4 wv = *(const uint4*)(p.w + (long long)n * p.Kpad + k8 * 8);
     if constexpr (U8) {
@@ -1488,7 +1505,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   int hgeo[HREG];
 #pragma unroll
   for (int i = 0; i < HREG; ++i) {
-    const int f = tid + 256 * i;
+    const int f = tid + NT * i;
     const int tt = f / (HROWS * WPX), rem = f - tt * (HROWS * WPX);
     const int hh = rem / WPX, wp = rem - hh * WPX;
     hgeo[i] = f < HALO ? (tt | (hh << 2) | (wp << 8)) : -1;
@@ -1510,7 +1527,7 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < HREG; ++i) {
-      const int f = tid + 256 * i;
+      const int f = tid + NT * i;
       if constexpr (U8) {
         if (f < HALO) *(uint4*)(X + f * 8) = hcv[i];
       } else {
@@ -1525,8 +1542,8 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf)
     abase[nf] = (uint32_t)(((nh * 32 + nf * 16 + l16) * STF_LDW + lg * 8) * 2);
-  const int pf0 = ph == 0 ? 0 : PFW;
-  const int npf = ph == 0 ? PFW : PF - PFW;
+  const int pf0 = ph * PF / NPG;  // balanced split of the PF fragments over the groups
+  const int npf = (ph + 1) * PF / NPG - pf0;
 #pragma unroll
   for (int j = 0; j < PFW; ++j) {
     int pos = (pf0 + j) * 16 + l16;
@@ -1621,18 +1638,38 @@ __global__ __launch_bounds__(256, 1) void stem_fwd_kernel(StemFwdParams p) {
   if (tid < 128) p.stats[(long long)blockIdx.x * 128 + tid] = red[tid];
 }
 
-template <int W2, bool U8>
-static int launch_stem_fwd(StemFwdParams& p, int grid, hipStream_t stream) {
-  constexpr int HALO = 3 * (2 * STW_HR + 5) * (W2 + 4);
-  const size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + 128 * 4;
+template <int W2, bool U8, int HR, int NPG>
+static int launch_stem_fwd_t(StemFwdParams& p, int grid, hipStream_t stream) {
+  constexpr int HALO = 3 * (2 * HR + 5) * (W2 + 4);
+  constexpr size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + 128 * 4;
+  static_assert(lds <= 160 * 1024, "stem forward LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_fwd_kernel<W2, U8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_fwd_kernel<W2, U8, HR, NPG>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
-  hipLaunchKernelGGL((stem_fwd_kernel<W2, U8>), dim3(grid), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((stem_fwd_kernel<W2, U8, HR, NPG>), dim3(grid), dim3(128 * NPG), lds, stream, p);
   return (int)hipGetLastError();
+}
+
+// Stem forward variant (MILNCE_STEM_FWD_V, read once): 1 = 4 output rows per item on 8 waves
+// (default), 0 = 2 rows per item on 4 waves (one wave per SIMD, the round-1 kernel).
+static int stem_fwd_variant() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("MILNCE_STEM_FWD_V");
+    v = e ? atoi(e) : 1;
+  }
+  return v;
+}
+
+static int stem_fwd_hr() { return stem_fwd_variant() == 0 ? 2 : 4; }
+
+template <int W2, bool U8>
+static int launch_stem_fwd(StemFwdParams& p, int grid, hipStream_t stream) {
+  if (stem_fwd_variant() == 0) return launch_stem_fwd_t<W2, U8, 2, 2>(p, grid, stream);
+  return launch_stem_fwd_t<W2, U8, 4, 4>(p, grid, stream);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2003,17 +2040,34 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
   if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
-  if (x_u8) hipLaunchKernelGGL(stem_wgrad_kernel<true>, dim3(grid), dim3(256), lds, stream, p);
-  else hipLaunchKernelGGL(stem_wgrad_kernel<false>, dim3(grid), dim3(256), lds, stream, p);
+  // MILNCE_STEM_WGRAD_V (read once): 0 = 4 waves (default), 1 = 8 waves in two channel groups
+  // (same-box bench: no faster, 2.41 vs 2.40 ms: twice the fragment reads per MFMA cancel the
+  // second wave per SIMD)
+  static int variant = -1;
+  if (variant < 0) {
+    const char* e = getenv("MILNCE_STEM_WGRAD_V");
+    variant = e ? atoi(e) : 0;
+  }
+  if (variant == 0) {
+    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 1>), dim3(grid), dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 1>), dim3(grid), dim3(256), lds, stream, p);
+  } else {
+    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 2>), dim3(grid), dim3(512), lds, stream, p);
+    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 2>), dim3(grid), dim3(512), lds, stream, p);
+  }
   HIP_RET(hipGetLastError());
   const long long total = 64LL * 672;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, slab, dw, grid,
@@ -2032,8 +2086,9 @@ MILNCE_API int milnce_stem_fwd(const void* x2, int x_u8, const void* wpacked, in
   p.B = B; p.T = T; p.H = H; p.Kpad = Kpad;
   p.To = (T + 2 - 3) / 2 + 1;
   p.Ho = (H + 6 - 7) / 2 + 1;
-  if (p.Ho % STW_HR || Kpad < 672) return -1;
-  p.nitems = B * p.To * (p.Ho / STW_HR);
+  const int hr = stem_fwd_hr();
+  if (p.Ho % hr || Kpad < 672) return -1;
+  p.nitems = B * p.To * (p.Ho / hr);
   p.x_bytes = (long long)B * T * H * W2 * (x_u8 ? 8 : 16);
   if (p.x_bytes > 0x7FFFFFF0LL) return -1;
   int grid = 256;

