@@ -434,6 +434,11 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 #define V3_PRIO_DEFAULT 1
 #endif
 constexpr bool V3_PRIO = V3_PRIO_DEFAULT;
+// software-pipelined fragment reads inside a stage (BK 64: two k-steps per barrier)
+#ifndef V3_PIPE_DEFAULT
+#define V3_PIPE_DEFAULT 0
+#endif
+constexpr bool V3_PIPE = V3_PIPE_DEFAULT;
 
 // NWM waves along M (each wave a 64 x BN/2 sub-tile, 2 waves along N): BM = 64*NWM rows,
 // 128*NWM threads. NWM = 4 (256 x BN tiles, 8 waves) re-reads each operand byte fewer times.
@@ -598,27 +603,56 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
       if (more) fire(kt + STAGES - 1);
       const bf16_t* a = ring + (kt % STAGES) * STAGE_ELEMS;
       const bf16_t* bsh = a + BM * BK;
+      auto xfrag = [&](int s, int i) {
+        const int row = wr * WM + i * 16 + (lane & 15);
+        return *(const bf16x8*)(a + row * BK + swz<BK>(row, s * 4 + (lane >> 4)) * 8);
+      };
+      auto wfrag = [&](int s, int j) {
+        const int row = wc * WN + j * 16 + (lane & 15);
+        return *(const bf16x8*)(bsh + row * BK + swz<BK>(row, s * 4 + (lane >> 4)) * 8);
+      };
+      if constexpr (V3_PIPE && KSTEPS > 1) {
+        // k-step s+1's fragments are read while k-step s's MFMAs run: its X fragments up front
+        // (4 extra registers each), each W fragment into the register its step-s twin frees
+        bf16x8 xf[TM], xn[TM], wf[TN];
 #pragma unroll
-      for (int s = 0; s < KSTEPS; ++s) {
-        bf16x8 xf[TM], wf[TN];
-        const int chunk = s * 4 + (lane >> 4);
+        for (int i = 0; i < TM; ++i) xf[i] = xfrag(0, i);
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = wr * WM + i * 16 + (lane & 15);
-          xf[i] = *(const bf16x8*)(a + row * BK + swz<BK>(row, chunk) * 8);
+        for (int j = 0; j < TN; ++j) wf[j] = wfrag(0, j);
+#pragma unroll
+        for (int s = 0; s < KSTEPS; ++s) {
+          if (s + 1 < KSTEPS) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) xn[i] = xfrag(s + 1, i);
+          }
+          if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+            if (s + 1 < KSTEPS) wf[j] = wfrag(s + 1, j);
+          }
+          if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) xf[i] = xn[i];
         }
+      } else {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int row = wc * WN + j * 16 + (lane & 15);
-          wf[j] = *(const bf16x8*)(bsh + row * BK + swz<BK>(row, chunk) * 8);
+        for (int s = 0; s < KSTEPS; ++s) {
+          bf16x8 xf[TM], wf[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) xf[i] = xfrag(s, i);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) wf[j] = wfrag(s, j);
+          if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA burst outranks the other workgroup's loads
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+          if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(0);
         }
-        if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(1);  // the MFMA burst outranks the other workgroup's loads
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
-        if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(0);
       }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1216,7 +1250,6 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __res
 // all of its items; one partial [64][672] per workgroup goes to the slab for wgrad_reduce.
 constexpr int STW_HR = 2;
 constexpr int STW_KF = 42;           // 672 / 16
-constexpr int STW_KFW = 11;          // K fragments per wave (11, 11, 11, 9)
 
 // 8 uint8 pixel channels (a width pair of RGB0 pixels) -> the same 8 integers as bf16 (exact:
 // 0..255 need 8 significant bits, so the fp32 value's upper half IS the bf16). The stems convert
@@ -1268,18 +1301,22 @@ __device__ __forceinline__ bf16x8 tr_pair(const bf16_t* a0, const bf16_t* a1) {
 constexpr int STW_HREG = 13;  // halo pixels per thread (<= 3 * 9 * 116 at 224x224)
 constexpr int STW_DREG = 7;   // dY chunks per thread (<= 224 rows x 8 chunks)
 
-// NH output-channel groups: 4 * NH waves, wave = (channel group, K quarter); NH 2 = 8 waves (two
-// per SIMD, 4 x 32 x (11 x 16) accumulator tiles each) so fragment reads overlap another wave's MFMAs.
-template <bool U8, int NH>
-__global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams p) {
-  constexpr int NT = 256 * NH;
-  constexpr int NAF = 4 / NH;                              // dY (A) fragments per wave
+// NKQ waves, one per K range: a wave owns the 64 x (K range x 16) accumulator tile of its range.
+// NKQ 4 (the round-1 kernel) holds 4 x 11 tiles per wave at one wave per SIMD; NKQ 8 holds 4 x 6
+// at two waves per SIMD, so one wave's fragment reads overlap the other's MFMAs (2.73 -> 2.19 ms
+// same-box; splitting the 64 channels over two 8-wave groups instead measured no gain: twice the
+// dY fragment reads per MFMA).
+template <bool U8, int NKQ>
+__global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams p) {
+  constexpr int NT = 64 * NKQ;
+  constexpr int NAF = 4;                                   // dY (A) fragments per wave
+  constexpr int KFW = (STW_KF + NKQ - 1) / NKQ;            // K fragments per wave (at most)
   constexpr int HREG = (STW_HREG * 256 + NT - 1) / NT;     // halo pixels per thread
   constexpr int DREG = (STW_DREG * 256 + NT - 1) / NT;     // dY chunks per thread
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wave % NH, wq = wave / NH;  // channel group, K quarter
+  const int wq = wave;  // K range
   const int hrows = 2 * STW_HR + 5, wpx = p.W2 + 4;
   const int buf_elems = (p.halo_px + p.dy_rows * 8) * 8;  // halo pixels, then dY rows (8 chunks each)
   bf16_t* const buf0 = (bf16_t*)smem;
@@ -1335,25 +1372,25 @@ __global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams
     }
   };
 
-  f32x4 acc[NAF][STW_KFW];
+  f32x4 acc[NAF][KFW];
 #pragma unroll
   for (int i = 0; i < NAF; ++i)
 #pragma unroll
-    for (int j = 0; j < STW_KFW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < KFW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
-  const int kf0 = wq * STW_KFW;
+  const int kf0 = wq * STW_KF / NKQ, kf_end = (wq + 1) * STW_KF / NKQ;  // balanced K ranges
   const int nchunks = p.dy_rows / 32;
   // fragments of one 32-position chunk: 4 dY (A) fragments and this wave's 11 X (B) fragments;
   // chunk c + 1's are read while chunk c's 44 MFMAs run (two register sets)
   struct Frags {
-    bf16x8 a[NAF], b[STW_KFW];
+    bf16x8 a[NAF], b[KFW];
   };
   auto read_frags = [&](const bf16_t* X, int c, Frags& f) {
     const bf16_t* D = X + p.halo_px * 8;
     const int p0 = c * 32;
 #pragma unroll
-    for (int nf = 0; nf < NAF; ++nf) f.a[nf] = tr_frag_sw(D, 64, 8, p0, (wn * NAF + nf) * 16, g, qq, pp);
+    for (int nf = 0; nf < NAF; ++nf) f.a[nf] = tr_frag_sw(D, 64, 8, p0, nf * 16, g, qq, pp);
     int pb[2];  // this lane's two positions (rows of the transposed reads): halo pixel bases
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1363,7 +1400,7 @@ __global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams
       pb[h] = (2 * hr) * wpx + wo;
     }
 #pragma unroll
-    for (int j = 0; j < STW_KFW; ++j) {
+    for (int j = 0; j < KFW; ++j) {
       const int kf = min(kf0 + j, STW_KF - 1);
       const int tr = kf >> 1;  // (dt, dh) tap row
       const int dt = tr / 7, dh = tr - 7 * (tr / 7);
@@ -1373,8 +1410,8 @@ __global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams
   };
   auto mfmas = [&](const Frags& f) {
 #pragma unroll
-    for (int j = 0; j < STW_KFW; ++j) {
-      if (kf0 + j < STW_KF) {
+    for (int j = 0; j < KFW; ++j) {
+      if (kf0 + j < kf_end) {
 #pragma unroll
         for (int nf = 0; nf < NAF; ++nf)
           acc[nf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[nf], f.b[j], acc[nf][j], 0, 0, 0);
@@ -1383,7 +1420,7 @@ __global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams
   };
   auto compute = [&](const bf16_t* X) {
     Frags f0, f1;
-    if constexpr (NH > 1) {  // one fragment set: the SIMD's other wave covers the read latency
+    if constexpr (NT > 256) {  // one fragment set: the SIMD's other wave covers the read latency
       for (int c = 0; c < nchunks; ++c) {
         read_frags(X, c, f0);
         mfmas(f0);
@@ -1419,12 +1456,12 @@ __global__ __launch_bounds__(256 * NH, 1) void stem_wgrad_kernel(StemWgradParams
 #pragma unroll
   for (int nf = 0; nf < NAF; ++nf)
 #pragma unroll
-    for (int j = 0; j < STW_KFW; ++j) {
+    for (int j = 0; j < KFW; ++j) {
       const int kf = kf0 + j;
-      if (kf < STW_KF) {
+      if (kf < kf_end) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          out[(long long)((wn * NAF + nf) * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] =
+          out[(long long)(nf * 16 + (lane >> 4) * 4 + r) * 672 + kf * 16 + (lane & 15)] =
               U8 ? acc[nf][j][r] * (1.0f / 255.0f) : acc[nf][j][r];
       }
     }
@@ -2040,33 +2077,31 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 1>,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 4>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 1>,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 4>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 2>,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 8>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 2>,
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 8>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
   if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
-  // MILNCE_STEM_WGRAD_V (read once): 0 = 4 waves (default), 1 = 8 waves in two channel groups
-  // (same-box bench: no faster, 2.41 vs 2.40 ms: twice the fragment reads per MFMA cancel the
-  // second wave per SIMD)
+  // MILNCE_STEM_WGRAD_V (read once): 2 = 8 waves over K eighths (default), 0 = 4 waves
   static int variant = -1;
   if (variant < 0) {
     const char* e = getenv("MILNCE_STEM_WGRAD_V");
-    variant = e ? atoi(e) : 0;
+    variant = e ? atoi(e) : 2;
   }
   if (variant == 0) {
-    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 1>), dim3(grid), dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 1>), dim3(grid), dim3(256), lds, stream, p);
+    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 4>), dim3(grid), dim3(256), lds, stream, p);
+    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 4>), dim3(grid), dim3(256), lds, stream, p);
   } else {
-    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 2>), dim3(grid), dim3(512), lds, stream, p);
-    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 2>), dim3(grid), dim3(512), lds, stream, p);
+    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 8>), dim3(grid), dim3(512), lds, stream, p);
+    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 8>), dim3(grid), dim3(512), lds, stream, p);
   }
   HIP_RET(hipGetLastError());
   const long long total = 64LL * 672;
