@@ -436,7 +436,7 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 constexpr bool V3_PRIO = V3_PRIO_DEFAULT;
 // software-pipelined fragment reads inside a stage (BK 64: two k-steps per barrier)
 #ifndef V3_PIPE_DEFAULT
-#define V3_PIPE_DEFAULT 0
+#define V3_PIPE_DEFAULT 1
 #endif
 constexpr bool V3_PIPE = V3_PIPE_DEFAULT;
 
@@ -1289,6 +1289,15 @@ struct StemWgradParams {
   int halo_px;       // 3 * (2*HR+5) * (W2+4)
   int dy_rows;       // HR * Wo rounded up to 32 (MFMA reduction chunks; tail rows are zero)
   long long x_bytes, dy_bytes;
+  // POOL kernels: dY is not read but rebuilt per item from the maxpool_2a backward and the stem's
+  // BN backward (csrc/pool.hip POOL_BWD_APPLY, same arithmetic and roundings): pdy / parg = the
+  // pooled gradient and uint8 arg-max [B, To, Ho/2, Wo/2, 64], ybn = the raw stem output [M, 64],
+  // ss = [mean, invstd, scale, shift], coef = [k0, k1, k2] (64 each)
+  const bf16_t* pdy;
+  const uint8_t* parg;
+  const bf16_t* ybn;
+  const float* ss;
+  const float* coef;
 };
 
 __device__ __forceinline__ bf16x8 tr_pair(const bf16_t* a0, const bf16_t* a1) {
@@ -1306,9 +1315,17 @@ constexpr int STW_DREG = 7;   // dY chunks per thread (<= 224 rows x 8 chunks)
 // at two waves per SIMD, so one wave's fragment reads overlap the other's MFMAs (2.73 -> 2.19 ms
 // same-box; splitting the 64 channels over two 8-wave groups instead measured no gain: twice the
 // dY fragment reads per MFMA).
-template <bool U8, int NKQ>
+// POOL: the item's two dY rows are one row of 2x2 quads of the 1x3x3 / (1,2,2) TF-SAME pool
+// (maxpool_2a): each thread gathers a quad's 4 pooled cells + arg-max bytes one item ahead (the
+// raw stem rows arrive in the D image by LDS-DMA), and the LDS store computes dz (pool_bwd_quad
+// order) and the BN backward dy = k0 (dz mask - k1 - xhat k2) in place: the full-resolution dy is
+// never written or read. Opt-in (hip_ops MILNCE_STEM_POOL_WGRAD=1): 3.68 ms against 2.19 + 1.09
+// for the BN-apply pass and the plain wgrad (same box): the gather registers push the kernel into
+// ~15 VGPR spills at two waves per SIMD and the per-item apply sits between compute and barrier.
+template <bool U8, int NKQ, bool POOL = false>
 __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams p) {
   constexpr int NT = 64 * NKQ;
+  constexpr int QREG = POOL ? (112 / 2 * 8 + NT - 1) / NT : 1;  // quad chunks per thread (Wo <= 112)
   constexpr int NAF = 4;                                   // dY (A) fragments per wave
   constexpr int KFW = (STW_KF + NKQ - 1) / NKQ;            // K fragments per wave (at most)
   constexpr int HREG = (STW_HREG * 256 + NT - 1) / NT;     // halo pixels per thread
@@ -1329,8 +1346,13 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
   // item is computed from LDS, then written to the other buffer
   using HReg = typename std::conditional<U8, uint2, uint4>::type;
   HReg hreg[HREG];
-  uint4 dreg[DREG];
-  auto load = [&](int it) {
+  uint4 dreg[POOL ? 1 : DREG];
+  uint4 qg[QREG][4];
+  uint2 qa[QREG][4];
+  const int nquad = (p.Wo / 2) * 8;  // quad chunks per item: (w2, 8-channel chunk)
+  float* bnc = (float*)(smem + 2 * (size_t)buf_elems * 2);  // POOL: [7][64] ss and coef
+  // dst: the LDS buffer the item will be staged in (POOL: its raw stem rows go there by LDS-DMA)
+  auto load = [&](int it, bf16_t* dst) {
     const int hg = it % hg_per, q = it / hg_per;
     const int to = q % p.To, b = q / p.To;
     const int t0 = 2 * to - 1, h0 = 2 * hg * STW_HR - 3;
@@ -1345,12 +1367,49 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
       hreg[i] = stem_px_load<U8>(xrs, v, ((b * p.T + ti) * p.H + hi) * p.W2 + wi);
     }
     const long long m0 = ((long long)(b * p.To + to) * p.Ho + hg * STW_HR) * p.Wo;
-    const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + m0 * 64), (short)0, real_rows * 128, 0x00020000);
+    if constexpr (POOL) {
+      static_assert(STW_HR == 2, "one quad row per item");
+      const int Hp = p.Ho / 2, Wp = p.Wo / 2;
+      const long long pbase = (long long)(b * p.To + to) * Hp;  // pooled row index of (b, to, 0)
+      const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.pdy + pbase * Wp * 64), (short)0,
+                                                         Hp * Wp * 128, 0x00020000);
+      const auto ars = __builtin_amdgcn_make_buffer_rsrc((void*)(p.parg + pbase * Wp * 64), (short)0,
+                                                         Hp * Wp * 64, 0x00020000);
+      const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.ybn + m0 * 64), (short)0, real_rows * 128,
+                                                         0x00020000);
+      // raw stem rows -> the D image by LDS-DMA: 1-KiB piece j holds chunks 64 j .. 64 j + 63 in
+      // lane order, the lane loading the source chunk its swizzled slot holds
+      char* dimg = (char*)(dst + p.halo_px * 8);
+      for (int j = wave; j * 64 < real_rows * 8; j += NKQ) {
+        const int ch = j * 64 + lane, row = ch >> 3;
+        const uint32_t off = ch < real_rows * 8 ? (uint32_t)(row * 128 + wg_swz(row, ch & 7, 8) * 16) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(yrs, (lds_ptr_t)(dimg + j * 1024), 16, off, 0, 0, 0);
+      }
 #pragma unroll
-    for (int i = 0; i < DREG; ++i) {
-      const int ch = tid + NT * i;  // chunk = row * 8 + logical column chunk
-      const uint32_t off = ch < real_rows * 8 ? (uint32_t)(ch * 16) : 0x80000000u;
-      dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+      for (int i = 0; i < QREG; ++i) {
+        const int qc = tid + NT * i;
+        const bool act = qc < nquad;
+        const int w2 = qc >> 3, c8 = (qc & 7) * 8;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {  // pooled cells (hg - jh, w2 - jw), u = 2 jh + jw
+          const int ho = hg - (u >> 1), wo = w2 - (u & 1);
+          const bool ok = act & (ho >= 0) & (wo >= 0);
+          const uint32_t cell = (uint32_t)(ho * Wp + wo);
+          qg[i][u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    prs, ok ? cell * 128 + c8 * 2 : 0x80000000u, 0, 0));
+          qa[i][u] = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(
+                                                    ars, ok ? cell * 64 + c8 : 0x80000000u, 0, 0));
+        }
+      }
+    } else {
+      const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + m0 * 64), (short)0, real_rows * 128,
+                                                         0x00020000);
+#pragma unroll
+      for (int i = 0; i < DREG; ++i) {
+        const int ch = tid + NT * i;  // chunk = row * 8 + logical column chunk
+        const uint32_t off = ch < real_rows * 8 ? (uint32_t)(ch * 16) : 0x80000000u;
+        dreg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+      }
     }
   };
   auto store = [&](bf16_t* base) {
@@ -1364,11 +1423,54 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
       }
     }
     bf16_t* D = base + p.halo_px * 8;
+    if constexpr (POOL) {
 #pragma unroll
-    for (int i = 0; i < DREG; ++i) {
-      const int ch = tid + NT * i;
-      const int row = ch >> 3, c = ch & 7;
-      if (row < p.dy_rows) *(uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8) = dreg[i];  // tail rows: zeros
+      for (int i = 0; i < QREG; ++i) {
+        const int qc = tid + NT * i;
+        if (qc >= nquad) continue;
+        const int w2 = qc >> 3, c = qc & 7;
+        // pool_bwd_quad: input (eh, ew) of the quad takes pooled cell u = (jh, jw) when its
+        // arg-max tap is (eh + 2 jh) * 3 + (ew + 2 jw); summed over u in the same order
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float dz[8], yv[8], o[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) dz[k] = 0.f;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int dh = (e >> 1) + 2 * (u >> 1), dw = (e & 1) + 2 * (u & 1);
+            if (dh >= 3 || dw >= 3) continue;  // compile-time after unrolling
+            const uint32_t tap = (uint32_t)(dh * 3 + dw);
+            float gf[8];
+            unpack8(qg[i][u], gf);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const uint32_t ak = ((k < 4 ? qa[i][u].x : qa[i][u].y) >> (8 * (k & 3))) & 0xff;
+              dz[k] += (ak == tap) ? gf[k] : 0.f;  // out-of-range cells loaded as zero gradient
+            }
+          }
+          // BN backward as csrc/pool.hip bn_apply, on the bf16-rounded dz
+          const int row = (e >> 1) * p.Wo + 2 * w2 + (e & 1);
+          uint4* slot = (uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8);  // raw y in, dy out
+          unpack8(pack8(dz), dz);
+          unpack8(*slot, yv);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int ch = c * 8 + k;
+            const float gm = (yv[k] * bnc[128 + ch] + bnc[192 + ch] > 0.f) ? dz[k] : 0.f;
+            const float xh = (yv[k] - bnc[ch]) * bnc[64 + ch];
+            o[k] = bnc[256 + ch] * (gm - bnc[320 + ch] - xh * bnc[384 + ch]);
+          }
+          *slot = pack8(o);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < DREG; ++i) {
+        const int ch = tid + NT * i;
+        const int row = ch >> 3, c = ch & 7;
+        if (row < p.dy_rows) *(uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8) = dreg[i];  // tail rows: zeros
+      }
     }
   };
 
@@ -1438,17 +1540,33 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
     if (c < nchunks) mfmas(f0);
   };
 
+  if constexpr (POOL) {
+    // BN constants, and the tail rows past the item's positions (never written by the quads: zero)
+    for (int t = tid; t < 7 * 64; t += NT) bnc[t] = t < 256 ? p.ss[t] : p.coef[t - 256];
+    for (int t = tid; t < (p.dy_rows - real_rows) * 8 * 2; t += NT) {
+      bf16_t* D = (t < (p.dy_rows - real_rows) * 8 ? buf0 : buf1) + p.halo_px * 8;
+      const int ch = t % ((p.dy_rows - real_rows) * 8);
+      const int row = real_rows + (ch >> 3), c = ch & 7;
+      *(uint4*)(D + row * 64 + wg_swz(row, c, 8) * 8) = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+  }
   int it = blockIdx.x;
   if (it < p.nitems) {
-    load(it);
+    load(it, buf0);
+    if constexpr (POOL) __syncthreads();  // the LDS-DMA'd stem rows landed (vmcnt(0) + barrier)
     store(buf0);
   }
   __syncthreads();
   for (int k = 0; it < p.nitems; it += gridDim.x, ++k) {
-    const bool more = it + (int)gridDim.x < p.nitems;
-    if (more) load(it + gridDim.x);
+    const bool more = it + (int)gridDim.x < p.nitems;  // workgroup-uniform
+    bf16_t* next = (k & 1) ? buf0 : buf1;
+    if (more) load(it + gridDim.x, next);
     compute((k & 1) ? buf1 : buf0);
-    if (more) store((k & 1) ? buf0 : buf1);
+    if (more) {
+      if constexpr (POOL) __syncthreads();
+      store(next);
+    }
     __syncthreads();
   }
   // partial dW[n][k] of this workgroup: C[i = n][j = k], row n = 4*(lane>>4) + r, col k = lane & 15
@@ -2057,11 +2175,23 @@ MILNCE_API int milnce_pack_weight(const float* w, void* out, int Cout, int Cin, 
 // Stem wgrad (see stem_wgrad_kernel): dW2 [64][8][3][7][4] (accumulated if `accumulate`).
 // x2 is the bf16 clip as width pairs [B,T,H,W2,8], or (x_u8) the native uint8 clip read the same way.
 // Returns hipErrorInvalidValue for geometries it does not cover (caller falls back).
-MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float* slab, long long slab_floats,
-                                 float* dw, int B, int T, int H, int W2, int accumulate, hipStream_t stream) {
-  StemWgradParams p;
-  p.dy = (const bf16_t*)dy; p.x = (const bf16_t*)x2; p.slab = slab;
-  p.B = B; p.T = T; p.H = H; p.W2 = W2;
+template <bool U8, int NKQ, bool POOL>
+static int stem_wgrad_launch(const StemWgradParams& p, int grid, size_t lds, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<U8, NKQ, POOL>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((stem_wgrad_kernel<U8, NKQ, POOL>), dim3(grid), dim3(64 * NKQ), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
+// pdy != nullptr: the POOL kernel (dY rebuilt from the maxpool_2a backward + BN backward, see
+// stem_wgrad_kernel); dy is then unused.
+static int stem_wgrad_impl(StemWgradParams& p, int x_u8, long long slab_floats, float* dw, int accumulate,
+                           hipStream_t stream) {
+  const int B = p.B, T = p.T, H = p.H, W2 = p.W2;
   p.To = (T + 2 - 3) / 2 + 1;
   p.Ho = (H + 6 - 7) / 2 + 1;
   p.Wo = W2;
@@ -2069,24 +2199,14 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float
   p.nitems = B * p.To * (p.Ho / STW_HR);
   p.halo_px = 3 * (2 * STW_HR + 5) * (W2 + 4);
   if (p.halo_px > 256 * STW_HREG || STW_HR * p.Wo > 32 * STW_DREG) return (int)hipErrorInvalidValue;
+  const bool pool = p.pdy != nullptr;
+  if (pool && (p.Wo % 2 || p.Wo > 112 || p.Ho % 2)) return (int)hipErrorInvalidValue;
   p.dy_rows = (STW_HR * p.Wo + 31) / 32 * 32;
   p.x_bytes = (long long)B * T * H * W2 * (x_u8 ? 8 : 16);
   p.dy_bytes = (long long)B * p.To * p.Ho * p.Wo * 128;
   if (p.x_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
-  const size_t lds = (size_t)2 * (p.halo_px + p.dy_rows * 8) * 16;
+  const size_t lds = (size_t)2 * (p.halo_px + p.dy_rows * 8) * 16 + (pool ? 7 * 64 * 4 : 0);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 4>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 4>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<false, 8>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_RET(hipFuncSetAttribute((const void*)stem_wgrad_kernel<true, 8>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
   if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
@@ -2096,18 +2216,43 @@ MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float
     const char* e = getenv("MILNCE_STEM_WGRAD_V");
     variant = e ? atoi(e) : 2;
   }
-  if (variant == 0) {
-    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 4>), dim3(grid), dim3(256), lds, stream, p);
-    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 4>), dim3(grid), dim3(256), lds, stream, p);
-  } else {
-    if (x_u8) hipLaunchKernelGGL((stem_wgrad_kernel<true, 8>), dim3(grid), dim3(512), lds, stream, p);
-    else hipLaunchKernelGGL((stem_wgrad_kernel<false, 8>), dim3(grid), dim3(512), lds, stream, p);
-  }
-  HIP_RET(hipGetLastError());
+  int rc;
+  if (pool) rc = x_u8 ? stem_wgrad_launch<true, 8, true>(p, grid, lds, stream)
+                      : stem_wgrad_launch<false, 8, true>(p, grid, lds, stream);
+  else if (variant == 0) rc = x_u8 ? stem_wgrad_launch<true, 4, false>(p, grid, lds, stream)
+                                   : stem_wgrad_launch<false, 4, false>(p, grid, lds, stream);
+  else rc = x_u8 ? stem_wgrad_launch<true, 8, false>(p, grid, lds, stream)
+                 : stem_wgrad_launch<false, 8, false>(p, grid, lds, stream);
+  if (rc) return rc;
   const long long total = 64LL * 672;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, slab, dw, grid,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, p.slab, dw, grid,
                      64, 672, 64, 8, 8, 84, accumulate);
   return (int)hipGetLastError();
+}
+
+MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float* slab, long long slab_floats,
+                                 float* dw, int B, int T, int H, int W2, int accumulate, hipStream_t stream) {
+  StemWgradParams p = {};
+  p.dy = (const bf16_t*)dy; p.x = (const bf16_t*)x2; p.slab = slab;
+  p.B = B; p.T = T; p.H = H; p.W2 = W2;
+  return stem_wgrad_impl(p, x_u8, slab_floats, dw, accumulate, stream);
+}
+
+// Stem wgrad straight from the maxpool_2a backward: pdy / parg = the pooled gradient and arg-max
+// [B, To, Ho/2, Wo/2, 64], y = the raw stem output [M, 64], ss / coef = the stem BN's
+// [mean, invstd, scale, shift] and finalised backward coefficients [k0, k1, k2] (milnce_bn_bwd_finalize).
+// Same dW as milnce_maxpool_bwd_apply into dy followed by milnce_stem_wgrad, without the dy tensor.
+MILNCE_API int milnce_stem_wgrad_pool(const void* pdy, const void* parg, const void* y, const float* ss,
+                                      const float* coef, const void* x2, int x_u8, float* slab,
+                                      long long slab_floats, float* dw, int B, int T, int H, int W2, int accumulate,
+                                      hipStream_t stream) {
+  StemWgradParams p = {};
+  p.x = (const bf16_t*)x2; p.slab = slab;
+  p.B = B; p.T = T; p.H = H; p.W2 = W2;
+  p.pdy = (const bf16_t*)pdy; p.parg = (const uint8_t*)parg; p.ybn = (const bf16_t*)y;
+  p.ss = ss; p.coef = coef;
+  if (!pdy || !parg || !y || !ss || !coef) return (int)hipErrorInvalidValue;
+  return stem_wgrad_impl(p, x_u8, slab_floats, dw, accumulate, stream);
 }
 
 // Stem forward (see stem_fwd_kernel): y [M, 64] bf16 and BN partials stats[nparts][2][64];

@@ -45,6 +45,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_set_pool_s1_impl": [I],
     "milnce_set_pool_s1_maxthr": [I],
     "milnce_stem_wgrad": [P, P, I, P, L, P, I, I, I, I, I, P],
+    "milnce_stem_wgrad_pool": [P, P, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
     "milnce_stem_fwd": [P, I, P, I, P, P, L, I, I, I, I, P],
     "milnce_maxpool_bwd_gate": [P, P, P] + [I] * 21 + [P, P, I, P],
     "milnce_bn_relu_gate_maxpool_fwd": [P, P, P, P, P] + [I] * 21 + [P],

@@ -733,6 +733,42 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     return plan, y, ss
 
 
+# Stem wgrad straight from the maxpool_2a backward (csrc/conv.hip stem_wgrad_kernel POOL): the BN
+# backward's dy of the stem is rebuilt per item from the pooled gradient, arg-max and raw stem
+# output instead of being written by milnce_maxpool_bwd_apply and read back. Opt-in
+# (MILNCE_STEM_POOL_WGRAD=1): same-box bench 4140 pairs/s without, 4121 with (the fused kernel's
+# register pressure costs more than the dy round trip it saves; csrc/conv.hip stem_wgrad_kernel).
+_STEM_POOL_WGRAD = os.environ.get("MILNCE_STEM_POOL_WGRAD", "0") == "1"
+
+
+def _stem_pool_wgrad_ok(plan: ConvPlan, lazy, x: torch.Tensor, C: int) -> bool:
+    if not (_STEM_POOL_WGRAD and _STEM_WGRAD and lazy[0] == "pool" and lazy[4] is None and C == 64
+            and _is_paired_stem(plan) and x.dtype in (BF16, torch.uint8)):
+        return False
+    geo = lazy[3]
+    B, T, H, W, _, To, Ho, Wo = geo[:8]
+    # (1,3,3) window, (1,2,2) stride, TF-SAME pads (0,0 / 0,1 / 0,1) over an even plane: 2x2 quads
+    return (tuple(geo[8:14]) == (1, 3, 3, 1, 2, 2) and tuple(geo[14:20]) == (0, 0, 0, 1, 0, 1)
+            and H == 2 * Ho and W == 2 * Wo and To == T)
+
+
+def _stem_pool_wgrad(lazy, x, y, ss, coef, weight, plan: ConvPlan) -> Optional[torch.Tensor]:
+    _, dout, arg, geo, _, _, _ = lazy
+    w_direct = _direct_grad(weight)
+    dw = w_direct if w_direct is not None else torch.empty(
+        (plan.Cout, plan.Cin_p) + tuple(plan.k), dtype=F32, device=dout.device)
+    slab = torch.empty((256 * 64 * 672,), dtype=F32, device=dout.device)
+    rc = lib().milnce_stem_wgrad_pool(ptr(dout), ptr(arg), ptr(y), ptr(ss), ptr(coef), ptr(x),
+                                      int(x.dtype == torch.uint8), ptr(slab), slab.numel(), ptr(dw), plan.B, plan.T,
+                                      plan.H, plan.W, int(w_direct is not None), stream())
+    if rc != 0:
+        raise RuntimeError(f"milnce_stem_wgrad_pool failed ({rc}) for {plan}")
+    if w_direct is not None:
+        _grad_done(weight)
+        return None
+    return dw
+
+
 def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     """Backward of conv -> BN -> ReLU from dz (grad of the ReLU output): BN backward (fused
     partials when the producer of dz attached them), dgrad, wgrad; BN and weight gradients are
@@ -758,6 +794,17 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     direct_bn = g_direct is not None and b_direct is not None
     dgamma = g_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
     dbeta = b_direct if direct_bn else torch.empty((C,), dtype=F32, device=dev)
+    if (lazy is not None and not ctx.needs_input_grad[0] and ctx.needs_input_grad[1]
+            and _stem_pool_wgrad_ok(plan, lazy, x, C)):
+        # stem -> maxpool_2a: the stem wgrad rebuilds dy from the pooled gradient (no dy tensor)
+        call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(plan.M), ptr(gamma), ptr(ss), ptr(dgamma),
+             ptr(dbeta), ptr(coef), int(direct_bn), int(ctx.training), stream())
+        if direct_bn:
+            _grad_done(gamma)
+            _grad_done(beta)
+            dgamma = dbeta = None
+        dw = _stem_pool_wgrad(lazy, x, y, ss, coef, weight, plan)
+        return None, dw, dgamma, dbeta
     dy = torch.empty_like(y)
     if lazy is not None:
         _bn_bwd_lazy(lazy, plan.B, plan.M, y, C, ss, C, gamma, part, nparts, ps, dgamma, dbeta, coef, dy, C,

@@ -538,6 +538,37 @@ def test_stem_bn_relu_pool_fused_matches_unfused():
     assert torch.equal(bns[0].running_mean, bns[1].running_mean)
 
 
+@pytest.mark.parametrize("S,u8", [(64, True), (64, False), (200, True)])
+def test_stem_wgrad_from_pool_gradient(S, u8):
+    """Stem wgrad straight from the maxpool_2a backward (dy rebuilt per item from the pooled
+    gradient, arg-max and raw stem output inside the wgrad kernel) == the unfused path (pool
+    backward BN-apply pass writing dy, then the stem wgrad): weight, BN gamma / beta gradients."""
+    torch.manual_seed(21)
+    h = hip()
+    B, T = 2, 4
+    u8c = torch.randint(0, 256, (B, T, S, S, 4), dtype=torch.uint8, device=DEV)
+    u8c[..., 3] = 0
+    x = h.prepare_stem_input(u8c, native=True, keep_u8=u8)
+    conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
+    bns = [nn.BatchNorm3d(64).to(DEV) for _ in range(2)]
+    bns[1].load_state_dict(bns[0].state_dict())
+    ws = [conv.weight.detach().clone().requires_grad_(True) for _ in range(2)]
+    g = None
+    old = h._STEM_POOL_WGRAD
+    try:
+        for i, fused in enumerate((True, False)):
+            h._STEM_POOL_WGRAD = fused
+            out = h.stem_conv_bn_relu_pool(x, ws[i], bns[i], True, (1, 3, 3), (1, 2, 2))
+            if g is None:
+                g = torch.randn_like(out.float()).to(torch.bfloat16)
+            out.backward(g)
+    finally:
+        h._STEM_POOL_WGRAD = old
+    assert rel_err(ws[0].grad, ws[1].grad) < 1e-5
+    assert rel_err(bns[0].weight.grad, bns[1].weight.grad) < 1e-6
+    assert rel_err(bns[0].bias.grad, bns[1].bias.grad) < 1e-6
+
+
 @pytest.mark.parametrize("S,fused", [(64, True), (64, False), (20, False), (200, True)])
 def test_stem_uint8_input(S, fused):
     """The stem on the native uint8 clip (no bf16 copy of the clip: the kernels stage it as
