@@ -439,6 +439,11 @@ constexpr bool V3_PRIO = V3_PRIO_DEFAULT;
 #define V3_PIPE_DEFAULT 1
 #endif
 constexpr bool V3_PIPE = V3_PIPE_DEFAULT;
+// the same for the register-staged wgrad (conv_wgrad_kernel)
+#ifndef WG_PIPE_DEFAULT
+#define WG_PIPE_DEFAULT 0
+#endif
+constexpr bool WG_PIPE = WG_PIPE_DEFAULT;
 
 // NWM waves along M (each wave a 64 x BN/2 sub-tile, 2 waves along N): BM = 64*NWM rows,
 // 128*NWM threads. NWM = 4 (256 x BN tiles, 8 waves) re-reads each operand byte fewer times.
@@ -958,6 +963,33 @@ __global__ __launch_bounds__(256, 2) void conv_wgrad_kernel(WgradParams p) {
   auto compute = [&](int buf) {
     const bf16_t* d = Ds + buf * R * LDN;
     const bf16_t* x = Xs + buf * R * LDK;
+    if constexpr (WG_PIPE && R / 32 > 1) {
+      // k-step ks+1's fragments are read under k-step ks's MFMAs: its X fragments up front, each
+      // dY fragment into the register its step-ks twin frees after its row of MFMAs
+      bf16x8 af[TI], bfr[TJ], bn[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = tr_frag(d, LDN, 0, wr * WN + i * 16, g, q, pp);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = tr_frag(x, LDK, 0, wc * WK + j * 16, g, q, pp);
+#pragma unroll
+      for (int ks = 0; ks < R / 32; ++ks) {
+        const bool more = ks + 1 < R / 32;
+        if (more) {
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) bn[j] = tr_frag(x, LDK, (ks + 1) * 32, wc * WK + j * 16, g, q, pp);
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          if (more) af[i] = tr_frag(d, LDN, (ks + 1) * 32, wr * WN + i * 16, g, q, pp);
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfr[j] = bn[j];
+      }
+      return;
+    }
 #pragma unroll
     for (int ks = 0; ks < R / 32; ++ks) {
       bf16x8 af[TI], bfr[TJ];
