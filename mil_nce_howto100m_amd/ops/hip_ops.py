@@ -148,6 +148,37 @@ _FWD_WGS_PER_CU = int(os.environ.get("MILNCE_FWD_WGS", "2"))
 _WIDE_IMPLS = {96: (3, 4), 160: (3, 4), 192: (3, 4, 5)}
 
 
+# persistent grid sizes (workgroups per CU) the forward / dgrad tuner tries per shape next to the
+# kernel variant: narrow tiles (BN 64: 48 KiB of LDS) fit three workgroups per CU, where the global
+# default of two leaves a third of the LDS idle. MILNCE_FWD_WGS_TUNE="2" restores the fixed grid.
+_FWD_WGS_TUNE = tuple(int(v) for v in os.environ.get("MILNCE_FWD_WGS_TUNE", "2,3").split(","))
+
+
+def _grid_for(M: int, npad: int, bn: int, wgs: int) -> int:
+    return max(1, min(_ceil(M, 128), _ceil(wgs * _NUM_CU, npad // bn)))
+
+
+def _stats_rows(M: int, npad: int, bn: int) -> int:
+    """Partial-statistics rows to allocate: the largest grid the tuner may pick."""
+    return max(_grid_for(M, npad, bn, w) for w in (_FWD_WGS_PER_CU,) + _FWD_WGS_TUNE)
+
+
+def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
+              max_rows: Optional[int] = None) -> Tuple[int, int]:
+    """(impl, grid) of the fastest (kernel variant, persistent grid) pair; launch(impl, grid).
+    Grids with more partial-statistics rows than ``max_rows`` (the caller's buffer) are skipped."""
+    wgs = tuple(w for w in dict.fromkeys((_FWD_WGS_PER_CU,) + _FWD_WGS_TUNE)
+                if w == _FWD_WGS_PER_CU or max_rows is None or _grid_for(M, npad, bn, w) <= max_rows)
+    code = {(i, w): 10 * i + w for i in plan_impls for w in wgs}
+    inv = {v: k for k, v in code.items()}
+    best = _tune(lambda c: launch(inv[c][0], _grid_for(M, npad, bn, inv[c][1])), tuple(code.values()),
+                 default=code.get((_DEFAULT_IMPL, _FWD_WGS_PER_CU)))
+    if best not in inv:  # autotune off: the default variant on the default grid
+        return best, _grid_for(M, npad, bn, _FWD_WGS_PER_CU)
+    impl, w = inv[best]
+    return impl, _grid_for(M, npad, bn, w)
+
+
 def _fwd_impls(bn: int, kpad: int) -> Tuple[int, ...]:
     """Forward / dgrad variants the tuner tries for an N tile (csrc/conv.hip launch_v3_impl)."""
     return _WIDE_IMPLS.get(bn, _IMPLS)
@@ -337,14 +368,22 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
 
-    def launch(impl):
+    def launch(impl, grid):
         call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
              plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
-             plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, plan.grid_m, plan.wo_override, impl, stream())
+             plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
 
+    rows = stats.numel() // (2 * plan.Npad) if stats is not None else None
     if plan.impl == 0:
-        plan.impl = (_tune(launch, _fwd_impls(plan.bn, plan.Kpad)) if x.dtype != torch.uint8 else 2)
-    launch(plan.impl)
+        if x.dtype == torch.uint8:
+            plan.impl = 2
+        else:
+            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad), plan.M, plan.Npad, plan.bn,
+                                               rows)
+    if rows is not None and rows < plan.grid_m:
+        raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
+                         f"(allocate _stats_rows(M, Npad, bn) rows)")
+    launch(plan.impl, plan.grid_m)
     return y
 
 
@@ -357,19 +396,21 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
     dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dy.device)
     pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
     part = None
+    md = plan.B * plan.T * plan.H * plan.W
     if producer_bn is not None:
-        part = torch.empty((plan.d_grid_m * 2 * plan.d_Npad,), dtype=F32, device=dy.device)
+        part = torch.empty((_stats_rows(md, plan.d_Npad, plan.d_bn) * 2 * plan.d_Npad,), dtype=F32, device=dy.device)
 
-    def launch(impl):
+    def launch(impl, grid):
         call("milnce_conv_fwd", ptr(dy), 0, ptr(wd), ptr(dx), ptr(part),
              ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
              producer_bn[2] if part is not None else 0,
              plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
-             plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, plan.d_grid_m, 0, impl, stream())
+             plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl = _tune(launch, _fwd_impls(plan.d_bn, plan.d_Kpad))
-    launch(plan.d_impl)
+        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad), md, plan.d_Npad,
+                                               plan.d_bn)
+    launch(plan.d_impl, plan.d_grid_m)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx
@@ -722,9 +763,10 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
         else:
             y = None
     if y is None:
-        nparts = plan.grid_m
-        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+        stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
+                 if training else None)
         y = conv_forward_raw(x, wp, plan, stats)
+        nparts = plan.grid_m  # as tuned
     C = plan.Cout
     ss = torch.empty((4 * C,), dtype=F32, device=dev)
     call("milnce_bn_finalize", ptr(stats), nparts, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
@@ -1019,7 +1061,8 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
     plan = conv_plan(x.shape, wcat.shape, (1, 1, 1), (0, 0, 0))
     dev = x.device
     wp = _pack(wcat, plan, 0)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=F32, device=dev) if training else None
+    stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
+             if training else None)
     y = conv_forward_raw(x, wp, plan, stats)
     thw = plan.To * plan.Ho * plan.Wo
     zs, sss, gsum = [], [], None

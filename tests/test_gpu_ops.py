@@ -55,11 +55,11 @@ def test_conv_fwd_dgrad_wgrad(case):
     w = torch.randn(Cout, Cin, *k, device=DEV) * (2.0 / (Cin * k[0] * k[1] * k[2])) ** 0.5
     plan = h.conv_plan(x.shape, w.shape, s, p)
     wp = h._pack(w, plan, 0)
-    stats = torch.empty(plan.grid_m * 2 * plan.Npad, device=DEV)
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device=DEV)
     y = h.conv_forward_raw(x, wp, plan, stats)
     yr = ref_conv(x, w, s, p)
     assert rel_err(y, yr) < 1e-2
-    st = stats.view(plan.grid_m, 2, plan.Npad).sum(0)[:, :Cout]
+    st = stats[:plan.grid_m * 2 * plan.Npad].view(plan.grid_m, 2, plan.Npad).sum(0)[:, :Cout]  # rows as tuned
     yf = yr.reshape(-1, Cout)
     assert rel_err(st[0], yf.sum(0)) < 2e-2
     assert rel_err(st[1], (yf * yf).sum(0)) < 2e-2
@@ -89,13 +89,13 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     wp = h._pack(w, plan, 0)
     wd = h._pack(w, plan, 1)
     dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device=DEV)
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device=DEV)
     outs = {}
     for impl in h._IMPLS:
         plan.impl = plan.d_impl = impl
         for rep in range(2):
             y = h.conv_forward_raw(x, wp, plan, stats)
-            st = stats.clone()
+            st = stats[:plan.grid_m * 2 * plan.Npad].clone()
             dx = h.conv_dgrad(dy, wd, plan)
             outs[(impl, rep)] = (y, st, dx)
     ref = outs[(4, 0)]

@@ -64,3 +64,26 @@ def test_grad_sink_deferral_bookkeeping():
 
 def test_deferred_reduce_is_opt_in():
     assert h._DEFER_WGRAD == (os.environ.get("MILNCE_DEFER_WGRAD") == "1")
+
+
+def test_forward_tuner_pairs_variants_with_grid_sizes(monkeypatch):
+    """The forward / dgrad tuner times (kernel variant, persistent grid) pairs; a grid whose
+    partial-statistics rows would not fit the caller's buffer is never launched."""
+    M, npad, bn = 256 * 8 * 50 * 50, 64, 64  # conv_2c dgrad: one 64-wide N tile
+    seen = []
+
+    def fake_tune(launch, codes, default=None):
+        for c in codes:
+            launch(c)
+        return max(codes)  # the last (variant, grid) pair
+
+    monkeypatch.setattr(h, "_tune", fake_tune)
+    monkeypatch.setattr(h, "_FWD_WGS_TUNE", (2, 3))
+    impl, grid = h._tune_fwd(lambda i, g: seen.append((i, g)), (3, 4), M, npad, bn)
+    assert {g for _, g in seen} == {2 * h._NUM_CU, 3 * h._NUM_CU}
+    assert {i for i, _ in seen} == {3, 4}
+    assert (impl, grid) == (4, 3 * h._NUM_CU)
+    assert h._stats_rows(M, npad, bn) == 3 * h._NUM_CU
+    seen.clear()
+    impl, grid = h._tune_fwd(lambda i, g: seen.append((i, g)), (3, 4), M, npad, bn, max_rows=2 * h._NUM_CU)
+    assert {g for _, g in seen} == {2 * h._NUM_CU} and grid == 2 * h._NUM_CU

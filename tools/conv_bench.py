@@ -61,7 +61,7 @@ def main():
              else torch.randn(xs, device="cuda").to(torch.bfloat16))
         w = torch.randn(ws, device="cuda") * 0.05
         wp = hip_ops._pack(w, plan, 0)
-        stats = torch.empty((plan.grid_m * 2 * plan.Npad,), dtype=torch.float32, device="cuda")
+        stats = torch.empty((hip_ops._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=torch.float32, device="cuda")
         fl = 2.0 * plan.M * plan.Cout * plan.k[0] * plan.k[1] * plan.k[2] * plan.Cin_p
         t_f = timeit(lambda: hip_ops.conv_forward_raw(x, wp, plan, stats))
         dy = torch.randn((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), device="cuda").to(torch.bfloat16)

@@ -43,7 +43,7 @@ def main():
     w = torch.randn(o.cout, o.cin, *k, device="cuda") * 0.05
     plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), pad)
     wp, wd = h._pack(w, plan, 0), h._pack(w, plan, 1)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device="cuda")
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device="cuda")
     dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, o.cout, device="cuda").to(torch.bfloat16)
     fl = 2.0 * plan.M * plan.Cout * plan.Ktot
     print(f"{tuple(x.shape)} -> {o.cout} k{k}: fwd tile bn {plan.bn} bk {plan.bk}, dgrad tile bn {plan.d_bn} "

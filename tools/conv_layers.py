@@ -65,7 +65,7 @@ def main():
         stem = h._is_paired_stem(plan)
         if plan.impl and not stem:
             wp = h._pack(w, plan, 0)
-            stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device="cuda")
+            stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device="cuda")
             tf = timeit(lambda: h.conv_forward_raw(x, wp, plan, stats))
         if plan.d_impl and not stem and stride == (1, 1, 1):
             wd = h._pack(w, plan, 1)

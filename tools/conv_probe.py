@@ -30,7 +30,7 @@ def main():
     w = torch.randn(o.cout, o.cin, *k, device="cuda") * 0.05
     plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), pad)
     wp, wd = h._pack(w, plan, 0), h._pack(w, plan, 1)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device="cuda")
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device="cuda")
     y = h.conv_forward_raw(x, wp, plan, stats)  # autotunes
     dy = torch.randn_like(y)
     h.conv_dgrad(dy, wd, plan)

@@ -26,7 +26,7 @@ def main():
     w2 = torch.randn(64, 8, 3, 7, 4, device="cuda") * 0.05
     plan = h.conv_plan(x2.shape, w2.shape, (2, 2, 1), (1, 3, 2), W2)
     wp = h._pack(w2, plan, 0)
-    stats = torch.empty((plan.grid_m * 2 * plan.Npad,), device="cuda")
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device="cuda")
     y = h.conv_forward_raw(x2, wp, plan, stats)
     dy = torch.randn_like(y)
     from mil_nce_howto100m_amd.ops._lib import lib, ptr, stream
