@@ -1129,6 +1129,9 @@ static bool is_s1_333(const PoolParams& p) {
          p.pw == 1 && !p.zero_pad && p.To == p.T && p.Ho == p.H && p.Wo == p.W;
 }
 
+// milnce_pool_set_quad(0) turns the quad / block gathers off (A/B runs and the equality tests)
+static bool g_pool_quad = true;
+
 static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s,
                              const float* bn_ss = nullptr, const float* gate = nullptr) {
   if (n >= (1ll << 31)) return false;
@@ -1178,8 +1181,6 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
   return false;
 }
 
-// milnce_pool_set_quad(0) turns the quad gather off (A/B runs and the equality test)
-static bool g_pool_quad = true;
 MILNCE_API int milnce_pool_set_quad(int on) {
   g_pool_quad = on != 0;
   return 0;

@@ -295,6 +295,20 @@ def test_maxpool(kernel, stride, tf):
     assert rel_err(xh.grad, xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 3, 14, 16, 24), (1, 2, 100, 100, 64), (2, 2, 2, 2, 8)])
+def test_maxpool_tf_same_even_plane(shape):
+    """1x3x3/(1,2,2) TF-SAME pool over an even plane (the maxpool_2a / 3a geometry: no front
+    padding, one back pad row / column) == the fp32 reference, outputs bitwise, incl. ties."""
+    torch.manual_seed(7)
+    h = hip()
+    x = torch.randn(*shape, device=DEV).relu().to(torch.bfloat16)
+    x[:, :, :2, :2] = 0.25  # ties inside a window
+    y = h.maxpool3d(x, (1, 3, 3), (1, 2, 2), True)
+    yr = aten.maxpool_tf_same(x.float(), (1, 3, 3), (1, 2, 2))
+    assert y.shape == yr.shape
+    assert torch.equal(y.float(), yr)
+
+
 @pytest.mark.parametrize("shape", [(2, 16, 25, 9, 16), (3, 4, 13, 13, 56), (2, 2, 7, 7, 832), (1, 3, 1, 5, 8)])
 def test_maxpool_s1_lds_shapes(shape):
     """LDS plane-sweep stride-1 pool: > 256 plane rows (1 group), partial channel chunks, W=5/H=1."""
