@@ -1245,26 +1245,49 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
 
 // Sum the split slabs (coalesced along k) and scatter to the PyTorch weight layout
 // [n][c_param][tap].
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, float* __restrict__ dw, int splits,
-                                    int Npad, int Kpad, int Cout, int Cin, int Cin_param, int taps,
-                                    int accumulate) {
+// Block = 64 output elements x WR_GROUPS split groups: group g sums splits g, g + 4, ... with four
+// independent accumulators (16 slab loads in flight per element instead of 4 serial ones per
+// thread), then the groups combine in LDS in a fixed order: deterministic, and the few-thousand-
+// split slabs of the wide-occupancy wgrad tilings no longer run one latency-bound chain per thread.
+constexpr int WR_GROUPS = 4;
+
+__global__ __launch_bounds__(64 * WR_GROUPS) void wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                     float* __restrict__ dw, int splits, int Npad,
+                                                                     int Kpad, int Cout, int Cin, int Cin_param,
+                                                                     int taps, int accumulate) {
+  __shared__ float part[WR_GROUPS][64];
   const int Ktot = taps * Cin;
   const long long total = (long long)Cout * Ktot;
   const long long plane = (long long)Npad * Kpad;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  for (long long base = blockIdx.x * 64LL; base < total; base += gridDim.x * 64LL) {  // block-uniform
+    const long long idx = base + e;
     const int n = (int)(idx / Ktot);
     const int k = (int)(idx - (long long)n * Ktot);
     const int tap = k / Cin, c = k - tap * Cin;
-    if (c >= Cin_param) continue;
-    const float* sp = slab + (long long)n * Kpad + k;
-    float s = 0.f;
-    int sp_i = 0;
-    for (; sp_i + 4 <= splits; sp_i += 4)
-      s += sp[sp_i * plane] + sp[(sp_i + 1) * plane] + sp[(sp_i + 2) * plane] + sp[(sp_i + 3) * plane];
-    for (; sp_i < splits; ++sp_i) s += sp[sp_i * plane];
-    const long long o = ((long long)n * Cin_param + c) * taps + tap;
-    dw[o] = accumulate ? dw[o] + s : s;
+    const bool live = idx < total && c < Cin_param;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (live) {
+      const float* sp = slab + (long long)n * Kpad + k;
+      int i = grp;
+      for (; i + 3 * WR_GROUPS < splits; i += 4 * WR_GROUPS) {
+        s0 += sp[i * plane];
+        s1 += sp[(i + WR_GROUPS) * plane];
+        s2 += sp[(i + 2 * WR_GROUPS) * plane];
+        s3 += sp[(i + 3 * WR_GROUPS) * plane];
+      }
+      for (; i < splits; i += WR_GROUPS) s0 += sp[i * plane];
+    }
+    part[grp][e] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (grp == 0 && live) {
+      float s = part[0][e];
+#pragma unroll
+      for (int g = 1; g < WR_GROUPS; ++g) s += part[g][e];
+      const long long o = ((long long)n * Cin_param + c) * taps + tap;
+      dw[o] = accumulate ? dw[o] + s : s;
+    }
+    __syncthreads();
   }
 }
 
@@ -2183,8 +2206,8 @@ MILNCE_API int milnce_conv_wgrad(const void* dy, int ldd, const void* x, int x_u
 int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int Kpad, int Cout, int Cin,
                         int Cin_param, int taps, int accumulate, hipStream_t stream) {
   const long long total = (long long)Cout * taps * Cin;
-  const int grid = (int)((total + 255) / 256 < 4096 ? (total + 255) / 256 : 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(256), 0, stream, slab, dw, splits, Npad, Kpad,
+  const int grid = (int)((total + 63) / 64 < 16384 ? (total + 63) / 64 : 16384);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(64 * WR_GROUPS), 0, stream, slab, dw, splits, Npad, Kpad,
                      Cout, Cin, Cin_param, taps, accumulate);
   return (int)hipGetLastError();
 }
@@ -2257,10 +2280,7 @@ static int stem_wgrad_impl(StemWgradParams& p, int x_u8, long long slab_floats, 
   else rc = x_u8 ? stem_wgrad_launch<true, 8, false>(p, grid, lds, stream)
                  : stem_wgrad_launch<false, 8, false>(p, grid, lds, stream);
   if (rc) return rc;
-  const long long total = 64LL * 672;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((int)((total + 255) / 256)), dim3(256), 0, stream, p.slab, dw, grid,
-                     64, 672, 64, 8, 8, 84, accumulate);
-  return (int)hipGetLastError();
+  return launch_wgrad_reduce(p.slab, dw, grid, 64, 672, 64, 8, 8, 84, accumulate, stream);
 }
 
 MILNCE_API int milnce_stem_wgrad(const void* dy, const void* x2, int x_u8, float* slab, long long slab_floats,
