@@ -108,7 +108,9 @@ def test_hip_graph_eval_forward_matches_eager():
         with torch.no_grad():
             a = fwd(v)
             b = g(v)
-        assert torch.equal(a, b)
+        # the SelfGating channel sums are committed with float atomics per row block
+        # (csrc/bn.hip bn_relu_apply_kernel), so replays may differ from eager in the last bits
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-6), (a - b).abs().max()
     with torch.no_grad():
         for f in (fwd, g):
             torch.cuda.synchronize()
