@@ -2243,6 +2243,10 @@ static int stem_wgrad_launch(const StemWgradParams& p, int grid, size_t lds, hip
   return (int)hipGetLastError();
 }
 
+// Geometry not covered by the stem kernels: the caller falls back to the generic implicit GEMM.
+// Every other non-zero return is a HIP error and must be raised, not fallen back from.
+constexpr int STEM_UNSUPPORTED = -1;
+
 // pdy != nullptr: the POOL kernel (dY rebuilt from the maxpool_2a backward + BN backward, see
 // stem_wgrad_kernel); dy is then unused.
 static int stem_wgrad_impl(StemWgradParams& p, int x_u8, long long slab_floats, float* dw, int accumulate,
@@ -2251,21 +2255,21 @@ static int stem_wgrad_impl(StemWgradParams& p, int x_u8, long long slab_floats, 
   p.To = (T + 2 - 3) / 2 + 1;
   p.Ho = (H + 6 - 7) / 2 + 1;
   p.Wo = W2;
-  if (p.Ho % STW_HR) return (int)hipErrorInvalidValue;
+  if (p.Ho % STW_HR) return STEM_UNSUPPORTED;
   p.nitems = B * p.To * (p.Ho / STW_HR);
   p.halo_px = 3 * (2 * STW_HR + 5) * (W2 + 4);
-  if (p.halo_px > 256 * STW_HREG || STW_HR * p.Wo > 32 * STW_DREG) return (int)hipErrorInvalidValue;
+  if (p.halo_px > 256 * STW_HREG || STW_HR * p.Wo > 32 * STW_DREG) return STEM_UNSUPPORTED;
   const bool pool = p.pdy != nullptr;
-  if (pool && (p.Wo % 2 || p.Wo > 112 || p.Ho % 2)) return (int)hipErrorInvalidValue;
+  if (pool && (p.Wo % 2 || p.Wo > 112 || p.Ho % 2)) return STEM_UNSUPPORTED;
   p.dy_rows = (STW_HR * p.Wo + 31) / 32 * 32;
   p.x_bytes = (long long)B * T * H * W2 * (x_u8 ? 8 : 16);
   p.dy_bytes = (long long)B * p.To * p.Ho * p.Wo * 128;
-  if (p.x_bytes > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
+  if (p.x_bytes > 0x7FFFFFF0LL) return STEM_UNSUPPORTED;
   const size_t lds = (size_t)2 * (p.halo_px + p.dy_rows * 8) * 16 + (pool ? 7 * 64 * 4 : 0);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (lds > 160 * 1024) return STEM_UNSUPPORTED;
   int grid = 256;
   if (grid > p.nitems) grid = p.nitems;
-  if ((long long)grid * 64 * 672 > slab_floats) return (int)hipErrorInvalidValue;
+  if ((long long)grid * 64 * 672 > slab_floats) return STEM_UNSUPPORTED;
   // MILNCE_STEM_WGRAD_V (read once): 2 = 8 waves over K eighths (default), 0 = 4 waves
   static int variant = -1;
   if (variant < 0) {
@@ -2310,8 +2314,8 @@ MILNCE_API int milnce_stem_wgrad_pool(const void* pdy, const void* parg, const v
 
 // Stem forward (see stem_fwd_kernel): y [M, 64] bf16 and BN partials stats[nparts][2][64];
 // x2 as for milnce_stem_wgrad (bf16, or uint8 scaled by 1/255 while staged);
-// returns the number of partial rows written (> 0), or a negative value for geometries it does
-// not cover (the caller falls back to the generic implicit GEMM).
+// returns the number of partial rows written (> 0), STEM_UNSUPPORTED (-1) for geometries it does
+// not cover (the caller falls back to the generic implicit GEMM), or -1000 - hipError on a launch error.
 MILNCE_API int milnce_stem_fwd(const void* x2, int x_u8, const void* wpacked, int Kpad, void* y, float* stats,
                                long long stats_floats, int B, int T, int H, int W2, hipStream_t stream) {
   StemFwdParams p;

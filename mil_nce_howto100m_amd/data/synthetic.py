@@ -10,7 +10,7 @@ belongs to one of ``num_classes`` latent classes; the class sets the clip's colo
 spatial frequency and drift of a moving grating, and the first few word slots of each of its
 K captions (class-specific token ids), the rest of the words are random. Samples are a pure
 function of (seed, sample index), so a DistributedSampler-like rank stride gives disjoint,
-reproducible shards. On GPU the video is produced by a HIP kernel (``csrc/synth.hip``).
+reproducible shards. On GPU the video is produced by a HIP kernel (``csrc/misc.hip (synth_video_kernel)``).
 """
 from __future__ import annotations
 
@@ -26,7 +26,7 @@ M32 = 0xFFFFFFFF
 
 
 def _mix(x: torch.Tensor) -> torch.Tensor:
-    """32-bit integer hash on int64 tensors; bit-identical to ``mix32`` in csrc/synth.hip."""
+    """32-bit integer hash on int64 tensors; bit-identical to ``mix32`` in csrc/misc.hip (synth_video_kernel)."""
     x = x & M32
     x = (((x >> 16) ^ x) * 0x45D9F3B) & M32
     x = (((x >> 16) ^ x) * 0x45D9F3B) & M32
@@ -78,7 +78,7 @@ class SyntheticClips:
         return v
 
     def _video_torch(self, ids: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
-        """Reference implementation of csrc/synth.hip (same formula)."""
+        """Reference implementation of csrc/misc.hip (synth_video_kernel) (same formula)."""
         b, t, s = ids.shape[0], self.t, self.s
         lab = labels.view(b, 1, 1, 1, 1).float()
         tt = torch.arange(t, device=self.device).view(1, t, 1, 1, 1).float()

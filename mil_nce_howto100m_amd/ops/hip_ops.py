@@ -529,6 +529,7 @@ def _grad_done(param: torch.Tensor) -> None:
 
 
 _STEM_WGRAD = os.environ.get("MILNCE_STEM_WGRAD", "1") != "0"
+_STEM_UNSUPPORTED = -1  # csrc/conv.hip STEM_UNSUPPORTED: geometry not covered, use the generic conv
 _STEM_FWD = os.environ.get("MILNCE_STEM_FWD", "1") != "0"
 
 
@@ -694,6 +695,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                                      plan.B, plan.T, plan.H, plan.W, acc, stream())
         if rc == 0:
             return dw
+        if rc != _STEM_UNSUPPORTED:  # a HIP error, not a geometry the stem kernel skips
+            raise RuntimeError(f"milnce_stem_wgrad failed (hip error {rc}) for {plan}")
 
     def launch_with(tn, impl, occ, tk, target, accumulate):
         """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
@@ -760,8 +763,10 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
                                    stats.numel(), plan.B, plan.T, plan.H, plan.W, stream())
         if rc > 0:
             nparts = rc
-        else:
+        elif rc == _STEM_UNSUPPORTED:
             y = None
+        else:
+            raise RuntimeError(f"milnce_stem_fwd failed (hip error {-rc - 1000}) for {plan}")
     if y is None:
         stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
                  if training else None)
@@ -1554,8 +1559,15 @@ class _TextTower(torch.autograd.Function):
         hm = torch.empty((N, F_), dtype=F32, device=w1.device)
         arg = torch.empty((N, F_), dtype=torch.uint8, device=w1.device)
         tok = tokens.to(torch.int64).contiguous()
-        call("milnce_text_fc1_max", ptr(tok), N, Wd, ptr(table), ptr(w1p), ptr(b1.float().contiguous()), F_, kp,
-             ptr(hm), ptr(arg), stream())
+        if _text_fused_ok(Wd, kp, F_):
+            call("milnce_text_fc1_max", ptr(tok), N, Wd, ptr(table), ptr(w1p), ptr(b1.float().contiguous()), F_, kp,
+                 ptr(hm), ptr(arg), stream())
+        else:
+            # any other sentence length / embedding width: gathered rows, one bf16 GEMM, then the
+            # ReLU + max-over-words kernel (same hm / arg contract as the fused kernel)
+            e = table.index_select(0, tok.reshape(-1))
+            h = (torch.mm(e, w1p.t()).float() + b1.float()).to(BF16).view(N, Wd, F_)  # fp32 bias, as fused
+            call("milnce_text_relu_max", ptr(h), N, Wd, F_, ptr(hm), ptr(arg), stream())
         out = torch.addmm(b2, hm, w2.t())
         ctx.save_for_backward(tok, table, hm, arg, w2)
         ctx.dims = (N, Wd, F_, D)
@@ -1592,9 +1604,18 @@ def text_table_padded(weight: torch.Tensor) -> torch.Tensor:
     return t
 
 
+_TXT_FT = 64  # csrc/misc.hip TXT_FT: fc1 output-feature tile of the fused kernel
+
+
+def _text_fused_ok(Wd: int, kp: int, F_: int) -> bool:
+    """Geometry of the fused gather + fc1 + max kernel (csrc/misc.hip milnce_text_fc1_max):
+    <= 32 words, the 300-d word2vec table (320 padded columns), fc1 width a multiple of TXT_FT."""
+    return 1 <= Wd <= 32 and kp == 320 and F_ % _TXT_FT == 0
+
+
 def text_tower(tokens, table_padded, w1, b1, w2, b2):
-    if tokens.shape[1] > 32:
-        raise ValueError(f"fused text tower supports up to 32 words per sentence, got {tokens.shape[1]}")
+    if tokens.shape[1] > 255:  # the arg-max is a uint8 word index
+        raise ValueError(f"text tower supports up to 255 words per sentence, got {tokens.shape[1]}")
     return _TextTower.apply(tokens.contiguous(), table_padded, w1, b1, w2, b2)
 
 

@@ -58,8 +58,14 @@ def init_distributed(backend: str = "nccl", device: str = "auto", timeout_s: int
     else:
         use_cuda = device == "cuda"
     if use_cuda:
-        torch.cuda.set_device(local_rank)
-        dev = torch.device("cuda", local_rank)
+        # MILNCE_DEVICE_INDEX pins every rank to one device (multi-rank tests on a 1-GPU box,
+        # with gloo: RCCL refuses two ranks on one GPU); otherwise rank i owns device i
+        idx = int(os.environ.get("MILNCE_DEVICE_INDEX", str(local_rank)))
+        if "MILNCE_DEVICE_INDEX" not in os.environ:
+            from .launch import check_local_rank
+            check_local_rank(local_rank)
+        torch.cuda.set_device(idx)
+        dev = torch.device("cuda", idx)
     else:
         dev = torch.device("cpu")
         if backend == "nccl":

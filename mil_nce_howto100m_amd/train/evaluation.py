@@ -49,6 +49,15 @@ def _sharded_batches(ds, batch_size, workers, rank, world):
     return sharded_loader(ds, batch_size, workers, rank, world, convert=_native)
 
 
+# the eval CSVs shipped with the repository (csv/, from the reference's csv/): the default when
+# --eval_csv is not given, resolved next to the package rather than against the cwd
+CSV_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "csv")
+
+
+def default_csv(name: str) -> str:
+    return os.path.join(CSV_DIR, name)
+
+
 def _use_real(csv: str, root: str) -> bool:
     return bool(csv) and os.path.isfile(csv) and os.path.isdir(root) and ffmpeg_available()
 
@@ -82,10 +91,10 @@ def eval_hmdb(args, device, model: Optional[S3D] = None, ctx=None) -> dict:
     model = model or load_eval_model(args, device)
     rank, world = _rank_world(ctx)
     _graph_env(args)
-    csv = getattr(args, "eval_csv", "") or os.path.join("csv", "hmdb51.csv")
+    csv = getattr(args, "eval_csv", "") or default_csv("hmdb51.csv")
     if _use_real(csv, args.eval_video_root):
         ds = HMDBDataset(csv, args.eval_video_root, args.num_windows_test, args.num_frames, args.video_size)
-        batches = _sharded_batches(ds, args.batch_size_val, max(1, args.num_thread_reader), rank, world)
+        batches = _sharded_batches(ds, args.batch_size_val, max(0, args.num_thread_reader), rank, world)
     else:
         _synthetic_fallback(args, csv, "HMDB")
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,
@@ -102,13 +111,13 @@ def eval_retrieval(args, device, kind: str, model: Optional[S3D] = None, ctx=Non
     model = model or load_eval_model(args, device)
     rank, world = _rank_world(ctx)
     _graph_env(args)
-    csv = getattr(args, "eval_csv", "") or os.path.join(
-        "csv", "msrvtt_test.csv" if kind == "msrvtt" else "validation_youcook.csv")
+    csv = getattr(args, "eval_csv", "") or default_csv("msrvtt_test.csv" if kind == "msrvtt"
+                                                       else "validation_youcook.csv")
     tok = Tokenizer(args.token_to_word_path, max_words=30)
     if _use_real(csv, args.eval_video_root):
         ds = WindowedClipDataset(csv, args.eval_video_root, tok, args.num_windows_test, args.fps, args.num_frames,
                                  args.video_size, kind)
-        batches = _sharded_batches(ds, args.batch_size_val, max(1, args.num_thread_reader), rank, world)
+        batches = _sharded_batches(ds, args.batch_size_val, max(0, args.num_thread_reader), rank, world)
     else:
         _synthetic_fallback(args, csv, kind)
         batches = SyntheticEvalSet(getattr(args, "synthetic_eval_videos", 96), args.num_windows_test,

@@ -402,22 +402,26 @@ def test_avgpool():
     assert torch.allclose(x.grad.float(), torch.full_like(x.float(), 1 / 98.0), rtol=1e-2)
 
 
-@pytest.mark.parametrize("Wd", [20, 7, 32])
-def test_text_tower(Wd):
+@pytest.mark.parametrize("Wd,D", [(20, 300), (7, 300), (32, 300), (40, 300), (16, 200)])
+def test_text_tower(Wd, D):
     """Fused gather + fc1 + ReLU + max-over-words kernel (csrc/misc.hip text_fc1_max_kernel)
-    and the fc2 / backward around it vs an fp32 reference on the same bf16 operands."""
+    and the fc2 / backward around it vs an fp32 reference on the same bf16 operands. Sentences
+    longer than 32 words or tables other than 300-d take the unfused GEMM + relu-max path."""
     torch.manual_seed(4)
     h = hip()
     N, V = 18, 1000  # 18 sentences: a partial last workgroup (4 sentences per workgroup)
     tok = torch.randint(0, V, (N, Wd), device=DEV)
     tok[:, Wd // 2:] = 0  # padded word slots hold token 0, as the tokenizer writes them
-    table = torch.randn(V, 300, device=DEV)
-    fc1, fc2 = nn.Linear(300, 2048).to(DEV), nn.Linear(2048, 512).to(DEV)
+    table = torch.randn(V, D, device=DEV)
+    fc1, fc2 = nn.Linear(D, 2048).to(DEV), nn.Linear(2048, 512).to(DEV)
     tp = h.text_table_padded(table)
-    assert tp.shape == (V, 320) and int(tp[:, 300:].float().abs().sum()) == 0
+    kp = (D + 31) // 32 * 32
+    assert tp.shape == (V, kp) and int(tp[:, D:].float().abs().sum()) == 0
+    assert h._text_fused_ok(Wd, kp, 2048) == (Wd <= 32 and D == 300)
     out = h.text_tower(tok, tp, fc1.weight, fc1.bias, fc2.weight, fc2.bias)
     e = F.embedding(tok, table.to(torch.bfloat16).float())
     w1 = nn.Parameter(fc1.weight.detach().to(torch.bfloat16).float())
+    assert e.shape[-1] == D
     b1 = nn.Parameter(fc1.bias.detach().clone())  # the kernel adds the fp32 bias
     w2 = nn.Parameter(fc2.weight.detach().clone())
     b2 = nn.Parameter(fc2.bias.detach().clone())

@@ -136,3 +136,89 @@ def test_bucket_readiness_multirank(world, chunks):
         assert torch.equal(flats[r], flats[0])
     s0 = torch.cat([sum(s[i] for s in snaps) for i in sorted(snaps[0])])
     assert torch.allclose(s0, flats[0], rtol=1e-5, atol=1e-7)
+
+
+def test_count_gpus_intersects_visibility(monkeypatch):
+    from mil_nce_howto100m_amd.parallel import launch
+    monkeypatch.setattr(launch, "_kfd_gpu_count", lambda: 8)
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert launch.count_gpus_no_init() == 8
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "0,1,2,3")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")  # indexes into the 4 ROCr left
+    assert launch.count_gpus_no_init() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1,2,3,4,5")
+    assert launch.count_gpus_no_init() == 4
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES")
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setattr(launch, "_kfd_gpu_count", lambda: 2)
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "0,1,2,3")  # lists more than the topology has
+    assert launch.count_gpus_no_init() == 2
+
+
+@pytest.mark.parametrize("sig", ["TERM", "HUP"])
+def test_launch_local_forwards_signals(sig):
+    """A SIGTERM / SIGHUP to the launcher reaches every rank: none survives it."""
+    import signal
+    import time
+    with tempfile.TemporaryDirectory() as d:
+        script = os.path.join(d, "w.py")
+        with open(script, "w") as f:
+            f.write("import os, time\n"
+                    "open(os.path.join(%r, 'pid%%s' %% os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                    "time.sleep(120)\n" % d)
+        parent = os.path.join(d, "p.py")
+        with open(parent, "w") as f:
+            f.write("import sys\nsys.path.insert(0, %r)\n"
+                    "from mil_nce_howto100m_amd.parallel.launch import launch_local\n"
+                    "sys.exit(launch_local(%r, [], 3, grace_s=5))\n" % (ROOT, script))
+        p = subprocess.Popen([sys.executable, parent], env=_clean_env())
+        t0 = time.time()
+        while len([n for n in os.listdir(d) if n.startswith("pid")]) < 3:
+            assert time.time() - t0 < 60 and p.poll() is None
+            time.sleep(0.1)
+        time.sleep(0.3)
+        pids = [int(open(os.path.join(d, f"pid{r}")).read()) for r in range(3)]
+        p.send_signal(getattr(signal, "SIG" + sig))
+        assert p.wait(timeout=30) == 128 + getattr(signal, "SIG" + sig)
+        for pid in pids:
+            try:
+                os.kill(pid, 0)
+                alive = os.path.exists(f"/proc/{pid}") and "zombie" not in open(f"/proc/{pid}/status").read()
+            except ProcessLookupError:
+                alive = False
+            assert not alive, f"rank pid {pid} survived the launcher's SIG{sig}"
+
+
+def test_launch_local_ranks_die_with_killed_parent():
+    """A SIGKILLed launcher (no handler runs) still takes its ranks down (PR_SET_PDEATHSIG)."""
+    import signal
+    import time
+    with tempfile.TemporaryDirectory() as d:
+        script = os.path.join(d, "w.py")
+        with open(script, "w") as f:
+            f.write("import os, time\n"
+                    "open(os.path.join(%r, 'pid%%s' %% os.environ['RANK']), 'w').write(str(os.getpid()))\n"
+                    "time.sleep(120)\n" % d)
+        parent = os.path.join(d, "p.py")
+        with open(parent, "w") as f:
+            f.write("import sys\nsys.path.insert(0, %r)\n"
+                    "from mil_nce_howto100m_amd.parallel.launch import launch_local\n"
+                    "sys.exit(launch_local(%r, [], 2))\n" % (ROOT, script))
+        p = subprocess.Popen([sys.executable, parent], env=_clean_env())
+        t0 = time.time()
+        while len([n for n in os.listdir(d) if n.startswith("pid")]) < 2:
+            assert time.time() - t0 < 60 and p.poll() is None
+            time.sleep(0.1)
+        time.sleep(0.3)
+        pids = [int(open(os.path.join(d, f"pid{r}")).read()) for r in range(2)]
+        p.send_signal(signal.SIGKILL)
+        p.wait(timeout=10)
+        deadline = time.time() + 15
+        for pid in pids:
+            while time.time() < deadline:
+                if not os.path.exists(f"/proc/{pid}") or "zombie" in open(f"/proc/{pid}/status").read().lower():
+                    break
+                time.sleep(0.1)
+            else:
+                raise AssertionError(f"rank pid {pid} outlived its killed launcher")
