@@ -68,6 +68,13 @@ def build(jobs: int = 8, debug: bool = False, verbose: bool = True, mode: str = 
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    # every kernel's host launch stub must be in the library: clang can silently drop one (e.g.
+    # for kernels in an anonymous namespace, or with template-sized local arrays), which only
+    # shows as an undefined symbol when the library is loaded
+    r = subprocess.run(["nm", "-C", "--undefined-only", lib], capture_output=True, text=True)
+    missing = [ln.split(None, 1)[1] for ln in r.stdout.splitlines() if "_kernel" in ln and ln.split()[0] == "U"]
+    if missing:
+        raise RuntimeError(f"{lib}: undefined kernel symbols (dropped launch stubs): {missing[:4]}")
     if verbose:
         print(f"built {lib} from {len(srcs)} sources")
     return lib

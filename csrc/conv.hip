@@ -17,38 +17,7 @@
 // Tiles: 256 threads = 4 waves (2 x 2), mfma_f32_16x16x32_bf16, LDS double buffering with
 // register staging (the gather needs per-element zero fill), XOR-swizzled A/B images so the
 // 16-lane ds_read_b128 groups are bank-conflict free, XCD-aware block remap.
-#include "common.h"
-
-struct ConvParams {
-  const void* x;       // [B, T, H, W, Cin] bf16 or uint8
-  const bf16_t* w;     // packed [Npad, Kpad] bf16 (k = (tap, c), c fastest)
-  bf16_t* y;           // [M, ldy] bf16
-  float* stats;        // [grid_m, 2, Npad] or nullptr
-  long long x_bstride; // T*H*W*Cin
-  int T, H, W, Cin;
-  int To, Ho, Wo, Cout;
-  int KT, KH, KW, st, sh, sw, pt, ph, pw;
-  int Ktot, Kpad, ldy, M;
-  int num_m_tiles, num_n_tiles, grid_m;
-  float in_scale;
-  long long x_total_bytes;
-  FastDiv fWo, fHo, fTo, fCin, fKW, fKH;
-  // epilogue statistics: 0 none; 1 BN forward sums of this conv's output (stats);
-  // 2 BN backward partials of the PRODUCER of this dgrad's output: the output is that
-  //   layer's dz, bn_y/bn_ss its raw conv output and [mean, invstd, scale, shift];
-  //   stats += (dz*mask, dz*mask*xhat) with mask = y*scale + shift > 0.
-  int bn_mode;
-  const bf16_t* bn_y;
-  const float* bn_ss;
-  int bn_ld;  // row stride of bn_y (elements)
-};
-
-template <int BK>
-__device__ __forceinline__ int swz(int row, int chunk) {
-  // 16-B chunk swizzle of a [rows][BK] bf16 tile (BK*2-byte rows).
-  if constexpr (BK == 32) return chunk ^ ((row >> 2) & 3);
-  else return chunk ^ ((row >> 1) & 7);
-}
+#include "conv_common.h"
 
 // Tap table entry: .x = element offset of the tap inside a clip ((dt*H + dh)*W + dw)*Cin,
 // .y = dt | dh << 8 | dw << 16.
@@ -407,29 +376,6 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
 // Workgroup barrier for the LDS-DMA rings. __builtin_amdgcn_s_barrier() is not a memory barrier
 // for the compiler (LDS reads could be hoisted above it, i.e. before other waves' DMA pieces
 // for the stage have landed), and __syncthreads() would add a vmcnt(0) that drains the ring.
-// One asm statement with a memory clobber orders both: this wave's LDS reads of the previous
-// stage are complete (lgkmcnt(0)) and no LDS access moves across the barrier.
-__device__ __forceinline__ void ring_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// Wait until at most N vector-memory operations (here: LDS-DMA pieces) of this wave are
-// outstanding. N must be exact (rounding up would let a piece of the stage about to be read
-// still be in flight), so it is a template constant; wait_stages picks N = ahead * NDMA.
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-template <int NDMA, int MAXAHEAD>
-__device__ __forceinline__ void wait_stages(int ahead) {
-  static_assert(MAXAHEAD <= 2, "ring depth");
-  if (ahead <= 0) wait_vmcnt<0>();
-  else if (ahead == 1 || MAXAHEAD < 2) wait_vmcnt<NDMA>();
-  else wait_vmcnt<(MAXAHEAD >= 2 ? 2 * NDMA : 0)>();
-}
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-
 #ifndef V3_PRIO_DEFAULT
 #define V3_PRIO_DEFAULT 1
 #endif
@@ -2070,6 +2016,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.fCin = make_fastdiv(Cin);
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
+  if (impl >= 8) return x_u8 ? V4_UNSUPPORTED : launch_fwd_v4(p, bn, impl, stream);  // conv_v4.hip
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
     // wide / odd N tiles: LDS-DMA ring variants only, BK 64
     if (bk != 64) return (int)hipErrorInvalidValue;

@@ -132,6 +132,10 @@ class ConvPlan:
     w_impl: int = 0       # wgrad kernel variant (2: register-staged, 3/4: LDS-DMA ring, 3/2 stages)
     w_occ: int = 4        # wgrad split-K target: workgroups per CU (fewer splits = smaller slab to reduce)
 
+    @property
+    def taps(self) -> int:
+        return self.k[0] * self.k[1] * self.k[2]
+
 
 _PLANS: Dict[tuple, ConvPlan] = {}
 _NUM_CU = 256
@@ -179,9 +183,30 @@ def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
     return impl, _grid_for(M, npad, bn, w)
 
 
-def _fwd_impls(bn: int, kpad: int) -> Tuple[int, ...]:
-    """Forward / dgrad variants the tuner tries for an N tile (csrc/conv.hip launch_v3_impl)."""
-    return _WIDE_IMPLS.get(bn, _IMPLS)
+# v4 forward / dgrad (csrc/conv_v4.hip): LDS-DMA ring with scalar per-stage offsets, for convs
+# whose input channel count is a multiple of 64 (every 64-wide K stage inside one tap). 8 / 10:
+# 16x16x32 MFMA, 2 / 3 stages; 9 / 11: 32x32x16 MFMA (N tiles 64 / 128 / 192). MILNCE_V4=0
+# leaves them out of the tuner (A/B runs); MILNCE_V4_IMPLS restricts the set.
+_V4 = os.environ.get("MILNCE_V4", "1") != "0"
+_V4_IMPLS = tuple(int(v) for v in os.environ.get("MILNCE_V4_IMPLS", "8,9,10,11").split(","))
+
+
+def _v4_ok(bn: int, cin: int, taps: int, kpad: int, impl: int) -> bool:
+    """Mirror of csrc/conv_v4.hip fwd_v4_supported."""
+    if cin % 64 or kpad != taps * cin or taps > 32 or bn not in (64, 96, 128, 160, 192):
+        return False
+    if impl in (9, 11) and (bn // 2) % 32:
+        return False
+    return True
+
+
+def _fwd_impls(bn: int, kpad: int, cin: int = 0, taps: int = 0) -> Tuple[int, ...]:
+    """Forward / dgrad variants the tuner tries for an N tile (csrc/conv.hip launch_v3_impl,
+    csrc/conv_v4.hip); ``cin`` = channels of the gathered operand (0: v3 variants only)."""
+    base = _WIDE_IMPLS.get(bn, _IMPLS)
+    if _V4 and cin:
+        base = base + tuple(i for i in _V4_IMPLS if _v4_ok(bn, cin, taps, kpad, i))
+    return base
 
 
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
@@ -378,8 +403,8 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
         if x.dtype == torch.uint8:
             plan.impl = 2
         else:
-            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad), plan.M, plan.Npad, plan.bn,
-                                               rows)
+            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps),
+                                               plan.M, plan.Npad, plan.bn, rows)
     if rows is not None and rows < plan.grid_m:
         raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
                          f"(allocate _stats_rows(M, Npad, bn) rows)")
@@ -408,8 +433,8 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad), md, plan.d_Npad,
-                                               plan.d_bn)
+        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps),
+                                               md, plan.d_Npad, plan.d_bn)
     launch(plan.d_impl, plan.d_grid_m)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
@@ -1566,7 +1591,9 @@ class _TextTower(torch.autograd.Function):
             # any other sentence length / embedding width: gathered rows, one bf16 GEMM, then the
             # ReLU + max-over-words kernel (same hm / arg contract as the fused kernel)
             e = table.index_select(0, tok.reshape(-1))
-            h = (torch.mm(e, w1p.t()).float() + b1.float()).to(BF16).view(N, Wd, F_)  # fp32 bias, as fused
+            # fp32 accumulate + fp32 bias, rounded to bf16 once (as the fused kernel does: the
+            # arg-max word that routes the gradient is decided on the same values)
+            h = torch.addmm(b1.float(), e.float(), w1p.float().t()).to(BF16).view(N, Wd, F_)
             call("milnce_text_relu_max", ptr(h), N, Wd, F_, ptr(hm), ptr(arg), stream())
         out = torch.addmm(b2, hm, w2.t())
         ctx.save_for_backward(tok, table, hm, arg, w2)

@@ -70,7 +70,15 @@ def probe(grad_numel: int, buckets: Sequence[Sequence[int]], emb_rows: int, emb_
     out["bucketed_allreduce_ms"] = round(bt * 1e3, 3)
     emb = torch.ones((emb_rows, emb_dim), dtype=emb_dtype, device=device)
     gathered = emb.new_empty((world * emb_rows, emb_dim))
-    ag = _timed(lambda: dist.all_gather_into_tensor(gathered, emb), reps, cuda)
+    if cuda and dist.get_backend() == "gloo":  # ranks sharing a GPU in tests: the host path of dist.py
+        def gather():
+            host = gathered.cpu()
+            dist.all_gather_into_tensor(host, emb.cpu())
+            gathered.copy_(host)
+    else:
+        def gather():
+            dist.all_gather_into_tensor(gathered, emb)
+    ag = _timed(gather, reps, cuda)
     gbytes = gathered.numel() * gathered.element_size()
     out["allgather_kib"] = round(gbytes / 1024, 1)
     out["allgather_ms"] = round(ag * 1e3, 3)

@@ -112,7 +112,13 @@ class _GatherLocalGrad(torch.autograd.Function):
     @staticmethod
     def forward(ctx, packed: torch.Tensor, world: int, rank: int):
         out = packed.new_empty((world * packed.shape[0],) + tuple(packed.shape[1:]))
-        dist.all_gather_into_tensor(out, packed.contiguous())
+        if packed.is_cuda and dist.get_backend() == "gloo":
+            # gloo over device tensors (multi-rank tests sharing one GPU): gather on the host
+            host = out.cpu()
+            dist.all_gather_into_tensor(host, packed.contiguous().cpu())
+            out.copy_(host)
+        else:
+            dist.all_gather_into_tensor(out, packed.contiguous())
         ctx.rows = packed.shape[0]
         ctx.rank = rank
         return out

@@ -121,6 +121,56 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     plan.impl = plan.d_impl = plan.w_impl = 0
 
 
+@pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 192, (3, 1, 1), (1, 0, 0)),
+                                          (128, 96, (1, 1, 1), (0, 0, 0)), (192, 64, (1, 3, 3), (0, 1, 1)),
+                                          (256, 320, (3, 1, 1), (1, 0, 0)), (64, 128, (3, 3, 3), (1, 1, 1))])
+def test_conv_v4_variants(cin, cout, k, p):
+    """csrc/conv_v4.hip (scalar-offset LDS-DMA ring): the 16x16x32 variants (8, 10) sum in v3's
+    order, so forward, dgrad and the producer-BN dgrad partials are bitwise those of v3 (impl 4);
+    the 32x32x16 variants (9, 11) match the fp32 reference. Small planes (every row near the
+    padding) and a runtime-shape (3,3,3) kernel."""
+    torch.manual_seed(13)
+    h = hip()
+    x = torch.randn(3, 6, 11, 13, cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(cout, cin, *k, device=DEV) * (2.0 / (cin * k[0] * k[1] * k[2])) ** 0.5
+    plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), p)
+    wp, wd = h._pack(w, plan, 0), h._pack(w, plan, 1)
+    dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device=DEV)
+    # a producer BN for the dgrad's fused partials: y = x itself, arbitrary scale / shift
+    ss = torch.cat([torch.randn(cin, device=DEV) * 0.1, torch.rand(cin, device=DEV) + 0.5,
+                    torch.randn(cin, device=DEV), torch.randn(cin, device=DEV) * 0.2])
+    yr = ref_conv(x, w, (1, 1, 1), p)
+    xr = x.float().requires_grad_(True)
+    F.conv3d(xr.permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).float(), None, 1, p).permute(0, 2, 3, 4, 1).backward(
+        dy.float())
+    fw_impls = [i for i in (8, 9, 10, 11) if h._v4_ok(plan.bn, cin, plan.taps, plan.Kpad, i)]
+    dg_impls = [i for i in (8, 9, 10, 11) if h._v4_ok(plan.d_bn, cout, plan.taps, plan.d_Kpad, i)]
+    assert 8 in fw_impls and (cout % 64 != 0 or 8 in dg_impls)
+    outs = {}
+    for impl in [4] + sorted(set(fw_impls) | set(dg_impls)):
+        plan.impl = impl if (impl == 4 or impl in fw_impls) else 4
+        plan.d_impl = impl if (impl == 4 or impl in dg_impls) else 4
+        y = h.conv_forward_raw(x, wp, plan, stats)
+        st = stats[:plan.grid_m * 2 * plan.Npad].view(plan.grid_m, 2, plan.Npad).double().sum(0)
+        dx = h.conv_dgrad(dy, wd, plan, (x, ss, cin))
+        part, nparts, ps = h.take_bn_partials(dx)
+        pst = part[:nparts * 2 * ps].view(nparts, 2, ps).double().sum(0)
+        outs[impl] = (y, st, dx, pst, plan.impl, plan.d_impl)
+        assert rel_err(y, yr) < 1e-2, impl
+        assert rel_err(dx, xr.grad) < 1e-2, impl
+    ref = outs[4]
+    for impl, (y, st, dx, pst, fi, di) in outs.items():
+        if fi in (8, 10):
+            assert torch.equal(y, ref[0]), ("y", impl)
+        if di in (8, 10):
+            assert torch.equal(dx, ref[2]), ("dx", impl)
+            assert torch.allclose(pst, ref[3], rtol=1e-4, atol=1e-3), ("partials", impl)
+        assert torch.allclose(st, ref[1], rtol=2e-3, atol=1e-1), ("stats", impl)
+        assert torch.allclose(pst, ref[3], rtol=2e-2, atol=1.0), ("partials", impl)
+    plan.impl = plan.d_impl = 0
+
+
 @pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 176, (1, 1, 1), (0, 0, 0)),
                                           (96, 288, (3, 1, 1), (1, 0, 0)), (192, 192, (3, 1, 1), (1, 0, 0)),
                                           (128, 96, (3, 1, 1), (1, 0, 0))])

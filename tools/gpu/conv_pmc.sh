@@ -2,7 +2,7 @@
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-D=gpurun_out/conv_pmc
+D=gpurun_out/${CONV_PMC_TAG:-conv_pmc}
 mkdir -p $D
 ARGS="${@:-}"
 timeout -s KILL 120 rocprofv3 -L > $D/counters_list.txt 2>&1 || true

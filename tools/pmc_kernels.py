@@ -37,6 +37,12 @@ def main(d):
             print(f"   clock {g / 8 / us / 1e3:.2f} GHz")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in m and g:
             print(f"   mfma busy share {m['SQ_VALU_MFMA_BUSY_CYCLES'] / (g / 8 * 256 * 4):.3f} (per SIMD)")
+        if m.get("SQ_LDS_IDX_ACTIVE") and g:
+            print(f"   lds active share {m['SQ_LDS_IDX_ACTIVE'] / (g / 8 * 256):.3f} (per CU, raw units)")
+        if m.get("SQ_INSTS_MFMA"):
+            print(f"   valu/mfma {m.get('SQ_INSTS_VALU', 0) / m['SQ_INSTS_MFMA']:.2f}  "
+                  f"lds/mfma {m.get('SQ_INSTS_LDS', 0) / m['SQ_INSTS_MFMA']:.2f}  "
+                  f"vmem/mfma {m.get('SQ_INSTS_VMEM', 0) / m['SQ_INSTS_MFMA']:.2f}")
         if m.get("SQ_LDS_IDX_ACTIVE"):
             print(f"   lds conflict ratio {m.get('SQ_LDS_BANK_CONFLICT', 0) / m['SQ_LDS_IDX_ACTIVE']:.3f}")
 
