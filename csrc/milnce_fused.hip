@@ -1,25 +1,33 @@
 // Fused MIL-NCE (loss.py:10-18) for large global batches: the logits x = V T^T ([Bg, Bg*K]) are
-// never stored. Exact fp32 via v_mfma_f32_16x16x4_f32 (f32 in / f32 accumulate, the reference's
-// fp32 logits): 64 x 64 tiles, 4 waves (16 rows x 64 columns each), D streamed through LDS.
+// never stored. The logit and gradient GEMMs run on bf16 MFMA (mfma_f32_16x16x32_bf16) with
+// split-bf16 operands for fp32-level accuracy: every fp32 operand X is held as X_hi = bf16(X),
+// X_lo = bf16(X - X_hi) (16 significant bits together), and A B = A_hi B_hi + A_hi B_lo + A_lo B_hi
+// (the dropped A_lo B_lo term is 2^-16 relative): 3 bf16 MFMAs per product, i.e. 16/3 x the rate
+// of the f32-input MFMA the first version used.
 //
-//   forward : per tile, row partial (max, sum e^{x-max}) over its 64 columns and, for each of its
-//             64/K text blocks, a block-column partial over its 64 rows; a finalize kernel merges
-//             them into den_i = LSE(row_i U blockcol_i) and takes nom_i = LSE_k V_i . T_{iK+k}
-//             (positives counted twice, as in the reference);
+//   split   : V, T (fp32) -> row-major [R][D] hi/lo and transposed [D][Rp] hi/lo bf16 copies (the
+//             transposed ones make the backward's reductions over the batch k-contiguous MFMA
+//             operands, like the forward's);
+//   forward : 64 x 64 logit tiles (4 waves x 16 rows), per tile a row partial (max, sum e^{x-max})
+//             over its 64 columns and, for each of its 64/K text blocks, a block-column partial
+//             over its 64 rows; a finalize kernel merges them into den_i = LSE(row_i U blockcol_i)
+//             and takes nom_i = LSE_k V_i . T_{iK+k} (positives counted twice, as in the reference);
 //   backward: G[i, j] = g/Bg (e^{x-den_i} + e^{x-den_{j/K}} - [j/K == i] e^{x-nom_i}) recomputed
-//             tile by tile; dV = G T accumulated in registers by a row-tile pass, dT = G^T V by a
-//             column-tile pass (no atomics, deterministic). 4 logit GEMMs per step instead of 2
-//             materialised fp32 [Bg, Bg*K] tensors (1 GiB each at Bg = 8192, K = 4).
+//             tile by tile and split to bf16 hi/lo in LDS; dV = G T by a row-tile pass (64 rows x
+//             D accumulated in registers), dT = G^T V by a column-tile pass; no atomics,
+//             deterministic. Nothing of size [Bg, Bg*K] is ever stored.
+//
+// LDS images are [64 rows][64 bf16] with the 16-B chunk XOR swizzle of the conv kernels
+// (conflict-free ds_read_b128 fragment reads); operands are register-staged one 64-wide K chunk
+// ahead of the MFMAs.
 #include "common.h"
 
 namespace {
 
 constexpr int TM = 64, TN = 64;  // tile rows (video) x tile columns (text)
-constexpr int KC = 32;           // D chunk staged per step of the logit GEMM
-constexpr int SP = KC + 1;       // padded LDS row (floats)
-constexpr int GP = TN + 1;       // padded S/G tile row
-constexpr int DC = 64;           // D chunk of the G GEMMs
-constexpr int DP = DC + 1;
+constexpr int KC = 64;           // K chunk of every GEMM (bf16 elements per LDS row)
+constexpr int GP = TN + 1;       // padded fp32 S tile row
+constexpr int IMG = 64 * KC;     // elements of one [64][64] bf16 image
 
 __device__ __forceinline__ void lse_add(float& m, float& s, float m2, float s2) {
   if (m2 == -INFINITY) return;
@@ -28,36 +36,87 @@ __device__ __forceinline__ void lse_add(float& m, float& s, float m2, float s2) 
   else { s += s2 * __expf(m2 - m); }
 }
 
-// S[64 x 64] tile = V[r0 : r0+64] . T[c0 : c0+64]^T into acc (wave w: rows 16w.., all 4 column
-// blocks; acc[nb][r] = S[16w + 4*(lane>>4) + r][16 nb + (lane & 15)]). Rows past the matrix read 0.
-__device__ __forceinline__ void logit_tile(const float* __restrict__ V, const float* __restrict__ T, int B, int N,
-                                           int D, int r0, int c0, float* Vs, float* Ts, f32x4 (&acc)[4]) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+__device__ __forceinline__ int sw(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+// Register staging of 64 rows x 64 columns of a bf16 [rows][ld] matrix (rows >= nrows read 0):
+// two 16-B pieces per thread.
+struct Stage2 {
+  uint4 v[2];
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ src, long long ld, int row0, int nrows, int col0) {
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb) acc[nb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < 2; ++it) {
+      const int e = threadIdx.x + it * 256, r = e >> 3, c = e & 7;
+      v[it] = row0 + r < nrows ? *(const uint4*)(src + (long long)(row0 + r) * ld + col0 + c * 8)
+                               : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  __device__ __forceinline__ void store(bf16_t* img) const {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int e = threadIdx.x + it * 256, r = e >> 3, c = e & 7;
+      *(uint4*)(img + r * KC + sw(r, c) * 8) = v[it];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8 frag(const bf16_t* img, int row, int s) {
+  // 16x16x32 operand fragment: row (lane & 15) of the 16-row block, k = 32 s + 8 (lane >> 4) ..
+  const int lane = threadIdx.x & 63;
+  return *(const bf16x8*)(img + row * KC + sw(row, s * 4 + (lane >> 4)) * 8);
+}
+
+// acc += A B^T over one staged 64-wide K chunk with split operands: A rows arow (16 per wave),
+// B rows 16 cb + (lane & 15) for cb = 0..3.
+__device__ __forceinline__ void mfma_chunk(const bf16_t* Ah, const bf16_t* Al, const bf16_t* Bh, const bf16_t* Bl,
+                                           int arow, f32x4 (&acc)[4]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const bf16x8 ah = frag(Ah, arow, s), al = frag(Al, arow, s);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int br = 16 * cb + (lane & 15);
+      const bf16x8 bh = frag(Bh, br, s), bl = frag(Bl, br, s);
+      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[cb], 0, 0, 0);
+      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[cb], 0, 0, 0);
+      acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc[cb], 0, 0, 0);
+    }
+  }
+}
+
+struct Split {  // split copies of one fp32 matrix X [R][D]
+  const bf16_t* h;   // [R][D]
+  const bf16_t* l;
+  const bf16_t* th;  // [D][Rp], Rp = R rounded up to 64 (zero padding)
+  const bf16_t* tl;
+};
+
+// S[64 x 64] = V[r0 : r0+64] . T[c0 : c0+64]^T into acc (wave w: rows 16w.., all 4 column blocks;
+// acc[cb][r] = S[16w + 4*(lane>>4) + r][16 cb + (lane & 15)]). img: 4 images (Vh, Vl, Th, Tl).
+__device__ __forceinline__ void logit_tile(const Split& V, const Split& T, int B, int N, int D, int r0, int c0,
+                                           bf16_t* img, f32x4 (&acc)[4]) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  Stage2 a, b, c, d;
+  a.load(V.h, D, r0, B, 0);
+  b.load(V.l, D, r0, B, 0);
+  c.load(T.h, D, c0, N, 0);
+  d.load(T.l, D, c0, N, 0);
   for (int k0 = 0; k0 < D; k0 += KC) {
+    __syncthreads();  // previous chunk's fragments read
+    a.store(img);
+    b.store(img + IMG);
+    c.store(img + 2 * IMG);
+    d.store(img + 3 * IMG);
     __syncthreads();
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {  // 64 rows x 8 float4 per matrix = 512 float4, 2 per thread
-      const int e = tid + it * 256, row = e >> 3, c4 = (e & 7) * 4;
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-      if (r0 + row < B) a = *(const float4*)(V + (long long)(r0 + row) * D + k0 + c4);
-      if (c0 + row < N) b = *(const float4*)(T + (long long)(c0 + row) * D + k0 + c4);
-      float* va = Vs + row * SP + c4;
-      float* tb = Ts + row * SP + c4;
-      va[0] = a.x; va[1] = a.y; va[2] = a.z; va[3] = a.w;
-      tb[0] = b.x; tb[1] = b.y; tb[2] = b.z; tb[3] = b.w;
+    if (k0 + KC < D) {
+      a.load(V.h, D, r0, B, k0 + KC);
+      b.load(V.l, D, r0, B, k0 + KC);
+      c.load(T.h, D, c0, N, k0 + KC);
+      d.load(T.l, D, c0, N, k0 + KC);
     }
-    __syncthreads();
-#pragma unroll
-    for (int kk = 0; kk < KC; kk += 4) {
-      const float a = Vs[(16 * w + (lane & 15)) * SP + kk + (lane >> 4)];
-#pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
-        const float b = Ts[(16 * nb + (lane & 15)) * SP + kk + (lane >> 4)];
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[nb], 0, 0, 0);
-      }
-    }
+    mfma_chunk(img, img + IMG, img + 2 * IMG, img + 3 * IMG, 16 * w + (lane & 15), acc);
   }
 }
 
@@ -69,18 +128,96 @@ __device__ __forceinline__ void store_tile(float* Ss, const f32x4 (&acc)[4]) {
     for (int r = 0; r < 4; ++r) Ss[(16 * w + 4 * (lane >> 4) + r) * GP + 16 * nb + (lane & 15)] = acc[nb][r];
 }
 
+// G tile from the logit tile in Ss, split into bf16 hi / lo images. TRANS = false: image rows are
+// the tile's rows i (dV pass: A = G); TRANS = true: rows are the tile's columns j (dT pass: A = G^T).
+template <bool TRANS>
+__device__ __forceinline__ void grad_tile(const float* Ss, bf16_t* Gh, bf16_t* Gl, int B, int K, int r0, int c0,
+                                          const float* __restrict__ den, const float* __restrict__ nom,
+                                          const float* __restrict__ gup) {
+  const int N = B * K;
+  const float gscale = gup[0] / (float)B;  // d loss / d x = (upstream grad) / Bg * (...)
+  // each thread: one image row, 8 consecutive image columns per pass (one 16-B chunk of hi and lo)
+  for (int e = threadIdx.x; e < 64 * 8; e += 256) {
+    const int row = e >> 3, ch = e & 7;
+    float hv[8], lv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int rr = TRANS ? ch * 8 + q : row, cc = TRANS ? row : ch * 8 + q;
+      const int i = r0 + rr, j = c0 + cc;
+      float g = 0.f;
+      if (i < B && j < N) {
+        const float x = Ss[rr * GP + cc];
+        const int blk = j / K;
+        g = __expf(x - den[i]) + __expf(x - den[blk]);
+        if (blk == i) g -= __expf(x - nom[i]);
+        g *= gscale;
+      }
+      hv[q] = g;
+    }
+    uint4 h, l;
+    h = pack8(hv);
+    float hf[8];
+    unpack8(h, hf);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) lv[q] = hv[q] - hf[q];
+    l = pack8(lv);
+    *(uint4*)(Gh + row * KC + sw(row, ch) * 8) = h;
+    *(uint4*)(Gl + row * KC + sw(row, ch) * 8) = l;
+  }
+}
+
 }  // namespace
 
+// X [R][D] fp32 -> h, l [R][D] and th, tl [D][Rp] bf16 (64 x 64 tiles through LDS for the transpose).
+__global__ __launch_bounds__(256) void milnce_split_kernel(const float* __restrict__ X, int R, int D, bf16_t* __restrict__ h,
+                                                           bf16_t* __restrict__ l, bf16_t* __restrict__ th,
+                                                           bf16_t* __restrict__ tl) {
+  __shared__ uint16_t sh[64][66], sl[64][66];
+  const int r0 = blockIdx.x * 64, d0 = blockIdx.y * 64;
+  for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+    const int r = e >> 4, c4 = (e & 15) * 4;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < R) v = *(const float4*)(X + (long long)(r0 + r) * D + d0 + c4);
+    const float f[4] = {v.x, v.y, v.z, v.w};
+    uint16_t hb[4], lb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      hb[q] = f2bf(f[q]);
+      lb[q] = f2bf(f[q] - bf2f(hb[q]));
+      sh[r][c4 + q] = hb[q];
+      sl[r][c4 + q] = lb[q];
+    }
+    if (r0 + r < R) {
+      *(uint2*)(h + (long long)(r0 + r) * D + d0 + c4) =
+          make_uint2(hb[0] | ((uint32_t)hb[1] << 16), hb[2] | ((uint32_t)hb[3] << 16));
+      *(uint2*)(l + (long long)(r0 + r) * D + d0 + c4) =
+          make_uint2(lb[0] | ((uint32_t)lb[1] << 16), lb[2] | ((uint32_t)lb[3] << 16));
+    }
+  }
+  __syncthreads();
+  // transposed copies [D][Rp], Rp = R rounded up to 64: the padding columns are written as zeros
+  // (the backward's staging reads whole 64-column pieces)
+  const long long Rp = (R + 63) / 64 * 64;
+  for (int e = threadIdx.x; e < 64 * 16; e += 256) {
+    const int dd = e >> 4, r4 = (e & 15) * 4;
+    *(uint2*)(th + (long long)(d0 + dd) * Rp + r0 + r4) =
+        make_uint2(sh[r4][dd] | ((uint32_t)sh[r4 + 1][dd] << 16), sh[r4 + 2][dd] | ((uint32_t)sh[r4 + 3][dd] << 16));
+    *(uint2*)(tl + (long long)(d0 + dd) * Rp + r0 + r4) =
+        make_uint2(sl[r4][dd] | ((uint32_t)sl[r4 + 1][dd] << 16), sl[r4 + 2][dd] | ((uint32_t)sl[r4 + 3][dd] << 16));
+  }
+}
+
 // rowpart: [n_ct][B] (max, sum); colpart: [n_rt][B] (max, sum) per text block.
-__global__ __launch_bounds__(256) void milnce_fused_fwd_kernel(const float* __restrict__ V, const float* __restrict__ T,
-                                                               int B, int K, int D, float2* __restrict__ rowpart,
+__global__ __launch_bounds__(256) void milnce_fused_fwd_kernel(Split V, Split T, int B, int K, int D,
+                                                               float2* __restrict__ rowpart,
                                                                float2* __restrict__ colpart) {
-  __shared__ float Vs[TM * SP], Ts[TN * SP], Ss[TM * GP];
+  __shared__ __attribute__((aligned(16))) bf16_t img[4 * IMG];
+  __shared__ float Ss[TM * GP];
   const int N = B * K;
   const int rt = blockIdx.y, ct = blockIdx.x;
   const int r0 = rt * TM, c0 = ct * TN;
   f32x4 acc[4];
-  logit_tile(V, T, B, N, D, r0, c0, Vs, Ts, acc);
+  logit_tile(V, T, B, N, D, r0, c0, img, acc);
   store_tile(Ss, acc);
   __syncthreads();
   const int tid = threadIdx.x;
@@ -158,83 +295,60 @@ __global__ __launch_bounds__(256) void milnce_fused_mean_kernel(const float* __r
   if (threadIdx.x == 0) loss[0] = (red[0] + red[1] + red[2] + red[3]) / (float)B;
 }
 
-namespace {
-
-// G tile from the logit tile (into Ss, in place): rows r0.., columns c0..
-__device__ __forceinline__ void grad_tile(float* Ss, int B, int K, int r0, int c0, const float* __restrict__ den,
-                                          const float* __restrict__ nom, const float* __restrict__ gup) {
+// One backward pass. DT = false: dV[r0 : r0+64, :] = sum over column tiles of G . T (rows of the
+// block = video rows); DT = true: dT[c0 : c0+64, :] = sum over row tiles of G^T . V. The product's
+// B operand is the transposed split copy ([D][R]) of T (resp. V), rows d, k over the tile.
+template <bool DT>
+__global__ __launch_bounds__(256) void milnce_fused_grad_kernel(Split V, Split T, int B, int K, int D,
+                                                                const float* __restrict__ den,
+                                                                const float* __restrict__ nom,
+                                                                const float* __restrict__ gup, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) bf16_t img[4 * IMG];  // logit operands, then the Xt chunk (2 images)
+  __shared__ __attribute__((aligned(16))) bf16_t gimg[2 * IMG];  // G (or G^T) hi / lo
+  __shared__ float Ss[TM * GP];
   const int N = B * K;
-  const float gscale = gup[0] / (float)B;  // d loss / d x = (upstream grad) / Bg * (...)
-  for (int e = threadIdx.x; e < TM * TN; e += 256) {
-    const int rr = e / TN, cc = e - rr * TN;
-    const int i = r0 + rr, j = c0 + cc;
-    float g = 0.f;
-    if (i < B && j < N) {
-      const float x = Ss[rr * GP + cc];
-      const int blk = j / K;
-      g = __expf(x - den[i]) + __expf(x - den[blk]);
-      if (blk == i) g -= __expf(x - nom[i]);
-      g *= gscale;
-    }
-    Ss[rr * GP + cc] = g;
-  }
-}
-
-}  // namespace
-
-// dV[r0 : r0+64, :] = sum over column tiles of G[rows, cols] . T[cols, :]
-__global__ __launch_bounds__(256) void milnce_fused_dv_kernel(const float* __restrict__ V, const float* __restrict__ T,
-                                                              int B, int K, int D, const float* __restrict__ den,
-                                                              const float* __restrict__ nom, const float* __restrict__ gup,
-                                                              float* __restrict__ dV) {
-  extern __shared__ float sm[];
-  float* Vs = sm;                 // [TM][SP]
-  float* Ts = Vs + TM * SP;       // [TN][SP]
-  float* Ss = Ts + TN * SP;       // [TM][GP]
-  float* Tc = Ss + TM * GP;       // [TN][DP]  T chunk for the G GEMM
-  const int N = B * K;
-  const int r0 = blockIdx.x * TM;
+  const int blk = blockIdx.x;
   const int split = blockIdx.y, splits = gridDim.y;
-  dV += (long long)split * B * D;  // split > 0 (or splits > 1): partial sums, reduced afterwards
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ndc = D / DC;
-  f32x4 out[8][4];  // up to D = 512: [d chunk][16-col block] of this wave's 16 rows
+  const int own0 = blk * 64;                       // rows of the output this block owns
+  const int R = DT ? N : B;                        // output rows
+  out += (long long)split * R * D;                 // split > 0 (or splits > 1): partial sums
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ndc = D / KC;
+  f32x4 acc_out[8][4];  // this wave's 16 output rows x D (up to 512)
 #pragma unroll
   for (int a = 0; a < 8; ++a)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int n_ct = (N + TN - 1) / TN;
-  const int ct_begin = (int)((long long)split * n_ct / splits), ct_end = (int)((long long)(split + 1) * n_ct / splits);
-  for (int ct = ct_begin; ct < ct_end; ++ct) {
-    const int c0 = ct * TN;
+    for (int c = 0; c < 4; ++c) acc_out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int n_other = DT ? (B + TM - 1) / TM : (N + TN - 1) / TN;
+  const int t_begin = (int)((long long)split * n_other / splits), t_end = (int)((long long)(split + 1) * n_other / splits);
+  const Split& X = DT ? V : T;  // the operand whose rows the tiles walk (reduction index of the product)
+  const long long xld = ((DT ? B : N) + 63) / 64 * 64;  // row length of its transposed copy
+  for (int t = t_begin; t < t_end; ++t) {
+    const int r0 = DT ? t * TM : own0, c0 = DT ? own0 : t * TN;
     f32x4 acc[4];
-    logit_tile(V, T, B, N, D, r0, c0, Vs, Ts, acc);
+    logit_tile(V, T, B, N, D, r0, c0, img, acc);
     store_tile(Ss, acc);
     __syncthreads();
-    grad_tile(Ss, B, K, r0, c0, den, nom, gup);
+    grad_tile<DT>(Ss, gimg, gimg + IMG, B, K, r0, c0, den, nom, gup);
+    const int x0 = DT ? r0 : c0;  // first row of X in this tile (k range of the product)
+    Stage2 ph, pl;
+    ph.load(X.th, xld, 0, D, x0);
+    pl.load(X.tl, xld, 0, D, x0);
 #pragma unroll
     for (int dc = 0; dc < 8; ++dc) {
       if (dc < ndc) {
+        __syncthreads();  // G images written / previous chunk's fragments read
+        ph.store(img);
+        pl.store(img + IMG);
         __syncthreads();
-        for (int e = tid; e < TN * (DC / 4); e += 256) {
-          const int row = e / (DC / 4), c4 = (e % (DC / 4)) * 4;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (c0 + row < N) v = *(const float4*)(T + (long long)(c0 + row) * D + dc * DC + c4);
-          float* d = Tc + row * DP + c4;
-          d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        if (dc + 1 < ndc) {
+          ph.load(X.th, xld, (dc + 1) * KC, D, x0);
+          pl.load(X.tl, xld, (dc + 1) * KC, D, x0);
         }
-        __syncthreads();
-#pragma unroll 4
-        for (int kk = 0; kk < TN; kk += 4) {
-          const float a = Ss[(16 * w + (lane & 15)) * GP + kk + (lane >> 4)];
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            const float b = Tc[(kk + (lane >> 4)) * DP + 16 * cb + (lane & 15)];
-            out[dc][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, out[dc][cb], 0, 0, 0);
-          }
-        }
+        mfma_chunk(gimg, gimg + IMG, img, img + IMG, 16 * w + (lane & 15), acc_out[dc]);
       }
     }
+    __syncthreads();  // Xt images read before the next tile's logit staging overwrites them
   }
 #pragma unroll
   for (int dc = 0; dc < 8; ++dc)
@@ -243,75 +357,8 @@ __global__ __launch_bounds__(256) void milnce_fused_dv_kernel(const float* __res
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int i = r0 + 16 * w + 4 * (lane >> 4) + r;
-          if (i < B) dV[(long long)i * D + dc * DC + 16 * cb + (lane & 15)] = out[dc][cb][r];
-        }
-}
-
-// dT[c0 : c0+64, :] = sum over row tiles of G[rows, cols]^T . V[rows, :]
-__global__ __launch_bounds__(256) void milnce_fused_dt_kernel(const float* __restrict__ V, const float* __restrict__ T,
-                                                              int B, int K, int D, const float* __restrict__ den,
-                                                              const float* __restrict__ nom, const float* __restrict__ gup,
-                                                              float* __restrict__ dT) {
-  extern __shared__ float sm[];
-  float* Vs = sm;
-  float* Ts = Vs + TM * SP;
-  float* Ss = Ts + TN * SP;
-  float* Vc = Ss + TM * GP;  // [TM][DP] V chunk
-  const int N = B * K;
-  const int c0 = blockIdx.x * TN;
-  const int split = blockIdx.y, splits = gridDim.y;
-  dT += (long long)split * N * D;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ndc = D / DC;
-  f32x4 out[8][4];  // this wave's 16 text rows (tile columns 16w..) x D
-#pragma unroll
-  for (int a = 0; a < 8; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int n_rt = (B + TM - 1) / TM;
-  const int rt_begin = (int)((long long)split * n_rt / splits), rt_end = (int)((long long)(split + 1) * n_rt / splits);
-  for (int rt = rt_begin; rt < rt_end; ++rt) {
-    const int r0 = rt * TM;
-    f32x4 acc[4];
-    logit_tile(V, T, B, N, D, r0, c0, Vs, Ts, acc);
-    store_tile(Ss, acc);
-    __syncthreads();
-    grad_tile(Ss, B, K, r0, c0, den, nom, gup);
-#pragma unroll
-    for (int dc = 0; dc < 8; ++dc) {
-      if (dc < ndc) {
-        __syncthreads();
-        for (int e = tid; e < TM * (DC / 4); e += 256) {
-          const int row = e / (DC / 4), c4 = (e % (DC / 4)) * 4;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (r0 + row < B) v = *(const float4*)(V + (long long)(r0 + row) * D + dc * DC + c4);
-          float* d = Vc + row * DP + c4;
-          d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int kk = 0; kk < TM; kk += 4) {
-          // A = G^T: A[i = text row 16w + (lane&15)][k = video row kk + (lane>>4)]
-          const float a = Ss[(kk + (lane >> 4)) * GP + 16 * w + (lane & 15)];
-#pragma unroll
-          for (int cb = 0; cb < 4; ++cb) {
-            const float b = Vc[(kk + (lane >> 4)) * DP + 16 * cb + (lane & 15)];
-            out[dc][cb] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, out[dc][cb], 0, 0, 0);
-          }
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int dc = 0; dc < 8; ++dc)
-    if (dc < ndc)
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int j = c0 + 16 * w + 4 * (lane >> 4) + r;
-          if (j < N) dT[(long long)j * D + dc * DC + 16 * cb + (lane & 15)] = out[dc][cb][r];
+          const int i = own0 + 16 * w + 4 * (lane >> 4) + r;
+          if (i < R) out[(long long)i * D + dc * KC + 16 * cb + (lane & 15)] = acc_out[dc][cb][r];
         }
 }
 
@@ -327,6 +374,39 @@ __global__ void milnce_split_sum_kernel(const float4* __restrict__ part, int spl
   }
 }
 
+namespace {
+
+// workspace layout (floats): rowpart [n_ct][B] float2, colpart [n_rt][B] float2, li [B], then the
+// split copies of V and T (bf16: 4 [R][D] arrays each = 2 floats per element)
+struct FusedWs {
+  float2* rowpart;
+  float2* colpart;
+  float* li;
+  Split V, T;
+};
+
+FusedWs carve(float* ws, int B, int K, int D) {
+  const long long N = (long long)B * K;
+  const long long n_ct = (N + TN - 1) / TN, n_rt = (B + TM - 1) / TM;
+  FusedWs w;
+  w.rowpart = (float2*)ws;
+  w.colpart = w.rowpart + n_ct * B;
+  w.li = (float*)(w.colpart + n_rt * B);
+  long long off = 2 * (n_ct * B + n_rt * B) + B;
+  off = (off + 63) / 64 * 64;  // 256-B alignment of the bf16 arrays
+  bf16_t* p = (bf16_t*)(ws + off);
+  const long long vb = (long long)B * D, vtb = (long long)D * ((B + 63) / 64 * 64);
+  const long long tb = N * D, ttb = (long long)D * ((N + 63) / 64 * 64);
+  w.V = {p, p + vb, p + 2 * vb, p + 2 * vb + vtb};
+  p += 2 * vb + 2 * vtb;
+  w.T = {p, p + tb, p + 2 * tb, p + 2 * tb + ttb};
+  return w;
+}
+
+bool geometry_ok(int B, int K, int D) { return K >= 1 && TN % K == 0 && D % KC == 0 && D <= 8 * KC && B >= 1; }
+
+}  // namespace
+
 // Split counts of the two backward passes: ~2 workgroups per CU over (tiles x reduction ranges).
 MILNCE_API int milnce_fused_bwd_splits(int B, int K, int* s_dv, int* s_dt) {
   const int N = B * K;
@@ -337,41 +417,48 @@ MILNCE_API int milnce_fused_bwd_splits(int B, int K, int* s_dv, int* s_dt) {
   return 0;
 }
 
-// Workspace floats needed by the fused forward (row + column partials).
-MILNCE_API long long milnce_fused_ws_floats(int B, int K) {
+// Workspace floats of the fused loss (partials + the split operand copies the backward reuses).
+MILNCE_API long long milnce_fused_ws_floats(int B, int K, int D) {
   const long long N = (long long)B * K;
   const long long n_ct = (N + TN - 1) / TN, n_rt = (B + TM - 1) / TM;
-  return 2 * (n_ct * B + n_rt * B) + B;
+  const long long off = (2 * (n_ct * B + n_rt * B) + B + 63) / 64 * 64;
+  const long long Bp = ((long long)B + 63) / 64 * 64, Np = (N + 63) / 64 * 64;
+  return off + ((long long)B + Bp + N + Np) * D;  // 4 bf16 arrays per matrix = (R + Rp) D floats
 }
 
 MILNCE_API int milnce_fused_fwd(const float* V, const float* T, int B, int K, int D, float* ws, float* den, float* nom,
                                 float* loss, hipStream_t stream) {
-  if (K < 1 || TN % K || D % DC || D > 8 * DC) return (int)hipErrorInvalidValue;
+  if (!geometry_ok(B, K, D)) return (int)hipErrorInvalidValue;
   const int N = B * K;
   const int n_ct = (N + TN - 1) / TN, n_rt = (B + TM - 1) / TM;
-  float2* rowpart = (float2*)ws;
-  float2* colpart = rowpart + (long long)n_ct * B;
-  float* li = (float*)(colpart + (long long)n_rt * B);
-  hipLaunchKernelGGL(milnce_fused_fwd_kernel, dim3(n_ct, n_rt), dim3(256), 0, stream, V, T, B, K, D, rowpart, colpart);
+  FusedWs w = carve(ws, B, K, D);
+  hipLaunchKernelGGL(milnce_split_kernel, dim3((B + 63) / 64, D / 64), dim3(256), 0, stream, V, B, D,
+                     (bf16_t*)w.V.h, (bf16_t*)w.V.l, (bf16_t*)w.V.th, (bf16_t*)w.V.tl);
   HIP_RET(hipGetLastError());
-  hipLaunchKernelGGL(milnce_fused_finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, V, T, B, K, D, rowpart,
-                     n_ct, colpart, n_rt, den, nom, li);
+  hipLaunchKernelGGL(milnce_split_kernel, dim3((N + 63) / 64, D / 64), dim3(256), 0, stream, T, N, D,
+                     (bf16_t*)w.T.h, (bf16_t*)w.T.l, (bf16_t*)w.T.th, (bf16_t*)w.T.tl);
   HIP_RET(hipGetLastError());
-  hipLaunchKernelGGL(milnce_fused_mean_kernel, dim3(1), dim3(256), 0, stream, li, B, loss);
+  hipLaunchKernelGGL(milnce_fused_fwd_kernel, dim3(n_ct, n_rt), dim3(256), 0, stream, w.V, w.T, B, K, D, w.rowpart,
+                     w.colpart);
+  HIP_RET(hipGetLastError());
+  hipLaunchKernelGGL(milnce_fused_finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, V, T, B, K, D, w.rowpart,
+                     n_ct, w.colpart, n_rt, den, nom, w.li);
+  HIP_RET(hipGetLastError());
+  hipLaunchKernelGGL(milnce_fused_mean_kernel, dim3(1), dim3(256), 0, stream, w.li, B, loss);
   return (int)hipGetLastError();
 }
 
-// dV / dT; with s_dv / s_dt > 1 the passes write partial sums to `part` ([s][B][D] then [s][N][D])
-// which are summed into dV / dT.
-MILNCE_API int milnce_fused_bwd(const float* V, const float* T, int B, int K, int D, const float* den, const float* nom,
+// dV / dT from the forward's workspace (its split copies); with s_dv / s_dt > 1 the passes write
+// partial sums to `part` ([s][B][D] then [s][N][D]) which are summed into dV / dT.
+MILNCE_API int milnce_fused_bwd(const float* ws, int B, int K, int D, const float* den, const float* nom,
                                 const float* gup, float* dV, float* dT, int s_dv, int s_dt, float* part,
                                 hipStream_t stream) {
-  if (K < 1 || TN % K || D % DC || D > 8 * DC) return (int)hipErrorInvalidValue;
+  if (!geometry_ok(B, K, D)) return (int)hipErrorInvalidValue;
   const int N = B * K;
-  const size_t lds = (size_t)(TM * SP + TN * SP + TM * GP + 64 * DP) * sizeof(float);
+  FusedWs w = carve((float*)ws, B, K, D);
   float* pv = s_dv > 1 ? part : dV;
-  hipLaunchKernelGGL(milnce_fused_dv_kernel, dim3((B + TM - 1) / TM, s_dv), dim3(256), lds, stream, V, T, B, K, D,
-                     den, nom, gup, pv);
+  hipLaunchKernelGGL(milnce_fused_grad_kernel<false>, dim3((B + TM - 1) / TM, s_dv), dim3(256), 0, stream, w.V, w.T,
+                     B, K, D, den, nom, gup, pv);
   HIP_RET(hipGetLastError());
   if (s_dv > 1) {
     const long long n4 = (long long)B * D / 4;
@@ -380,8 +467,8 @@ MILNCE_API int milnce_fused_bwd(const float* V, const float* T, int B, int K, in
     HIP_RET(hipGetLastError());
   }
   float* pt = s_dt > 1 ? part : dT;
-  hipLaunchKernelGGL(milnce_fused_dt_kernel, dim3((N + TN - 1) / TN, s_dt), dim3(256), lds, stream, V, T, B, K, D,
-                     den, nom, gup, pt);
+  hipLaunchKernelGGL(milnce_fused_grad_kernel<true>, dim3((N + TN - 1) / TN, s_dt), dim3(256), 0, stream, w.V, w.T,
+                     B, K, D, den, nom, gup, pt);
   HIP_RET(hipGetLastError());
   if (s_dt > 1) {
     const long long n4 = (long long)N * D / 4;

@@ -220,7 +220,7 @@ class S3D(nn.Module):
         if v.dtype == torch.uint8:
             v = v.to(wdt) / 255.0
         v = v.contiguous()
-        if video.is_cuda:
+        if video.is_cuda and not ops.keep_dtype():
             return v.to(torch.bfloat16)
         return v.to(wdt)
 

@@ -24,16 +24,31 @@ def use_hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_ATEN
 
 
+_KEEP_DTYPE = False
+
+
+def keep_dtype() -> bool:
+    """True inside ``force_aten(keep_dtype=True)``: the ATen path on GPU computes in the model's
+    parameter dtype (an fp32 reference) instead of bf16 activations."""
+    return _KEEP_DTYPE
+
+
 class force_aten:
-    """Context manager: run the ATen implementations on GPU too (A/B comparisons in tests)."""
+    """Context manager: run the ATen implementations on GPU too (A/B comparisons in tests).
+    ``keep_dtype=True`` also keeps the activations in the parameters' dtype (fp32 oracle)."""
+
+    def __init__(self, keep_dtype: bool = False):
+        self.keep = keep_dtype
 
     def __enter__(self):
-        global _FORCE_ATEN
+        global _FORCE_ATEN, _KEEP_DTYPE
         self._prev, _FORCE_ATEN = _FORCE_ATEN, True
+        self._prev_keep, _KEEP_DTYPE = _KEEP_DTYPE, self.keep
 
     def __exit__(self, *exc):
-        global _FORCE_ATEN
+        global _FORCE_ATEN, _KEEP_DTYPE
         _FORCE_ATEN = self._prev
+        _KEEP_DTYPE = self._prev_keep
 
 
 def _hip():

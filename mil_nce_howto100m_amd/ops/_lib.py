@@ -63,13 +63,19 @@ SIGNATURES: Dict[str, list] = {
     "milnce_text_fc1_max": [P, I, I, P, P, P, I, I, P, P, P],
     "milnce_loss_fwd": [P, I, I, P, P, P, P],
     "milnce_fused_fwd": [P, P, I, I, I, P, P, P, P, P],
-    "milnce_fused_bwd": [P, P, I, I, I, P, P, P, P, P, I, I, P, P],
+    "milnce_fused_bwd": [P, I, I, I, P, P, P, P, P, I, I, P, P],
+    "milnce_fused_ws_floats": [I, I, I],
     "milnce_fused_bwd_splits": [I, I, P, P],
     "milnce_loss_bwd": [P, P, P, P, I, I, P, P],
-    "milnce_softdtw_fwd": [P, I, I, I, I, I, L, L, F, F, P, P, P],
-    "milnce_softdtw_bwd": [P, P, I, I, I, I, I, L, L, F, F, P, P, P],
+    "milnce_softdtw_fwd": [P, I, I, I, I, I, L, L, F, F, I, P, P, L, L, L, L, P, P, P],
+    "milnce_softdtw_bwd": [P, P, I, I, I, I, I, L, L, F, F, I, P, P, L, L, L, L, P, P, P, P, P],
+    "milnce_rowstat": [P, L, I, I, P, P],
+    "milnce_rowscale_add": [P, P, P, L, I, P],
     "milnce_dtw_path": [P, I, I, I, P, P, P],
 }
+
+# entry points that return something other than an int status
+RESTYPES = {"milnce_fused_ws_floats": ctypes.c_longlong}
 
 _lib = None
 
@@ -92,7 +98,7 @@ def lib():
         if fn is None:
             continue
         fn.argtypes = argtypes
-        fn.restype = c_int
+        fn.restype = RESTYPES.get(name, c_int)
     _lib = l
     return l
 

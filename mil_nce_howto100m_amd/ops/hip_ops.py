@@ -1683,35 +1683,36 @@ class _MILNCE(torch.autograd.Function):
 
 
 class _MILNCEFused(torch.autograd.Function):
-    """MIL-NCE without the [Bg, Bg*K] logits (csrc/milnce_fused.hip): tiled fp32-MFMA logits with
-    row / block-column log-sum-exp partials forward, tile-wise recompute backward."""
+    """MIL-NCE without the [Bg, Bg*K] logits (csrc/milnce_fused.hip): split-bf16 MFMA logit tiles
+    with row / block-column log-sum-exp partials forward, tile-wise recompute backward. The
+    workspace (partials + the split operand copies) is kept for the backward."""
 
     @staticmethod
     def forward(ctx, v, t):
         B, D = v.shape
         K = t.shape[0] // B
-        n_ct, n_rt = _ceil(B * K, 64), _ceil(B, 64)
-        ws = torch.empty((2 * (n_ct * B + n_rt * B) + B,), dtype=F32, device=v.device)
+        ws = torch.empty((int(lib().milnce_fused_ws_floats(B, K, D)),), dtype=F32, device=v.device)
         den = torch.empty((B,), dtype=F32, device=v.device)
         nom = torch.empty((B,), dtype=F32, device=v.device)
         loss = torch.empty((1,), dtype=F32, device=v.device)
         call("milnce_fused_fwd", ptr(v), ptr(t), B, K, D, ptr(ws), ptr(den), ptr(nom), ptr(loss), stream())
-        ctx.save_for_backward(v, t, den, nom)
+        ctx.save_for_backward(ws, den, nom)
+        ctx.dims = (B, K, D)
         return loss.view(())
 
     @staticmethod
     def backward(ctx, g):
-        v, t, den, nom = ctx.saved_tensors
-        B, D = v.shape
-        K = t.shape[0] // B
-        dv, dt = torch.empty_like(v), torch.empty_like(t)
+        ws, den, nom = ctx.saved_tensors
+        B, K, D = ctx.dims
+        dv = torch.empty((B, D), dtype=F32, device=ws.device)
+        dt = torch.empty((B * K, D), dtype=F32, device=ws.device)
         gg = g.reshape(1).float().contiguous()
         sv, st = ctypes.c_int(1), ctypes.c_int(1)
         lib().milnce_fused_bwd_splits(B, K, ctypes.byref(sv), ctypes.byref(st))
         sv, st = int(sv.value), int(st.value)
         part = torch.empty((max(sv * B, st * B * K if st > 1 else 0) * D if max(sv, st) > 1 else 1,), dtype=F32,
-                           device=v.device)
-        call("milnce_fused_bwd", ptr(v), ptr(t), B, K, D, ptr(den), ptr(nom), ptr(gg), ptr(dv), ptr(dt), sv, st,
+                           device=ws.device)
+        call("milnce_fused_bwd", ptr(ws), B, K, D, ptr(den), ptr(nom), ptr(gg), ptr(dv), ptr(dt), sv, st,
              ptr(part), stream())
         return dv, dt
 

@@ -2,9 +2,10 @@
 
 * GPU: the wavefront DP is a HIP kernel (``csrc/softdtw.hip``), one workgroup per pair, one
   lane per row, R kept for the backward; the backward is the reverse wavefront. The distance
-  matrix is produced by one batched GEMM (hipBLASLt) — never by the reference's
-  ``[B, N, M, D]`` expand — and the all-pairs form reads every pair's block in place from a
-  single ``[b*n, b*m]`` GEMM output.
+  function is fused into both kernels: they read the GEMM output S = X Y^T (one batched GEMM,
+  hipBLASLt — never the reference's ``[B, N, M, D]`` expand; the all-pairs form reads every
+  pair's block in place from a single ``[b*n, b*m]`` GEMM output) through f(S, row norms), and
+  the backward emits dL/dS and the norm terms directly (``_SoftDTWFusedHIP``).
 * CPU: a float64 numpy implementation of the same recursions (the oracle for the GPU kernel,
   mirroring the reference's Numba CPU path ``soft_dtw_cuda.py:185-240``).
 
@@ -150,7 +151,7 @@ class _SoftDTWHIP(torch.autograd.Function):
         R = torch.empty((P, n + 2, m + 2), dtype=torch.float64, device=D.device)
         out = torch.empty((P,), dtype=torch.float32, device=D.device)
         call("milnce_softdtw_fwd", ptr(D), P, n, m, ld, div, s_i, s_j, float(gamma), float(bandwidth),
-             ptr(R), ptr(out), stream())
+             0, None, None, 0, 0, 0, 0, ptr(R), ptr(out), stream())
         ctx.save_for_backward(D, R)
         ctx.meta = (gamma, bandwidth, pairs_b, P, n, m, ld, div, s_i, s_j)
         return out
@@ -162,11 +163,87 @@ class _SoftDTWHIP(torch.autograd.Function):
         gamma, bw, pairs_b, P, n, m, ld, div, s_i, s_j = ctx.meta
         G = torch.empty((P, n, m), dtype=torch.float32, device=D.device)
         call("milnce_softdtw_bwd", ptr(D), ptr(R), P, n, m, ld, div, s_i, s_j, float(gamma), float(bw),
-             ptr(g.float().contiguous()), ptr(G), stream())
+             0, None, None, 0, 0, 0, 0, None, None, ptr(g.float().contiguous()), ptr(G), stream())
         if pairs_b:
             b = pairs_b
             G = G.view(b, b, n, m).permute(0, 2, 1, 3).reshape(b * n, b * m)
         return G, None, None, None
+
+
+# distance functions the HIP kernels apply to the GEMM output in place (csrc/softdtw.hip DistKind)
+_DIST_KIND = {"negative_dot": 1, "cosine": 2, "negative_cosine": 3, None: 4, "sqeuclidean": 4, "euclidean": 5}
+
+
+class _SoftDTWFusedHIP(torch.autograd.Function):
+    """Soft-DTW of X, Y with the distance function fused into the wavefront kernels
+    (``soft_dtw_cuda.py:325-363``): one GEMM S = X Y^T (hipBLASLt) and per-row norms are the only
+    other work; the forward reads D = f(S) cell by cell, the backward writes dS = dL/dD * f'(S) in
+    S's layout plus the norm terms as per-row coefficients, so dX = dS Y + ca * X, dY = dS^T X +
+    cb * Y (two GEMMs and a row-scaled add). No [P, n, m] elementwise pass runs in ATen.
+    Layout 'batch': X [P, n, d], Y [P, m, d]; 'pairs' (pairs_b = b): X [b*n, d], Y [b*m, d], all
+    b*b pairs from one [b*n, b*m] GEMM."""
+
+    @staticmethod
+    def forward(ctx, X, Y, kind, gamma, bandwidth, pairs_b):
+        from ._lib import call, ptr, stream
+        Xf, Yf = X.float().contiguous(), Y.float().contiguous()
+        d = Xf.shape[-1]
+        if pairs_b:
+            b = pairs_b
+            n, m = Xf.shape[0] // b, Yf.shape[0] // b
+            S = torch.mm(Xf, Yf.t())
+            P, ld, div, s_i, s_j = b * b, b * m, b, n * b * m, m
+            a_si, a_sj, b_si, b_sj = n, 0, 0, m
+        else:
+            P, n, _ = Xf.shape
+            m = Yf.shape[1]
+            S = torch.bmm(Xf, Yf.transpose(1, 2))
+            ld, div, s_i, s_j = m, 1, n * m, 0
+            a_si, a_sj, b_si, b_sj = n, 0, m, 0
+        stats = kind >= 2
+        sq = int(kind >= 4)
+        A = Bs = None
+        if stats:
+            A = torch.empty((Xf.numel() // d,), dtype=torch.float32, device=X.device)
+            Bs = torch.empty((Yf.numel() // d,), dtype=torch.float32, device=X.device)
+            call("milnce_rowstat", ptr(Xf), A.numel(), d, sq, ptr(A), stream())
+            call("milnce_rowstat", ptr(Yf), Bs.numel(), d, sq, ptr(Bs), stream())
+        R = torch.empty((P, n + 2, m + 2), dtype=torch.float64, device=X.device)
+        out = torch.empty((P,), dtype=torch.float32, device=X.device)
+        call("milnce_softdtw_fwd", ptr(S), P, n, m, ld, div, s_i, s_j, float(gamma), float(bandwidth), kind,
+             ptr(A), ptr(Bs), a_si, a_sj, b_si, b_sj, ptr(R), ptr(out), stream())
+        ctx.save_for_backward(Xf, Yf, S, R, A, Bs)
+        ctx.meta = (kind, gamma, bandwidth, pairs_b, P, n, m, ld, div, s_i, s_j, a_si, a_sj, b_si, b_sj,
+                    X.dtype, Y.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ._lib import call, ptr, stream
+        Xf, Yf, S, R, A, Bs = ctx.saved_tensors
+        (kind, gamma, bw, pairs_b, P, n, m, ld, div, s_i, s_j, a_si, a_sj, b_si, b_sj, xdt, ydt) = ctx.meta
+        dS = torch.empty_like(S)
+        stats = kind >= 2
+        ca = torch.zeros_like(A) if stats else None
+        cb = torch.zeros_like(Bs) if stats else None
+        call("milnce_softdtw_bwd", ptr(S), ptr(R), P, n, m, ld, div, s_i, s_j, float(gamma), float(bw), kind,
+             ptr(A), ptr(Bs), a_si, a_sj, b_si, b_sj, ptr(ca), ptr(cb), ptr(g.float().contiguous()), ptr(dS),
+             stream())
+        if pairs_b:
+            dX, dY = torch.mm(dS, Yf), torch.mm(dS.t(), Xf)
+        else:
+            dX, dY = torch.bmm(dS, Yf), torch.bmm(dS.transpose(1, 2), Xf)
+        d = Xf.shape[-1]
+        if stats:
+            call("milnce_rowscale_add", ptr(dX), ptr(Xf), ptr(ca), ca.numel(), d, stream())
+            call("milnce_rowscale_add", ptr(dY), ptr(Yf), ptr(cb), cb.numel(), d, stream())
+        return dX.to(xdt), dY.to(ydt), None, None, None, None
+
+
+def _fused_ok(X: torch.Tensor, Y: torch.Tensor, dist_func, pairs: bool) -> bool:
+    """GPU tensors, a distance the kernels implement, rows of whole float4s (the row-statistic
+    kernels); ``SoftDTW`` then also checks the sequence length against GPU_MAX_N."""
+    return use_hip(X) and dist_func in _DIST_KIND and X.shape[-1] % 4 == 0
 
 
 GPU_MAX_N = 6600  # csrc/softdtw.hip kSdtwMaxN: the LDS ring holds 3 x (N + 2) doubles
@@ -204,20 +281,28 @@ class SoftDTW(torch.nn.Module):
         self.use_cuda = use_cuda  # device placement follows the inputs
         self.dist_func = dist_func
 
+    def _sdtw(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
+        if _fused_ok(X, Y, self.dist_func, False) and X.shape[-2] <= GPU_MAX_N:
+            return _SoftDTWFusedHIP.apply(X, Y, _DIST_KIND[self.dist_func], self.gamma, self.bandwidth, 0)
+        return softdtw_from_dist(dist_matrix(X, Y, self.dist_func), self.gamma, self.bandwidth)
+
     def forward(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
         assert X.shape[0] == Y.shape[0] and X.shape[2] == Y.shape[2]
         if self.normalize:
             x = torch.cat([X, X, Y])
             y = torch.cat([Y, X, Y])
-            out = softdtw_from_dist(dist_matrix(x, y, self.dist_func), self.gamma, self.bandwidth)
+            out = self._sdtw(x, y)
             out_xy, out_xx, out_yy = torch.split(out, X.shape[0])
             return out_xy - 0.5 * (out_xx + out_yy)
-        return softdtw_from_dist(dist_matrix(X, Y, self.dist_func), self.gamma, self.bandwidth)
+        return self._sdtw(X, Y)
 
     def pairwise(self, X: torch.Tensor, Y: torch.Tensor) -> torch.Tensor:
         """[b, n, d] x [b, m, d] -> [b, b] with out[i, j] = sdtw(X[i], Y[j]); one GEMM."""
         b, n, d = X.shape
         m = Y.shape[1]
+        if _fused_ok(X, Y, self.dist_func, True) and n <= GPU_MAX_N:
+            return _SoftDTWFusedHIP.apply(X.reshape(b * n, d), Y.reshape(b * m, d), _DIST_KIND[self.dist_func],
+                                          self.gamma, self.bandwidth, b).view(b, b)
         Dbig = dist_matrix(X.reshape(b * n, d), Y.reshape(b * m, d), self.dist_func)
         return softdtw_pairwise_from_dist(Dbig, b, self.gamma, self.bandwidth)
 

@@ -46,7 +46,7 @@ def test_halo_wgrad_matches_fp32(shape, cc):
                                         (96, 8, 0.05), (2048, 4, 0.05)])
 def test_fused_milnce_matches_fp64(B, K, scale):
     """Fused MIL-NCE (csrc/milnce_fused.hip, no [Bg, Bg*K] tensor) vs the loss.py formula in fp64:
-    loss and both gradients; B not a multiple of the 64-tile, every K that divides 64."""
+    loss and both gradients to 1e-4 relative; B not a multiple of the 64-tile, every K that divides 64."""
     from mil_nce_howto100m_amd.ops import aten
     from mil_nce_howto100m_amd.ops import hip_ops as h
     torch.manual_seed(B + K)
@@ -59,14 +59,15 @@ def test_fused_milnce_matches_fp64(B, K, scale):
     tr = t.detach().double().cpu().requires_grad_(True)
     lr = aten.milnce_loss(vr, tr)
     (lr * 1.7).backward()
-    assert abs(loss.item() - lr.item()) < 1e-5 * max(1.0, abs(lr.item())), (loss.item(), lr.item())
+    # split-bf16 logits (hi*hi + hi*lo + lo*hi, 16 significant bits per operand): 1e-4 relative
+    assert abs(loss.item() - lr.item()) < 1e-4 * max(1.0, abs(lr.item())), (loss.item(), lr.item())
     rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
     assert rel(v.grad, vr.grad) < 1e-4 and rel(t.grad, tr.grad) < 1e-4, (rel(v.grad, vr.grad), rel(t.grad, tr.grad))
 
 
 def test_fused_milnce_memory_and_time_at_8192():
-    """BASELINE config 5's global batch (Bg = 8192, K = 4): the fused loss allocates ~1 MiB of
-    workspace instead of two 1 GiB logit / dlogit tensors."""
+    """BASELINE config 5's global batch (Bg = 8192, K = 4): the fused loss's workspace (partials and
+    the split-bf16 operand copies, ~170 MiB) instead of two 1 GiB logit / dlogit tensors."""
     import time
     from mil_nce_howto100m_amd.ops import hip_ops as h
     B, K = 8192, 4

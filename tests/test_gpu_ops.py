@@ -685,41 +685,56 @@ def test_stem_uint8_input(S, fused):
     assert torch.isfinite(ws[0].grad).all()
 
 
-@pytest.mark.parametrize("dist", ["cosine", "negative_dot", None])
+@pytest.mark.parametrize("dist", ["cosine", "negative_dot", None, "negative_cosine", "euclidean"])
 @pytest.mark.parametrize("B,N,M,bw", [(4, 8, 8, 0.0), (3, 17, 15, 0.0), (2, 70, 66, 0.0), (2, 12, 12, 3.0),
                                       (1, 1500, 40, 0.0)])
 def test_softdtw_vs_cpu_oracle(dist, B, N, M, bw):
+    """Fused-distance soft-DTW (csrc/softdtw.hip reads the GEMM output through the distance
+    function; the backward emits dS and the norm terms) against the fp64 CPU oracle on the
+    ATen distance matrix: value and both input gradients."""
     from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
     torch.manual_seed(7)
-    x = torch.randn(B, N, 16, device=DEV, requires_grad=True)
-    y = torch.randn(B, M, 16, device=DEV)
+    scale = 0.15 if dist == "euclidean" else 1.0  # exp(||x - y||) stays O(10)
+    x = (torch.randn(B, N, 16, device=DEV) * scale).requires_grad_(True)
+    y = (torch.randn(B, M, 16, device=DEV) * scale).requires_grad_(True)
     gamma = 0.1
     sd = SoftDTW(True, gamma=gamma, bandwidth=bw if bw > 0 else None, dist_func=dist)
     out = sd(x, y)
-    xc = x.detach().cpu().requires_grad_(True)
-    outc = sd(xc, y.cpu())
-    assert torch.allclose(out.cpu(), outc, rtol=1e-3, atol=1e-3)
-    out.sum().backward()
-    outc.sum().backward()
-    assert rel_err(x.grad.cpu(), xc.grad) < 1e-3
+    xc = x.detach().cpu().double().requires_grad_(True)
+    yc = y.detach().cpu().double().requires_grad_(True)
+    outc = sd(xc, yc)
+    assert torch.allclose(out.cpu().double(), outc, rtol=1e-3, atol=1e-3)
+    w = torch.randn(B, dtype=torch.float64)
+    (out.double() * w.to(DEV)).sum().backward()
+    (outc * w).sum().backward()
+    assert rel_err(x.grad.cpu(), xc.grad) < 1e-3 and rel_err(y.grad.cpu(), yc.grad) < 1e-3
 
 
-def test_softdtw_pairwise_matches_batched():
+@pytest.mark.parametrize("dist", ["negative_dot", "cosine"])
+def test_softdtw_pairwise_matches_batched(dist):
+    """All b*b pairs from one GEMM with the distance fused (pairs layout: X / Y rows and their
+    norm coefficients shared by b pairs) vs the expanded batch and the fp64 CPU oracle."""
     from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
     torch.manual_seed(8)
     b, n, d = 6, 8, 32
     v = torch.randn(b, n, d, device=DEV, requires_grad=True)
-    t = torch.randn(b, n, d, device=DEV)
-    sd = SoftDTW(True, gamma=0.1, dist_func="negative_dot")
+    t = torch.randn(b, n, d, device=DEV, requires_grad=True)
+    sd = SoftDTW(True, gamma=0.1, dist_func=dist)
     pw = sd.pairwise(v, t)
     row = v.unsqueeze(1).expand(b, b, n, d).reshape(-1, n, d)
     col = t.unsqueeze(0).expand(b, b, n, d).reshape(-1, n, d)
     ref = sd(row, col).view(b, b)
     assert torch.allclose(pw, ref, rtol=1e-4, atol=1e-4)
+    vc = v.detach().cpu().double().requires_grad_(True)
+    tc = t.detach().cpu().double().requires_grad_(True)
+    pc = sd.pairwise(vc, tc)
+    assert torch.allclose(pw.cpu().double(), pc, rtol=1e-4, atol=1e-4)
     g = torch.randn(b, b, device=DEV)
-    (gv,) = torch.autograd.grad((pw * g).sum(), v)
-    (gr,) = torch.autograd.grad((ref * g).sum(), v)
-    assert rel_err(gv, gr) < 1e-4
+    gv, gt = torch.autograd.grad((pw * g).sum(), (v, t))
+    gr, gtr = torch.autograd.grad((ref * g).sum(), (v, t))
+    gvc, gtc = torch.autograd.grad((pc * g.cpu().double()).sum(), (vc, tc))
+    assert rel_err(gv, gr) < 1e-4 and rel_err(gt, gtr) < 1e-4
+    assert rel_err(gv.cpu(), gvc) < 1e-3 and rel_err(gt.cpu(), gtc) < 1e-3
 
 
 def test_hard_dtw_path_matches_cpu():
