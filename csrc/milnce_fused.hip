@@ -8,7 +8,7 @@
 //   split   : V, T (fp32) -> row-major [R][D] hi/lo and transposed [D][Rp] hi/lo bf16 copies (the
 //             transposed ones make the backward's reductions over the batch k-contiguous MFMA
 //             operands, like the forward's);
-//   forward : 64 x 64 logit tiles (4 waves x 16 rows), per tile a row partial (max, sum e^{x-max})
+//   forward : 64 x 64 logit tiles (8 waves x 16 rows x 32 columns), per tile a row partial (max, sum e^{x-max})
 //             over its 64 columns and, for each of its 64/K text blocks, a block-column partial
 //             over its 64 rows; a finalize kernel merges them into den_i = LSE(row_i U blockcol_i)
 //             and takes nom_i = LSE_k V_i . T_{iK+k} (positives counted twice, as in the reference);
@@ -38,24 +38,19 @@ __device__ __forceinline__ void lse_add(float& m, float& s, float m2, float s2) 
 
 __device__ __forceinline__ int sw(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+constexpr int NT = 512;  // 8 waves per workgroup
+
 // Register staging of 64 rows x 64 columns of a bf16 [rows][ld] matrix (rows >= nrows read 0):
-// two 16-B pieces per thread.
-struct Stage2 {
-  uint4 v[2];
+// one 16-B piece per thread.
+struct Stage1 {
+  uint4 v;
   __device__ __forceinline__ void load(const bf16_t* __restrict__ src, long long ld, int row0, int nrows, int col0) {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int e = threadIdx.x + it * 256, r = e >> 3, c = e & 7;
-      v[it] = row0 + r < nrows ? *(const uint4*)(src + (long long)(row0 + r) * ld + col0 + c * 8)
-                               : make_uint4(0u, 0u, 0u, 0u);
-    }
+    const int r = threadIdx.x >> 3, c = threadIdx.x & 7;
+    v = row0 + r < nrows ? *(const uint4*)(src + (long long)(row0 + r) * ld + col0 + c * 8) : make_uint4(0u, 0u, 0u, 0u);
   }
   __device__ __forceinline__ void store(bf16_t* img) const {
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int e = threadIdx.x + it * 256, r = e >> 3, c = e & 7;
-      *(uint4*)(img + r * KC + sw(r, c) * 8) = v[it];
-    }
+    const int r = threadIdx.x >> 3, c = threadIdx.x & 7;
+    *(uint4*)(img + r * KC + sw(r, c) * 8) = v;
   }
 };
 
@@ -66,16 +61,17 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int row, int s) {
 }
 
 // acc += A B^T over one staged 64-wide K chunk with split operands: A rows arow (16 per wave),
-// B rows 16 cb + (lane & 15) for cb = 0..3.
+// B rows 16 (cb0 + cb) + (lane & 15) for cb < NB.
+template <int NB>
 __device__ __forceinline__ void mfma_chunk(const bf16_t* Ah, const bf16_t* Al, const bf16_t* Bh, const bf16_t* Bl,
-                                           int arow, f32x4 (&acc)[4]) {
+                                           int arow, int cb0, f32x4 (&acc)[NB]) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const bf16x8 ah = frag(Ah, arow, s), al = frag(Al, arow, s);
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const int br = 16 * cb + (lane & 15);
+    for (int cb = 0; cb < NB; ++cb) {
+      const int br = 16 * (cb0 + cb) + (lane & 15);
       const bf16x8 bh = frag(Bh, br, s), bl = frag(Bl, br, s);
       acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc[cb], 0, 0, 0);
       acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc[cb], 0, 0, 0);
@@ -91,14 +87,15 @@ struct Split {  // split copies of one fp32 matrix X [R][D]
   const bf16_t* tl;
 };
 
-// S[64 x 64] = V[r0 : r0+64] . T[c0 : c0+64]^T into acc (wave w: rows 16w.., all 4 column blocks;
-// acc[cb][r] = S[16w + 4*(lane>>4) + r][16 cb + (lane & 15)]). img: 4 images (Vh, Vl, Th, Tl).
+// S[64 x 64] = V[r0 : r0+64] . T[c0 : c0+64]^T, 8 waves: wave w holds rows 16 (w & 3).. and the
+// two 16-column blocks 2 (w >> 2) + cb (acc[cb][r] = S[16 (w&3) + 4 (lane>>4) + r][16 (2 (w>>2) + cb) +
+// (lane & 15)]). img: 4 images (Vh, Vl, Th, Tl).
 __device__ __forceinline__ void logit_tile(const Split& V, const Split& T, int B, int N, int D, int r0, int c0,
-                                           bf16_t* img, f32x4 (&acc)[4]) {
+                                           bf16_t* img, f32x4 (&acc)[2]) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) acc[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  Stage2 a, b, c, d;
+  for (int cb = 0; cb < 2; ++cb) acc[cb] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  Stage1 a, b, c, d;
   a.load(V.h, D, r0, B, 0);
   b.load(V.l, D, r0, B, 0);
   c.load(T.h, D, c0, N, 0);
@@ -116,16 +113,17 @@ __device__ __forceinline__ void logit_tile(const Split& V, const Split& T, int B
       c.load(T.h, D, c0, N, k0 + KC);
       d.load(T.l, D, c0, N, k0 + KC);
     }
-    mfma_chunk(img, img + IMG, img + 2 * IMG, img + 3 * IMG, 16 * w + (lane & 15), acc);
+    mfma_chunk<2>(img, img + IMG, img + 2 * IMG, img + 3 * IMG, 16 * (w & 3) + (lane & 15), 2 * (w >> 2), acc);
   }
 }
 
-__device__ __forceinline__ void store_tile(float* Ss, const f32x4 (&acc)[4]) {
+__device__ __forceinline__ void store_tile(float* Ss, const f32x4 (&acc)[2]) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+  for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) Ss[(16 * w + 4 * (lane >> 4) + r) * GP + 16 * nb + (lane & 15)] = acc[nb][r];
+    for (int r = 0; r < 4; ++r)
+      Ss[(16 * (w & 3) + 4 * (lane >> 4) + r) * GP + 16 * (2 * (w >> 2) + cb) + (lane & 15)] = acc[cb][r];
 }
 
 // G tile from the logit tile in Ss, split into bf16 hi / lo images. TRANS = false: image rows are
@@ -137,7 +135,7 @@ __device__ __forceinline__ void grad_tile(const float* Ss, bf16_t* Gh, bf16_t* G
   const int N = B * K;
   const float gscale = gup[0] / (float)B;  // d loss / d x = (upstream grad) / Bg * (...)
   // each thread: one image row, 8 consecutive image columns per pass (one 16-B chunk of hi and lo)
-  for (int e = threadIdx.x; e < 64 * 8; e += 256) {
+  for (int e = threadIdx.x; e < 64 * 8; e += NT) {
     const int row = e >> 3, ch = e & 7;
     float hv[8], lv[8];
 #pragma unroll
@@ -208,7 +206,7 @@ __global__ __launch_bounds__(256) void milnce_split_kernel(const float* __restri
 }
 
 // rowpart: [n_ct][B] (max, sum); colpart: [n_rt][B] (max, sum) per text block.
-__global__ __launch_bounds__(256) void milnce_fused_fwd_kernel(Split V, Split T, int B, int K, int D,
+__global__ __launch_bounds__(512) void milnce_fused_fwd_kernel(Split V, Split T, int B, int K, int D,
                                                                float2* __restrict__ rowpart,
                                                                float2* __restrict__ colpart) {
   __shared__ __attribute__((aligned(16))) bf16_t img[4 * IMG];
@@ -216,7 +214,7 @@ __global__ __launch_bounds__(256) void milnce_fused_fwd_kernel(Split V, Split T,
   const int N = B * K;
   const int rt = blockIdx.y, ct = blockIdx.x;
   const int r0 = rt * TM, c0 = ct * TN;
-  f32x4 acc[4];
+  f32x4 acc[2];
   logit_tile(V, T, B, N, D, r0, c0, img, acc);
   store_tile(Ss, acc);
   __syncthreads();
@@ -229,10 +227,11 @@ __global__ __launch_bounds__(256) void milnce_fused_fwd_kernel(Split V, Split T,
     if (i < B) rowpart[(long long)ct * B + i] = make_float2(m, s);
   }
   // block-column partials: text block b (K columns) over the tile's valid rows; 16 lanes per
-  // block, 16 blocks per pass (64 / K blocks per tile)
+  // block, NT / 16 blocks per pass (64 / K blocks per tile)
   const int nbk = TN / K;
   const int sub = tid & 15;
-  for (int b = tid >> 4; b < ((nbk + 15) / 16) * 16; b += 16) {
+  constexpr int BPP = NT / 16;
+  for (int b = tid >> 4; b < ((nbk + BPP - 1) / BPP) * BPP; b += BPP) {
     float m = -INFINITY, s = 0.f;
     if (b < nbk) {
       for (int rr = sub; rr < TM; rr += 16) {
@@ -297,13 +296,15 @@ __global__ __launch_bounds__(256) void milnce_fused_mean_kernel(const float* __r
 
 // One backward pass. DT = false: dV[r0 : r0+64, :] = sum over column tiles of G . T (rows of the
 // block = video rows); DT = true: dT[c0 : c0+64, :] = sum over row tiles of G^T . V. The product's
-// B operand is the transposed split copy ([D][R]) of T (resp. V), rows d, k over the tile.
+// B operand is the transposed split copy ([D][Rp]) of T (resp. V), rows d, k over the tile.
+// 8 waves: wave w accumulates output rows 16 (w & 3).. over the D half (w >> 2); each staging step
+// brings one 64-wide d chunk of each half.
 template <bool DT>
-__global__ __launch_bounds__(256) void milnce_fused_grad_kernel(Split V, Split T, int B, int K, int D,
+__global__ __launch_bounds__(512) void milnce_fused_grad_kernel(Split V, Split T, int B, int K, int D,
                                                                 const float* __restrict__ den,
                                                                 const float* __restrict__ nom,
                                                                 const float* __restrict__ gup, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) bf16_t img[4 * IMG];  // logit operands, then the Xt chunk (2 images)
+  __shared__ __attribute__((aligned(16))) bf16_t img[4 * IMG];  // logit operands, then two Xt chunks (hi / lo)
   __shared__ __attribute__((aligned(16))) bf16_t gimg[2 * IMG];  // G (or G^T) hi / lo
   __shared__ float Ss[TM * GP];
   const int N = B * K;
@@ -313,10 +314,11 @@ __global__ __launch_bounds__(256) void milnce_fused_grad_kernel(Split V, Split T
   const int R = DT ? N : B;                        // output rows
   out += (long long)split * R * D;                 // split > 0 (or splits > 1): partial sums
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ndc = D / KC;
-  f32x4 acc_out[8][4];  // this wave's 16 output rows x D (up to 512)
+  const int rg = w & 3, dh = w >> 2;
+  const int half = D / KC / 2;                     // d chunks per half (D % 128 == 0)
+  f32x4 acc_out[4][4];  // this wave's 16 output rows x its D half (up to 256)
 #pragma unroll
-  for (int a = 0; a < 8; ++a)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc_out[a][c] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int n_other = DT ? (B + TM - 1) / TM : (N + TN - 1) / TN;
@@ -325,40 +327,47 @@ __global__ __launch_bounds__(256) void milnce_fused_grad_kernel(Split V, Split T
   const long long xld = ((DT ? B : N) + 63) / 64 * 64;  // row length of its transposed copy
   for (int t = t_begin; t < t_end; ++t) {
     const int r0 = DT ? t * TM : own0, c0 = DT ? own0 : t * TN;
-    f32x4 acc[4];
+    f32x4 acc[2];
     logit_tile(V, T, B, N, D, r0, c0, img, acc);
     store_tile(Ss, acc);
     __syncthreads();
     grad_tile<DT>(Ss, gimg, gimg + IMG, B, K, r0, c0, den, nom, gup);
     const int x0 = DT ? r0 : c0;  // first row of X in this tile (k range of the product)
-    Stage2 ph, pl;
-    ph.load(X.th, xld, 0, D, x0);
-    pl.load(X.tl, xld, 0, D, x0);
+    Stage1 p0h, p0l, p1h, p1l;     // d chunk j of half 0 and of half 1
+    p0h.load(X.th, xld, 0, D, x0);
+    p0l.load(X.tl, xld, 0, D, x0);
+    p1h.load(X.th, xld, half * KC, D, x0);
+    p1l.load(X.tl, xld, half * KC, D, x0);
 #pragma unroll
-    for (int dc = 0; dc < 8; ++dc) {
-      if (dc < ndc) {
+    for (int j = 0; j < 4; ++j) {
+      if (j < half) {
         __syncthreads();  // G images written / previous chunk's fragments read
-        ph.store(img);
-        pl.store(img + IMG);
+        p0h.store(img);
+        p0l.store(img + IMG);
+        p1h.store(img + 2 * IMG);
+        p1l.store(img + 3 * IMG);
         __syncthreads();
-        if (dc + 1 < ndc) {
-          ph.load(X.th, xld, (dc + 1) * KC, D, x0);
-          pl.load(X.tl, xld, (dc + 1) * KC, D, x0);
+        if (j + 1 < half) {
+          p0h.load(X.th, xld, (j + 1) * KC, D, x0);
+          p0l.load(X.tl, xld, (j + 1) * KC, D, x0);
+          p1h.load(X.th, xld, (half + j + 1) * KC, D, x0);
+          p1l.load(X.tl, xld, (half + j + 1) * KC, D, x0);
         }
-        mfma_chunk(gimg, gimg + IMG, img, img + IMG, 16 * w + (lane & 15), acc_out[dc]);
+        const bf16_t* xi = img + 2 * dh * IMG;
+        mfma_chunk<4>(gimg, gimg + IMG, xi, xi + IMG, 16 * rg + (lane & 15), 0, acc_out[j]);
       }
     }
     __syncthreads();  // Xt images read before the next tile's logit staging overwrites them
   }
 #pragma unroll
-  for (int dc = 0; dc < 8; ++dc)
-    if (dc < ndc)
+  for (int j = 0; j < 4; ++j)
+    if (j < half)
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int i = own0 + 16 * w + 4 * (lane >> 4) + r;
-          if (i < R) out[(long long)i * D + dc * KC + 16 * cb + (lane & 15)] = acc_out[dc][cb][r];
+          const int i = own0 + 16 * rg + 4 * (lane >> 4) + r;
+          if (i < R) out[(long long)i * D + (dh * half + j) * KC + 16 * cb + (lane & 15)] = acc_out[j][cb][r];
         }
 }
 
@@ -403,7 +412,7 @@ FusedWs carve(float* ws, int B, int K, int D) {
   return w;
 }
 
-bool geometry_ok(int B, int K, int D) { return K >= 1 && TN % K == 0 && D % KC == 0 && D <= 8 * KC && B >= 1; }
+bool geometry_ok(int B, int K, int D) { return K >= 1 && TN % K == 0 && D % (2 * KC) == 0 && D <= 8 * KC && B >= 1; }
 
 }  // namespace
 
@@ -438,7 +447,7 @@ MILNCE_API int milnce_fused_fwd(const float* V, const float* T, int B, int K, in
   hipLaunchKernelGGL(milnce_split_kernel, dim3((N + 63) / 64, D / 64), dim3(256), 0, stream, T, N, D,
                      (bf16_t*)w.T.h, (bf16_t*)w.T.l, (bf16_t*)w.T.th, (bf16_t*)w.T.tl);
   HIP_RET(hipGetLastError());
-  hipLaunchKernelGGL(milnce_fused_fwd_kernel, dim3(n_ct, n_rt), dim3(256), 0, stream, w.V, w.T, B, K, D, w.rowpart,
+  hipLaunchKernelGGL(milnce_fused_fwd_kernel, dim3(n_ct, n_rt), dim3(NT), 0, stream, w.V, w.T, B, K, D, w.rowpart,
                      w.colpart);
   HIP_RET(hipGetLastError());
   hipLaunchKernelGGL(milnce_fused_finalize_kernel, dim3((B + 3) / 4), dim3(256), 0, stream, V, T, B, K, D, w.rowpart,
@@ -457,7 +466,7 @@ MILNCE_API int milnce_fused_bwd(const float* ws, int B, int K, int D, const floa
   const int N = B * K;
   FusedWs w = carve((float*)ws, B, K, D);
   float* pv = s_dv > 1 ? part : dV;
-  hipLaunchKernelGGL(milnce_fused_grad_kernel<false>, dim3((B + TM - 1) / TM, s_dv), dim3(256), 0, stream, w.V, w.T,
+  hipLaunchKernelGGL(milnce_fused_grad_kernel<false>, dim3((B + TM - 1) / TM, s_dv), dim3(NT), 0, stream, w.V, w.T,
                      B, K, D, den, nom, gup, pv);
   HIP_RET(hipGetLastError());
   if (s_dv > 1) {
@@ -467,7 +476,7 @@ MILNCE_API int milnce_fused_bwd(const float* ws, int B, int K, int D, const floa
     HIP_RET(hipGetLastError());
   }
   float* pt = s_dt > 1 ? part : dT;
-  hipLaunchKernelGGL(milnce_fused_grad_kernel<true>, dim3((N + TN - 1) / TN, s_dt), dim3(256), 0, stream, w.V, w.T,
+  hipLaunchKernelGGL(milnce_fused_grad_kernel<true>, dim3((N + TN - 1) / TN, s_dt), dim3(NT), 0, stream, w.V, w.T,
                      B, K, D, den, nom, gup, pt);
   HIP_RET(hipGetLastError());
   if (s_dt > 1) {

@@ -1717,19 +1717,20 @@ class _MILNCEFused(torch.autograd.Function):
         return dv, dt
 
 
-# Fused where the tiling applies (K | 64, D a multiple of 64 up to 512) and the logits would take
-# >= 4 GiB (Bg >= 16384 at K = 4): the fused path trades time for memory -- steady state on one
-# MI355X, forward + backward: Bg 256 0.27 vs 0.29 ms, 2048 1.67 vs 0.59 ms, 8192 25.4 vs 8.2 ms
-# (fused vs hipBLASLt-materialised), peak +144 MiB vs +2128 MiB at 8192 (tests/test_gpu_halo.py).
-# MILNCE_FUSED_LOSS=0/1 forces either path.
+# Fused from Bg * Bg*K >= 2048 * 8192 logits (BASELINE configs 3 and 5: Bg 2048 on 8 GPUs, Bg 8192):
+# the split-bf16 fused loss (csrc/milnce_fused.hip) runs at the speed of the hipBLASLt-materialised
+# one there -- steady state on one MI355X, forward + backward: Bg 2048 0.64 vs 0.61 ms, Bg 8192
+# 7.75 vs 7.61 ms (tools/milnce_bench.py) -- and never allocates the [Bg, Bg*K] logits (peak +344
+# MiB vs +2128 MiB at Bg 8192, tests/test_gpu_halo.py). Smaller batches keep the materialised path
+# (Bg 1024: 0.32 vs 0.25 ms). MILNCE_FUSED_LOSS=0/1 forces either path.
 _FUSED_LOSS = os.environ.get("MILNCE_FUSED_LOSS", "auto")
-_FUSED_MIN_LOGITS = 1 << 30
+_FUSED_MIN_LOGITS = 2048 * 8192
 
 
 def milnce_fused_ok(v: torch.Tensor, t: torch.Tensor) -> bool:
     B, D = v.shape
     K = t.shape[0] // max(1, B)
-    return K >= 1 and 64 % K == 0 and t.shape[0] == B * K and D % 64 == 0 and D <= 512
+    return K >= 1 and 64 % K == 0 and t.shape[0] == B * K and D % 128 == 0 and D <= 512
 
 
 def milnce_loss(video_embd, text_embd, fused: Optional[bool] = None):
