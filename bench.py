@@ -48,7 +48,7 @@ def main():
     ap.add_argument("--loss", type=str, default="milnce",
                     help="milnce (configs 2/3) | cdtw | sdtw_cidm | sdtw_negative | sdtw_3 (config 4)")
     ap.add_argument("--seq_len", type=int, default=8, help="clips per sequence for the soft-DTW losses")
-    ap.add_argument("--grad_cache_chunks", type=int, default=0,
+    ap.add_argument("--grad_cache_chunks", type=int, default=-1,
                     help="GradCache micro-batches per GPU (config 5: 32f, 1024 clips/GPU)")
     opts = ap.parse_args()
 
@@ -167,7 +167,7 @@ def main():
                        "num_candidates": opts.num_candidates,
                        "parallelism": f"dp{observed}",
                        "backend": ctx.backend,
-                       "grad_cache_chunks": opts.grad_cache_chunks},
+                       "grad_cache_chunks": trainer.grad_cache_chunks()},
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
         }

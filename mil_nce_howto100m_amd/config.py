@@ -100,9 +100,11 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
                    help="end this run after this epoch (simulated interruption for resume tests)")
     g.add_argument("--hip_graph", type=int, default=1,
                    help="replay evaluation forwards from captured HIP graphs (launch-bound at small batch)")
-    g.add_argument("--grad_cache_chunks", type=int, default=0,
+    g.add_argument("--grad_cache_chunks", type=int, default=-1,
                    help="GradCache-style step in this many micro-batches per GPU: exact global-negative "
-                        "MIL-NCE with bounded activation memory (BASELINE config 5); 0/1: off")
+                        "MIL-NCE with bounded activation memory; 0/1: off (the reference's one-shot step); "
+                        "-1 (default): one-shot whenever the step's activations fit the GPU's memory "
+                        "(BASELINE config 5, 1024 x 32f clips, fits 288 GB one-shot), else the fewest chunks that fit")
     g.add_argument("--watchdog_s", type=float, default=0.0,
                    help="abort a rank (exit 3, stacks dumped) after this many seconds without a finished step")
     g.add_argument("--phase_timers", type=int, default=0,

@@ -118,7 +118,7 @@ class Trainer:
         if self.buffers is not None:
             with self.timer.phase("broadcast_buffers"):
                 self.buffers()
-        chunks = int(getattr(self.args, "grad_cache_chunks", 0) or 0)
+        chunks = self.grad_cache_chunks(video_batch=batch["video"])
         arena = self.ctx.device.type == "cuda" and ops.use_hip(self.bucketer.flat)
         if arena:
             from ..ops import hip_ops
@@ -140,6 +140,34 @@ class Trainer:
             self.scheduler.step()
         self.global_step += 1
         return loss.detach()
+
+    # Peak memory of the one-shot bf16 step per clip, measured on MI355X (profiles/r3_configs_4_5.md):
+    # 203.5 GiB at 1024 clips of 32 x 200^2 (BASELINE config 5), i.e. ~0.199 GiB per clip at 32 x 200^2;
+    # activations scale with frames x pixels. The auto mode keeps 10 % of the device in reserve.
+    GIB_PER_CLIP_32F200 = 203.5 / 1024
+
+    def grad_cache_chunks(self, video_batch: Optional[torch.Tensor] = None) -> int:
+        """Micro-batches of the step: --grad_cache_chunks if set (0/1: one-shot), else (-1) the
+        reference's one-shot step whenever its activations fit the device, else the fewest
+        GradCache chunks that do. Resolved once, on the first batch."""
+        req = int(getattr(self.args, "grad_cache_chunks", 0) or 0)
+        if req >= 0:
+            return req
+        if getattr(self, "_auto_chunks", None) is not None:
+            return self._auto_chunks
+        chunks = 0
+        if self.device.type == "cuda" and video_batch is not None:
+            v = video_batch
+            b = v.shape[0]
+            t, h, w = (v.shape[1], v.shape[2], v.shape[3]) if v.shape[-1] in (3, 4) and v.dim() == 5 else \
+                (v.shape[2], v.shape[3], v.shape[4])
+            est = self.GIB_PER_CLIP_32F200 * b * (t / 32.0) * (h * w / 200.0 ** 2) * 2 ** 30
+            free, total = torch.cuda.mem_get_info(self.device)
+            budget = 0.9 * total - (total - free)  # what this step may still allocate
+            if est > budget > 0:
+                chunks = int(min(b, -(-est // budget)))
+        self._auto_chunks = chunks if chunks > 1 else 0
+        return self._auto_chunks
 
     def _grad_cache_backward(self, batch: Dict[str, torch.Tensor], chunks: int) -> torch.Tensor:
         """GradCache two-pass step: the loss still sees every rank's

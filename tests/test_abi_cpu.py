@@ -15,7 +15,7 @@ def _c_decls():
     out = {}
     for path in glob.glob(os.path.join(ROOT, "csrc", "*.hip")):
         src = open(path).read()
-        for m in re.finditer(r"MILNCE_API\s+\w+\s+(\w+)\s*\(([^)]*)\)", src):
+        for m in re.finditer(r"MILNCE_API\s+(?:\w+\s+)+?(\w+)\s*\(([^)]*)\)", src):
             params = [p.strip() for p in m.group(2).replace("\n", " ").split(",") if p.strip()]
             out[m.group(1)] = params
     return out
