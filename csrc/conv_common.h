@@ -62,7 +62,8 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 
 // v4 forward / dgrad (conv_v4.hip): uniform-tap LDS-DMA ring with scalar stage offsets.
-// impl 8 / 9: 16x16x32 / 32x32x16 MFMA, 2-stage ring; 10 / 11: the same, 3 stages.
+// impl 8 / 9: 16x16x32 / 32x32x16 MFMA, 2-stage ring; 10 / 11: the same, 3 stages;
+// 12 / 13: 256-row tiles (8 waves), 2 stages.
 // Returns V4_UNSUPPORTED for shapes it does not cover (Cin % 64, K padding, tap count, N tile).
 constexpr int V4_UNSUPPORTED = -1;
 int launch_fwd_v4(ConvParams& p, int bn, int impl, hipStream_t stream);

@@ -54,16 +54,19 @@ __device__ __forceinline__ uint32_t tap_mask(int rt, int rh, int rw, const ConvP
   return m;
 }
 
-template <int BN, int STAGES, int EPI, int MF, int KS>
-__global__ __launch_bounds__(256, 1) void conv_fwd_v4_kernel(ConvParams p) {
-  constexpr int BK = V4_BK, BM = V4_BM;
-  constexpr int NT = 256, NWAVES = 4;
+// NWM waves along M (each wave a 64 x BN/2 tile, 2 along N): BM = 64 NWM rows, 128 NWM threads.
+// NWM = 4 (256-row tiles, 8 waves) halves the weight-tile re-reads per output row: at N = 192 the
+// weight stream (re-read per M tile) is the larger part of the ring's L2 traffic.
+template <int BN, int STAGES, int EPI, int MF, int KS, int NWM>
+__global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p) {
+  constexpr int BK = V4_BK, BM = 64 * NWM;
+  constexpr int NT = 128 * NWM, NWAVES = 2 * NWM;
   constexpr int CPR = BK / 8;                 // 16-B chunks per tile row
   constexpr int RPI = 64 / CPR;               // rows per DMA instruction (1 KiB)
   constexpr int A_INST = BM / RPI / NWAVES;   // 4
   constexpr int B_INST = BN / RPI / NWAVES;
   constexpr int NDMA = A_INST + B_INST;
-  constexpr int WM = BM / 2, WN = BN / 2;     // wave tile 64 x BN/2 (2 x 2 waves)
+  constexpr int WM = 64, WN = BN / 2;        // wave tile 64 x BN/2 (NWM x 2 waves)
   constexpr int TM = WM / MF, TN = WN / MF;
   constexpr int KSTEPS = BK / (MF == 16 ? 32 : 16);
   constexpr int LDE = BN + 8;
@@ -79,7 +82,7 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v4_kernel(ConvParams p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave >> 1, wc = wave & 1;  // wr in [0, NWM)
   const int nblocks = p.num_n_tiles * p.grid_m;
   const int logical = xcd_remap(blockIdx.x, nblocks);
   const int n_tile = logical % p.num_n_tiles;
@@ -372,46 +375,49 @@ __global__ __launch_bounds__(256, 1) void conv_fwd_v4_kernel(ConvParams p) {
   }
 }
 
-template <int BN, int STAGES, int EPI, int MF, int KS>
+template <int BN, int STAGES, int EPI, int MF, int KS, int NWM>
 static int launch_v4_t(ConvParams& p, hipStream_t stream) {
-  constexpr size_t ring = (size_t)STAGES * (V4_BM + BN) * V4_BK * 2;
-  constexpr size_t epi = (size_t)V4_BM * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
-  constexpr size_t red = (size_t)16 * 256 * 4;
+  constexpr int BM = 64 * NWM;
+  constexpr size_t ring = (size_t)STAGES * (BM + BN) * V4_BK * 2;
+  constexpr size_t epi = (size_t)BM * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
+  constexpr size_t red = (size_t)16 * 128 * NWM * 4;
   constexpr size_t lds = ring > epi ? (ring > red ? ring : red) : (epi > red ? epi : red);
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v4_kernel<BN, STAGES, EPI, MF, KS>,
+    HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v4_kernel<BN, STAGES, EPI, MF, KS, NWM>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr_set = true;
   }
   ConvParams q = p;
-  q.num_m_tiles = (p.M + V4_BM - 1) / V4_BM;
+  q.num_m_tiles = (p.M + BM - 1) / BM;
   const int nblocks = q.num_n_tiles * q.grid_m;
-  hipLaunchKernelGGL((conv_fwd_v4_kernel<BN, STAGES, EPI, MF, KS>), dim3(nblocks), dim3(256), lds, stream, q);
+  hipLaunchKernelGGL((conv_fwd_v4_kernel<BN, STAGES, EPI, MF, KS, NWM>), dim3(nblocks), dim3(128 * NWM), lds, stream,
+                     q);
   return (int)hipGetLastError();
 }
 
-template <int BN, int STAGES, int MF, int KS>
+template <int BN, int STAGES, int MF, int KS, int NWM>
 static int launch_v4_epi(ConvParams& p, hipStream_t stream) {
-  if (p.bn_mode == 0) return launch_v4_t<BN, STAGES, 0, MF, KS>(p, stream);
-  if (p.bn_mode == 1) return launch_v4_t<BN, STAGES, 1, MF, KS>(p, stream);
-  return launch_v4_t<BN, STAGES, 2, MF, KS>(p, stream);
+  if (p.bn_mode == 0) return launch_v4_t<BN, STAGES, 0, MF, KS, NWM>(p, stream);
+  if (p.bn_mode == 1) return launch_v4_t<BN, STAGES, 1, MF, KS, NWM>(p, stream);
+  return launch_v4_t<BN, STAGES, 2, MF, KS, NWM>(p, stream);
 }
 
-template <int BN, int STAGES, int MF>
+template <int BN, int STAGES, int MF, int NWM = 2>
 static int launch_v4_ks(ConvParams& p, hipStream_t stream) {
   const int ks = p.KT * 100 + p.KH * 10 + p.KW;
-  if (ks == 111) return launch_v4_epi<BN, STAGES, MF, 111>(p, stream);
-  if (ks == 133) return launch_v4_epi<BN, STAGES, MF, 133>(p, stream);
-  if (ks == 311) return launch_v4_epi<BN, STAGES, MF, 311>(p, stream);
-  return launch_v4_epi<BN, STAGES, MF, 0>(p, stream);
+  if (ks == 111) return launch_v4_epi<BN, STAGES, MF, 111, NWM>(p, stream);
+  if (ks == 133) return launch_v4_epi<BN, STAGES, MF, 133, NWM>(p, stream);
+  if (ks == 311) return launch_v4_epi<BN, STAGES, MF, 311, NWM>(p, stream);
+  return launch_v4_epi<BN, STAGES, MF, 0, NWM>(p, stream);
 }
 
 template <int BN>
 static int launch_v4_bn(ConvParams& p, int impl, hipStream_t stream) {
   constexpr bool mf32 = (BN / 2) % 32 == 0;
   constexpr bool three = 3 * (V4_BM + BN) * V4_BK * 2 <= 160 * 1024;
+  constexpr bool wide_m = BN % 64 == 0;  // 8 waves: B rows split into 1-KiB pieces of 8 waves
   if (impl == 8) return launch_v4_ks<BN, 2, 16>(p, stream);
   if constexpr (mf32) {
     if (impl == 9) return launch_v4_ks<BN, 2, 32>(p, stream);
@@ -422,17 +428,22 @@ static int launch_v4_bn(ConvParams& p, int impl, hipStream_t stream) {
       if (impl == 11) return launch_v4_ks<BN, 3, 32>(p, stream);
     }
   }
+  if constexpr (wide_m) {
+    if (impl == 12) return launch_v4_ks<BN, 2, 16, 4>(p, stream);
+    if (impl == 13) return launch_v4_ks<BN, 2, 32, 4>(p, stream);
+  }
   return V4_UNSUPPORTED;
 }
 
 bool fwd_v4_supported(const ConvParams& p, int bn, int impl) {
   const int taps = p.KT * p.KH * p.KW;
-  if (impl < 8 || impl > 11) return false;
+  if (impl < 8 || impl > 13) return false;
   if (p.Cin % V4_BK || p.Kpad != taps * p.Cin || taps > 32) return false;
   if (p.KT > 4 || p.KH > 8 || p.KW > 8) return false;  // tap_mask<0> loop bounds
   if (bn != 64 && bn != 96 && bn != 128 && bn != 160 && bn != 192) return false;
   if ((impl == 9 || impl == 11) && (bn / 2) % 32) return false;
-  if (impl >= 10 && 3 * (V4_BM + bn) * V4_BK * 2 > 160 * 1024) return false;
+  if ((impl == 10 || impl == 11) && 3 * (V4_BM + bn) * V4_BK * 2 > 160 * 1024) return false;
+  if (impl >= 12 && bn % 64) return false;
   return true;
 }
 

@@ -173,7 +173,8 @@ def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
     Grids with more partial-statistics rows than ``max_rows`` (the caller's buffer) are skipped."""
     wgs = tuple(w for w in dict.fromkeys((_FWD_WGS_PER_CU,) + _FWD_WGS_TUNE)
                 if w == _FWD_WGS_PER_CU or max_rows is None or _grid_for(M, npad, bn, w) <= max_rows)
-    code = {(i, w): 10 * i + w for i in plan_impls for w in wgs}
+    code = {(i, w): 10 * i + w for i in plan_impls if i not in _V4_WIDE_M for w in wgs}
+    code.update({(i, w): 10 * i + w for i in plan_impls if i in _V4_WIDE_M for w in (1, 2)})
     inv = {v: k for k, v in code.items()}
     best = _tune(lambda c: launch(inv[c][0], _grid_for(M, npad, bn, inv[c][1])), tuple(code.values()),
                  default=code.get((_DEFAULT_IMPL, _FWD_WGS_PER_CU)))
@@ -188,14 +189,19 @@ def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
 # 16x16x32 MFMA, 2 / 3 stages; 9 / 11: 32x32x16 MFMA (N tiles 64 / 128 / 192). MILNCE_V4=0
 # leaves them out of the tuner (A/B runs); MILNCE_V4_IMPLS restricts the set.
 _V4 = os.environ.get("MILNCE_V4", "1") != "0"
-_V4_IMPLS = tuple(int(v) for v in os.environ.get("MILNCE_V4_IMPLS", "8,9,10,11").split(","))
+_V4_IMPLS = tuple(int(v) for v in os.environ.get("MILNCE_V4_IMPLS", "8,9,10,11,12,13").split(","))
+# 12 / 13: 256-row tiles with 8 waves (one workgroup per CU at N 192 / 128): tuned on 1 or 2
+# workgroups per CU of persistent grid instead of 2 or 3
+_V4_WIDE_M = (12, 13)
 
 
 def _v4_ok(bn: int, cin: int, taps: int, kpad: int, impl: int) -> bool:
     """Mirror of csrc/conv_v4.hip fwd_v4_supported."""
     if cin % 64 or kpad != taps * cin or taps > 32 or bn not in (64, 96, 128, 160, 192):
         return False
-    if impl in (9, 11) and (bn // 2) % 32:
+    if impl in (9, 11, 13) and (bn // 2) % 32:
+        return False
+    if impl in _V4_WIDE_M and bn % 64:
         return False
     return True
 

@@ -125,9 +125,9 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
                                           (128, 96, (1, 1, 1), (0, 0, 0)), (192, 64, (1, 3, 3), (0, 1, 1)),
                                           (256, 320, (3, 1, 1), (1, 0, 0)), (64, 128, (3, 3, 3), (1, 1, 1))])
 def test_conv_v4_variants(cin, cout, k, p):
-    """csrc/conv_v4.hip (scalar-offset LDS-DMA ring): the 16x16x32 variants (8, 10) sum in v3's
+    """csrc/conv_v4.hip (scalar-offset LDS-DMA ring): the 16x16x32 variants (8, 10, 12) sum in v3's
     order, so forward, dgrad and the producer-BN dgrad partials are bitwise those of v3 (impl 4);
-    the 32x32x16 variants (9, 11) match the fp32 reference. Small planes (every row near the
+    the 32x32x16 variants (9, 11, 13) match the fp32 reference. 12 / 13 are the 256-row tiles. Small planes (every row near the
     padding) and a runtime-shape (3,3,3) kernel."""
     torch.manual_seed(13)
     h = hip()
@@ -144,8 +144,8 @@ def test_conv_v4_variants(cin, cout, k, p):
     xr = x.float().requires_grad_(True)
     F.conv3d(xr.permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).float(), None, 1, p).permute(0, 2, 3, 4, 1).backward(
         dy.float())
-    fw_impls = [i for i in (8, 9, 10, 11) if h._v4_ok(plan.bn, cin, plan.taps, plan.Kpad, i)]
-    dg_impls = [i for i in (8, 9, 10, 11) if h._v4_ok(plan.d_bn, cout, plan.taps, plan.d_Kpad, i)]
+    fw_impls = [i for i in (8, 9, 10, 11, 12, 13) if h._v4_ok(plan.bn, cin, plan.taps, plan.Kpad, i)]
+    dg_impls = [i for i in (8, 9, 10, 11, 12, 13) if h._v4_ok(plan.d_bn, cout, plan.taps, plan.d_Kpad, i)]
     assert 8 in fw_impls and (cout % 64 != 0 or 8 in dg_impls)
     outs = {}
     for impl in [4] + sorted(set(fw_impls) | set(dg_impls)):
@@ -161,9 +161,9 @@ def test_conv_v4_variants(cin, cout, k, p):
         assert rel_err(dx, xr.grad) < 1e-2, impl
     ref = outs[4]
     for impl, (y, st, dx, pst, fi, di) in outs.items():
-        if fi in (8, 10):
+        if fi in (8, 10, 12):
             assert torch.equal(y, ref[0]), ("y", impl)
-        if di in (8, 10):
+        if di in (8, 10, 12):
             assert torch.equal(dx, ref[2]), ("dx", impl)
             assert torch.allclose(pst, ref[3], rtol=1e-4, atol=1e-3), ("partials", impl)
         assert torch.allclose(st, ref[1], rtol=2e-3, atol=1e-1), ("stats", impl)

@@ -48,8 +48,13 @@ def main():
     fl = 2.0 * plan.M * plan.Cout * plan.Ktot
     print(f"{tuple(x.shape)} -> {o.cout} k{k}: fwd tile bn {plan.bn} bk {plan.bk}, dgrad tile bn {plan.d_bn} "
           f"bk {plan.d_bk}; {fl / 1e9:.0f} GFLOP", flush=True)
+    g0, dg0 = plan.grid_m, plan.d_grid_m
     for impl in o.impls:
         plan.impl = plan.d_impl = impl
+        # the 256-row variants hold one workgroup per CU: persistent grid of 1 per CU
+        wide = impl in h._V4_WIDE_M
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, 1) if wide else g0
+        plan.d_grid_m = h._grid_for(plan.B * plan.T * plan.H * plan.W, plan.d_Npad, plan.d_bn, 1) if wide else dg0
         try:
             tf = timeit(lambda: h.conv_forward_raw(x, wp, plan, stats))
             td = timeit(lambda: h.conv_dgrad(dy, wd, plan))
