@@ -201,6 +201,8 @@ def _v4_ok(bn: int, cin: int, taps: int, kpad: int, impl: int) -> bool:
         return False
     if impl in (9, 11, 13) and (bn // 2) % 32:
         return False
+    if impl in (10, 11) and 3 * (128 + bn) * 64 * 2 > 160 * 1024:  # three stages in LDS
+        return False
     if impl in _V4_WIDE_M and bn % 64:
         return False
     return True
