@@ -25,6 +25,13 @@ template <int MF> struct AccT { typedef f32x4 type; };
 template <> struct AccT<32> { typedef f32x16 type; };
 
 static constexpr int V4_BK = 64;
+
+// Diagnostic ablations (separate debug libraries only, tools/gpu/v4_ablate.sh; results are
+// garbage): bit 0 skips the activation LDS-DMA, bit 1 the weight LDS-DMA, bit 2 the epilogue's
+// global stores and statistics. Timing them bounds what the ring traffic / epilogue cost.
+#ifndef V4_ABLATE
+#define V4_ABLATE 0
+#endif
 static constexpr int V4_BM = 128;
 
 // per-row tap validity: bit t of the mask is set when tap t = (dt*KH + dh)*KW + dw of output row
@@ -171,12 +178,14 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
       const int woff = __builtin_amdgcn_readfirstlane(kt * BK * 2);
 #pragma unroll
       for (int i = 0; i < A_INST; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * BK), 16,
-                                                 oa[i], 0, 0, 0);
+        if (!(V4_ABLATE & 1))
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)(sa + (i * NWAVES * RPI + wave * RPI) * BK), 16,
+                                                   oa[i], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < B_INST; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16,
-                                                 ob[i], woff, 0, 0);
+        if (!(V4_ABLATE & 2))
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16,
+                                                   ob[i], woff, 0, 0);
       // advance the issue state by one 64-wide K stage
       if (++is_cb == cps) {
         is_cb = 0;
@@ -321,7 +330,7 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
       for (int row = tid / OCPR; row < BM; row += RPP) {
         const int m = m0 + row, n = n0 + cc * 8;
         const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
-        const bool ok = (m < p.M) & (n < p.Cout);
+        const bool ok = (m < p.M) & (n < p.Cout) & !(V4_ABLATE & 4);
         KASSERT(!ok || n + 8 <= p.ldy);
         if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
         if constexpr (EPI == 1) {

@@ -5,7 +5,8 @@ group, times the two collectives the step issues so the xGMI behaviour is on rec
 step time of every N > 1 run (the driver's 2/4/8-GPU scaling runs included):
 
 * the gradient all-reduce: one flat fp32 buffer the size of the model gradient, reduced whole
-  and in the bucketer's bucket slices (``parallel/ddp.py``, launched during backward), and
+  (also on a bf16 wire, ``--grad_comm_dtype bf16``) and in the bucketer's bucket slices
+  (``parallel/ddp.py``, launched during backward), and
 * the embedding all-gather of the MIL-NCE negatives (``parallel/dist.py::all_gather_embeddings``).
 
 Bus bandwidth follows the usual ring convention: all-reduce moves 2 (N-1)/N of the buffer per
@@ -57,6 +58,11 @@ def probe(grad_numel: int, buckets: Sequence[Sequence[int]], emb_rows: int, emb_
     out["grad_mib"] = round(nbytes / 2 ** 20, 2)
     out["allreduce_ms"] = round(ar * 1e3, 3)
     out["allreduce_busbw_gbps"] = round(nbytes * 2 * (world - 1) / world / ar / 1e9, 1)
+    # the same gradient on a bf16 wire (--grad_comm_dtype bf16): half the bytes per hop
+    flat16 = torch.ones(grad_numel, dtype=torch.bfloat16, device=device)
+    ar16 = _timed(lambda: dist.all_reduce(flat16), reps, cuda)
+    out["allreduce_bf16_ms"] = round(ar16 * 1e3, 3)
+    del flat16
     sizes: List[int] = [int(e) - int(s) for s, e in buckets]
     views = [flat[int(s):int(e)] for s, e in buckets]
 

@@ -13,6 +13,9 @@ sized design:
   8x MI355X (7 xGMI links, ~153 GB/s each) a ring step moves size/8 per link, so 8 MiB
   buckets are ~1 MiB per hop — large enough to be bandwidth- not latency-bound, small
   enough that the last bucket (the stem, issued after the final backward kernel) is short;
+* ``comm_dtype=torch.bfloat16`` (``--grad_comm_dtype bf16``) puts each bucket on the wire as
+  bf16 (half the xGMI bytes; the ring then sums in bf16, ~3 significant digits per hop) and
+  writes the reduced values back into the fp32 buffer; the default keeps fp32 on the wire;
 * the reduction is a SUM; the 1/world_size factor (reference semantics: DDP mean, with
   ``AllGather.backward`` returning only the local slice, ``utils.py:19-24``) or 1 (exact
   full-batch gradient) is folded into the optimizer kernel as ``grad_scale``;
@@ -41,10 +44,14 @@ class GradBucketer:
     reduced copy. Costs two extra gradient copies; for debugging only."""
 
     def __init__(self, params: Sequence[torch.nn.Parameter], world_size: int,
-                 bucket_bytes: int = 8 << 20, process_group=None, verify: Optional[bool] = None):
+                 bucket_bytes: int = 8 << 20, process_group=None, verify: Optional[bool] = None,
+                 comm_dtype: torch.dtype = torch.float32):
         self.verify = (os.environ.get("MILNCE_VERIFY_BUCKETS", "0") == "1") if verify is None else bool(verify)
         self._snap: Dict[int, torch.Tensor] = {}
         self._comm: Dict[int, torch.Tensor] = {}
+        if comm_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"gradient comm dtype must be fp32 or bf16, got {comm_dtype}")
+        self.comm_dtype = comm_dtype
         self.params = [p for p in params if p.requires_grad]
         self.world_size = world_size
         self.group = process_group
@@ -101,6 +108,9 @@ class GradBucketer:
         buf = self.flat[s:e]
         if self.verify:  # reduce a private copy; keep another to check the slice against later
             self._snap[b] = buf.clone()
+        if self.comm_dtype != torch.float32:  # narrow wire copy, written back in finish()
+            buf = self._comm[b] = buf.to(self.comm_dtype)
+        elif self.verify:
             buf = self._comm[b] = buf.clone()
         self._handles[b] = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
@@ -142,6 +152,10 @@ class GradBucketer:
                 self._launch(b)
         for h in self._handles:
             h.wait()
+        if self.comm_dtype != torch.float32 and not self.verify:
+            for b, (s, e) in enumerate(self.buckets):
+                self.flat[s:e].copy_(self._comm[b])
+            self._comm.clear()
         if self.verify:
             bad = []
             for b, (s, e) in enumerate(self.buckets):

@@ -70,7 +70,9 @@ class Trainer:
         else:
             raise ValueError(args.optimizer)
         self.bucketer = GradBucketer(params, ctx.world_size, int(getattr(args, "bucket_mb", 8.0) * (1 << 20)),
-                                     verify=bool(getattr(args, "verify_buckets", 0)) or None)
+                                     verify=bool(getattr(args, "verify_buckets", 0)) or None,
+                                     comm_dtype=(torch.bfloat16 if getattr(args, "grad_comm_dtype", "fp32") == "bf16"
+                                                 else torch.float32))
         self.optimizer.bind_flat_grad(self.bucketer.flat, self.bucketer.offsets)
         self.buffers = BufferBroadcaster(model, ctx.world_size) if getattr(args, "broadcast_buffers", 1) else None
         self.scheduler = cosine_schedule_with_warmup(self.optimizer, args.warmup_steps,

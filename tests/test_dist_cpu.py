@@ -301,3 +301,34 @@ def test_bucket_order_verifier(late_write):
         else:
             assert err is None
     assert torch.equal(res[0][1], res[1][1])  # the reduced gradient was installed on both ranks
+
+
+def _worker_bf16_wire(rank, world, port, outdir):
+    _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.ddp import GradBucketer
+    torch.manual_seed(0)
+    lin = torch.nn.Sequential(torch.nn.Linear(16, 16), torch.nn.Linear(16, 4))
+    res = []
+    for dt in (torch.float32, torch.bfloat16):
+        bk = GradBucketer(list(lin.parameters()), world, bucket_bytes=256, comm_dtype=dt)
+        bk.zero()
+        x = torch.linspace(-1, 1, 48).view(3, 16) * (1.0 + rank)
+        lin(x).pow(2).sum().backward()
+        bk.finish()
+        assert bk.flat.dtype == torch.float32 and len(bk.buckets) > 1
+        res.append(bk.flat.clone())
+    _put(outdir, rank, res)
+    dist.destroy_process_group()
+
+
+def test_bucket_bf16_wire():
+    """--grad_comm_dtype bf16: every bucket is reduced as bf16 and written back into the fp32
+    flat buffer; the sum matches the fp32 wire to bf16 accuracy on every rank."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker_bf16_wire, args=(world, _port(), d), nprocs=world, join=True)
+        res = _collect(d, world)
+    f32, b16 = res[0]
+    assert torch.equal(b16, res[1][1]) and torch.equal(f32, res[1][0])
+    assert not torch.equal(f32, b16)  # really went through bf16
+    assert ((f32 - b16).norm() / f32.norm()).item() < 1e-2

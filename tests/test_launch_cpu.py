@@ -54,6 +54,7 @@ def test_bench_self_launches_n_ranks():
     c = r["comm"]
     assert c["world_size"] == 2 and c["buckets"] >= 1 and c["grad_mib"] > 0
     assert c["allreduce_ms"] > 0 and c["bucketed_allreduce_ms"] > 0 and c["allgather_ms"] > 0
+    assert c["allreduce_bf16_ms"] > 0
     assert c["allgather_kib"] == 2 * 2 * (1 + 4) * 512 * 4 / 1024  # W * b(1+K) rows * 512 fp32
 
 
