@@ -2016,6 +2016,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.fCin = make_fastdiv(Cin);
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
+  if (impl == 14 || impl == 15) return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, nullptr, stream);  // conv_box.hip
   if (impl >= 8) return x_u8 ? V4_UNSUPPORTED : launch_fwd_v4(p, bn, impl, stream);  // conv_v4.hip
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
     // wide / odd N tiles: LDS-DMA ring variants only, BK 64

@@ -1,0 +1,568 @@
+// Box-tiled implicit-GEMM forward / dgrad for S3D-G's stride-1 same-padded (1,3,3) and (3,1,1)
+// convs on gfx950 (impl 14 in the autotuner, next to v3 / v4).
+//
+// Why: the v4 ring gathers a fresh [256 x 64] activation tile per (tap, channel block) stage, so
+// every input element is staged through LDS once per tap (9x for (1,3,3), 3x for (3,1,1)). The
+// v4 ablation (tools/gpu/v4_ablate.sh, profiles/r3_box_conv.md) measured that gather at ~1/3 of
+// the conv_2c kernel time and the LDS-staged epilogue at another ~1/5, against a bare
+// LDS-read + MFMA loop at 1.8 PF/s. Here:
+//
+//   * the activation operand of a tile is staged ONCE per 64-channel block as a "box": every
+//     input row any tap of the tile reads, in a padded layout where each tap is a constant row
+//     shift, register-staged (buffer loads -> ds_write_b128) into rows of 80 bf16 (160 B pitch:
+//     conflict-free ds_read_b128 fragments at ANY row shift, see below);
+//       (1,3,3): rows in the "extended" plane order e = q*(H+1)(W+1) + (h+1)(W+1) + (w+1) (q =
+//                clip-frame plane; the pad row / column is shared by neighbouring planes / rows),
+//                tap (dh,dw) of output m reads box row e(m) - e(m0) + dh*(W+1) + dw;
+//       (3,1,1): a tile is P = 256/T positions x all T frames of one clip (rows t*P + j), the box
+//                (T+2) x P rows, tap dt reads box row (t+dt)*P + j;
+//   * the weight stages [(channel block, tap)] stream through a 3-deep LDS-DMA ring (the v4 swizzle)
+//     that runs continuously across tiles: a tile's last iterations already fire the next tile's
+//     first stages, so their latency hides under the epilogue;
+//   * the next box (next channel block, or the next tile's first) is loaded into registers at the
+//     first tap of a block and written to LDS after its last tap; the exact per-wave vmcnt waits
+//     account for the box loads and the epilogue stores in flight (all counts compile-time);
+//   * the epilogue stores bf16 straight from the accumulators (8 B per lane per 4 channels,
+//     buffer stores: out-of-range rows go past num_records, so every wave issues the same count)
+//     and reduces the BN statistics / producer-BN partials through LDS atomics.
+//
+// LDS fragment reads: lane l of a 16x16x32 fragment reads row r0 + (l & 15) at chunk c0 + (l >> 4).
+// With a 160-B pitch (10 chunks) the 16 lanes of each ds_read_b128 bank group hit 4-bank slots
+// (10 r + c) mod 16 that are all distinct for any r0 (the rows of a group split into even / odd
+// slot sets), so shifted taps stay conflict-free (the w-wrap inside a fragment can cost one).
+#include "conv_common.h"
+
+#include <type_traits>
+
+static constexpr int BX_BM = 256;        // output rows per tile: 4 waves along M x 64 rows
+static constexpr int BX_BK = 64;         // channels per box / K stage
+// bf16 per box row: 16x16x32 fragments (lane rows l & 15, chunks c + (l >> 4)) are conflict-free
+// at a 10-chunk pitch, 32x32x16 fragments (rows l & 31, one chunk per half-wave) at 9 chunks
+template <int MF> struct BoxPitch { static constexpr int v = 80; };
+template <> struct BoxPitch<32> { static constexpr int v = 72; };
+static constexpr int BX_ROWS = 448;      // box capacity (rows)
+static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per thread: 7
+static constexpr int BX_STAGES = 3;
+
+struct BoxGeo {
+  int KS;          // 133 or 311
+  int W1, PL;      // 133: W + 1, (H + 1) * (W + 1)
+  int P, tpc;      // 311: positions per tile (256 / T), tiles per clip
+  int HW;
+  FastDiv fHW, fW, fPL, fW1, ftpc, fP;
+  const float* pro_ss;  // [4][Cin] of the input's BN (scale at 2*Cin, shift at 3*Cin) or null
+};
+
+// vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
+template <int N>
+__device__ __forceinline__ void bx_wait() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BN, int KS, int EPI, int PRO, int MF>
+__global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g) {
+  constexpr int BM = BX_BM, BK = BX_BK, PITCH = BoxPitch<MF>::v;
+  constexpr int NT = 512, NWAVES = 8;
+  constexpr int WM = 64, WN = BN / 2;
+  constexpr int TM = WM / MF, TN = WN / MF;
+  constexpr int KSTEPS = BK / (MF == 16 ? 32 : 16);
+  constexpr int TAPS = KS == 133 ? 9 : 3;
+  constexpr int CPR = BK / 8, RPI = 64 / CPR;  // B ring: 8 rows (1 KiB) per DMA instruction
+  constexpr int B_INST = BN / RPI / NWAVES;    // DMA pieces per wave per stage
+  constexpr int NDMA = B_INST;
+  constexpr int NBX = BX_NBX;
+  constexpr int NST = WN / 4;                  // epilogue stores (8 B, 4 channels) per wave per tile
+  static_assert(WN % MF == 0, "wave tile");
+  constexpr int STAGE_ELEMS = BN * BK;
+  static_assert(B_INST * RPI * NWAVES == BN, "DMA mapping");
+  static_assert(NST + NDMA + NBX <= 63, "vmcnt range");
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
+  bf16_t* ring = box + BX_ROWS * 80;                             // [STAGES][BN][BK]
+  float* st_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // [2][BN] statistics
+  float* ss_lds = st_lds + 2 * BN;                               // EPI 2: [4][BN]; PRO: [2][Cin]
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nblocks = p.num_n_tiles * p.grid_m;
+  const int logical = xcd_remap(blockIdx.x, nblocks);
+  const int n_tile = logical % p.num_n_tiles;
+  const int m_slot = logical / p.num_n_tiles;
+  const int n0 = n_tile * BN;
+  const int ncb = p.Cin / BK;
+  const int nst_tile = ncb * TAPS;  // stages per tile
+  const int Cin = p.Cin;
+
+  // ---- one-time LDS setup: statistics accumulators, BN constants ----
+  for (int t = tid; t < 2 * BN; t += NT) st_lds[t] = 0.f;
+  if constexpr (EPI == 2) {
+    for (int t = tid; t < 4 * BN; t += NT) {
+      const int q = t / BN, c = n0 + (t - q * BN);
+      ss_lds[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
+    }
+  }
+  if constexpr (PRO) {
+    for (int t = tid; t < 2 * Cin; t += NT) ss_lds[t] = g.pro_ss[2 * Cin + t];  // scale [Cin], shift [Cin]
+  }
+
+  // ---- weight ring (v4 layout: swizzled chunks, soffset = stage K offset) ----
+  const int slot = lane % CPR;
+  const int lrow = wave * RPI + lane / CPR;
+  const int src_chunk = swz<BK>(lrow, slot);
+  const auto wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0,
+                                                     (int)((long long)p.num_n_tiles * BN * p.Kpad * 2), 0x00020000);
+  // fixed array bounds: template-constant bounds captured by the lambdas make clang's host pass
+  // drop the kernel's launch stub (as in conv_v4.hip)
+  static_assert(B_INST <= 8 && TM <= 4, "offset arrays");
+  uint32_t ob[8];
+#pragma unroll
+  for (int i = 0; i < B_INST; ++i)
+    ob[i] = (uint32_t)(((long long)(n0 + i * NWAVES * RPI + lrow) * p.Kpad + src_chunk * 8) * 2);
+  // stage s of a tile = (cb, tap) = (s / TAPS, s % TAPS): weight columns tap * Cin + cb * 64
+  auto fire = [&](int gslot, int s_in_tile) {
+    const int cb = s_in_tile / TAPS, tap = s_in_tile - cb * TAPS;
+    bf16_t* sb = ring + gslot * STAGE_ELEMS;
+    const int woff = __builtin_amdgcn_readfirstlane((tap * Cin + cb * BK) * 2);
+#pragma unroll
+    for (int i = 0; i < B_INST; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, ob[i],
+                                               woff, 0, 0);
+  };
+
+  // ---- tile geometry ----
+  const int xch = tid & 7, xrow0 = tid >> 3;  // box staging: chunk, first row (rows xrow0 + 64 k)
+  struct TileInfo {
+    long long xbase;     // byte offset of the tile's input base
+    long long ybase;     // element offset of the tile's output base row
+    uint32_t xnrec;
+    int e0, elast, m0;   // 133: extended index of the first / last output row, first row
+    int b, p0;           // 311
+  };
+  auto tile_info = [&](int m_tile) {
+    TileInfo ti;
+    if constexpr (KS == 133) {
+      const int m0 = m_tile * BM;
+      const int ml = min(p.M, m0 + BM) - 1;
+      auto ext = [&](int m) {
+        const uint32_t q = fdiv((uint32_t)m, g.fHW);
+        const int r = m - (int)q * g.HW;
+        const uint32_t h = fdiv((uint32_t)r, g.fW);
+        const int w = r - (int)h * p.W;
+        return (int)q * g.PL + ((int)h + 1) * g.W1 + w + 1;
+      };
+      ti.m0 = m0;
+      ti.e0 = ext(m0);
+      ti.elast = ext(ml);
+      const int qlo = (int)fdiv((uint32_t)max(0, ti.e0 - g.W1 - 1), g.fPL);
+      ti.xbase = (long long)qlo * g.HW * Cin * 2;
+      ti.ybase = (long long)m0 * p.ldy;
+      ti.b = qlo;
+      ti.p0 = 0;
+    } else {
+      const uint32_t b = fdiv((uint32_t)m_tile, g.ftpc);
+      const int pb = m_tile - (int)b * g.tpc;
+      ti.b = (int)b;
+      ti.p0 = pb * g.P;
+      ti.xbase = (long long)b * p.T * g.HW * Cin * 2;
+      ti.ybase = (long long)b * p.T * g.HW * p.ldy;
+      ti.m0 = ti.e0 = ti.elast = 0;
+    }
+    const long long remain = p.x_total_bytes - ti.xbase;
+    ti.xnrec = remain > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)(remain > 0 ? remain : 0);
+    return ti;
+  };
+  // byte offset (relative to the tile's xbase, without the channel block) of box row j, or
+  // 0x80000000 (reads zero) for padding / out-of-range rows
+  auto box_off = [&](const TileInfo& ti, int j) -> uint32_t {
+    if constexpr (KS == 133) {
+      const int e = ti.e0 - g.W1 - 1 + j;
+      if (e < 0 || e > ti.elast + g.W1 + 1) return 0x80000000u;
+      const uint32_t q = fdiv((uint32_t)e, g.fPL);
+      const int r = e - (int)q * g.PL;
+      const uint32_t hh = fdiv((uint32_t)r, g.fW1);
+      const int ww = r - (int)hh * g.W1;
+      if (hh == 0 || ww == 0 || (int)q >= p.M / g.HW) return 0x80000000u;
+      const int qrel = (int)q - ti.b;
+      return (uint32_t)((((long long)qrel * p.H + (int)hh - 1) * p.W + ww - 1) * Cin * 2 + xch * 16);
+    } else {
+      const int tp = (int)fdiv((uint32_t)j, g.fP), jj = j - tp * g.P;
+      const int t_in = tp - 1, pos = ti.p0 + jj;
+      if (t_in < 0 || t_in >= p.T || pos >= g.HW || j >= (p.T + 2) * g.P) return 0x80000000u;
+      return (uint32_t)(((long long)t_in * g.HW + pos) * Cin * 2 + xch * 16);
+    }
+  };
+
+  // ---- box staging registers ----
+  uint4 xr[NBX];
+  uint32_t xo[NBX];
+  auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb) {
+    const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
+#pragma unroll
+    for (int k = 0; k < NBX; ++k)
+      xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, xo[k], coff, 0));
+  };
+  auto box_store = [&](int cb) {
+#pragma unroll
+    for (int k = 0; k < NBX; ++k) {
+      uint4 v = xr[k];
+      if constexpr (PRO) {
+        if (xo[k] != 0x80000000u) {
+          float f[8];
+          unpack8(v, f);
+          const int c0 = cb * BK + xch * 8;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) f[u] = fmaxf(f[u] * ss_lds[c0 + u] + ss_lds[Cin + c0 + u], 0.f);
+          v = pack8(f);
+        }
+      }
+      *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
+    }
+  };
+
+  // ---- per-lane fragment rows of a tile ----
+  auto frag_rows = [&](const TileInfo& ti, int (&rb)[4], uint32_t (&yo)[4]) {  // box row, output byte offset
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int lr = wr * WM + i * MF + (lane & (MF - 1));
+      if constexpr (KS == 133) {
+        const int m = ti.m0 + lr;
+        if (m < p.M) {
+          const uint32_t q = fdiv((uint32_t)m, g.fHW);
+          const int r = m - (int)q * g.HW;
+          const uint32_t h = fdiv((uint32_t)r, g.fW);
+          const int w = r - (int)h * p.W;
+          rb[i] = (int)q * g.PL + ((int)h + 1) * g.W1 + w + 1 - ti.e0;
+          yo[i] = (uint32_t)(lr * p.ldy * 2);
+        } else {
+          rb[i] = 0;
+          yo[i] = 0x80000000u;
+        }
+      } else {
+        const int t = (int)fdiv((uint32_t)lr, g.fP), j = lr - t * g.P;
+        rb[i] = lr;
+        yo[i] = (ti.p0 + j < g.HW) ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2) : 0x80000000u;
+      }
+    }
+  };
+
+  const int ntiles = p.num_m_tiles;
+  int m_tile = m_slot;
+  if (m_tile >= ntiles) {  // no tile for this slot: its statistics row is zero
+    if constexpr (EPI != 0) {
+      const int npad = p.num_n_tiles * BN;
+      for (int t = tid; t < BN; t += NT) {
+        p.stats[(long long)m_slot * 2 * npad + n0 + t] = 0.f;
+        p.stats[(long long)m_slot * 2 * npad + npad + n0 + t] = 0.f;
+      }
+    }
+    return;
+  }
+
+  __syncthreads();  // setup writes visible
+
+  // ---- prologue: first tile's box (cb 0), synchronously; first two weight stages ----
+  TileInfo ti = tile_info(m_tile);
+  auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + ti.xbase), (short)0, (int)ti.xnrec,
+                                               0x00020000);
+#pragma unroll
+  for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + 64 * k);
+  box_load(xrs, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  box_store(0);
+  int gs = 0;  // global stage counter (ring slot = gs % 3)
+  fire(0, 0);
+  fire(1, 1 % nst_tile);
+  bool first_tile = true;
+
+  typedef typename std::conditional<MF == 16, f32x4, f32x16>::type acc_t;
+  while (true) {
+    int rb[4];
+    {
+      uint32_t yo_unused[4];
+      frag_rows(ti, rb, yo_unused);
+    }
+    const int next_tile = m_tile + p.grid_m;
+    const bool has_next = next_tile < ntiles;
+    TileInfo tn = has_next ? tile_info(next_tile) : ti;
+    acc_t acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = acc_t{};
+
+    for (int cb = 0; cb < ncb; ++cb) {
+      const bool last_cb = cb == ncb - 1;
+#pragma unroll
+      for (int t = 0; t < TAPS; ++t) {
+        const int s = cb * TAPS + t;  // stage within the tile
+        // wait for stage s: count the wave's younger vector-memory ops (exact, in issue order)
+        //   * stage s+1 (fired one iteration ago) unless s is the tile's last stage [never: the
+        //     next tile's first stage is fired there too, see below] -> NDMA
+        //   * box loads issued at tap 0 of this block after firing stage cb*TAPS+2: younger
+        //     than stages up to cb*TAPS+2 -> waits at taps 1, 2
+        //   * epilogue stores of the previous tile: younger than the first two stages of this tile
+        if (cb == 0 && !first_tile) {
+          if (t == 0) bx_wait<NDMA + NST>();
+          else if (t == 1) bx_wait<NST + NDMA + NBX>();
+          else if (t == 2) bx_wait<NBX + NDMA>();
+          else bx_wait<NDMA>();
+        } else {
+          if (t == 1 || t == 2) bx_wait<NDMA + NBX>();
+          else bx_wait<NDMA>();
+        }
+        ring_barrier();
+        // fire stage s + 2 (continuing into the next tile: the weights do not depend on the tile)
+        {
+          int s2 = s + 2;
+          if (s2 >= nst_tile) s2 -= nst_tile;
+          if (s2 >= nst_tile) s2 = 0;  // nst_tile == 1 (not used by the supported shapes)
+          fire((gs + 2) % BX_STAGES, s2);
+        }
+        if (t == 0) {
+          // prefetch the next box: next channel block of this tile, or the next tile's block 0
+          if (!last_cb) {
+            box_load(xrs, cb + 1);
+          } else {
+            auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + tn.xbase), (short)0,
+                                                         (int)(has_next ? tn.xnrec : 0u), 0x00020000);
+#pragma unroll
+            for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
+            box_load(nrs, 0);
+            xrs = nrs;
+          }
+        }
+        // ---- MFMAs of stage s: A = weights (ring), B = box rows shifted by the tap ----
+        const bf16_t* bsh = ring + (gs % BX_STAGES) * STAGE_ELEMS;
+        int shift;
+        if constexpr (KS == 133) shift = (t / 3) * g.W1 + (t % 3);
+        else shift = t * g.P;
+        const int sh = __builtin_amdgcn_readfirstlane(shift * PITCH);
+        auto xfrag = [&](int ks, int i) {
+          const int ch = MF == 16 ? ks * 4 + (lane >> 4) : ks * 2 + (lane >> 5);
+          return *(const bf16x8*)(box + rb[i] * PITCH + sh + ch * 8);
+        };
+        auto wfrag = [&](int ks, int j) {
+          const int row = wc * WN + j * MF + (lane & (MF - 1));
+          const int ch = MF == 16 ? ks * 4 + (lane >> 4) : ks * 2 + (lane >> 5);
+          return *(const bf16x8*)(bsh + row * BK + swz<BK>(row, ch) * 8);
+        };
+#pragma unroll
+        for (int ks = 0; ks < KSTEPS; ++ks) {
+          bf16x8 xf[TM], wf[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) xf[i] = xfrag(ks, i);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) wf[j] = wfrag(ks, j);
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+              if constexpr (MF == 16)
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+              else
+                acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        ++gs;
+      }
+      // every wave is done with this box: write the prefetched one (the next iteration's ring
+      // barrier publishes it)
+      lds_barrier();
+      if (!last_cb) box_store(cb + 1);
+      else if (has_next) box_store(0);
+    }
+
+    // ---- epilogue: bf16 straight from the accumulators (lane: 4 channels of one row) ----
+    {
+      int rb_unused[4];
+      uint32_t yo[4];
+      frag_rows(ti, rb_unused, yo);
+      const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
+      constexpr int NG = MF == 16 ? 1 : 4;  // runs of 4 channels per lane per fragment
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+#pragma unroll
+        for (int gq = 0; gq < NG; ++gq) {
+          // tile-local channel of this lane's 4-run: 16x16: 4 (l >> 4); 32x32: 8 gq + 4 (l >> 5)
+          const int nl = wc * WN + j * MF + (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4);
+          const int n = n0 + nl;
+          float es[4] = {0.f, 0.f, 0.f, 0.f}, eq[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc[j][i][gq * 4 + r];
+            uint2 o;
+            o.x = pack2bf(v[0], v[1]);
+            o.y = pack2bf(v[2], v[3]);
+            const bool ok = (yo[i] != 0x80000000u) & (n < p.Cout);
+            const uint32_t off = ok ? yo[i] + (uint32_t)n * 2 : 0x80000000u;
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, o), yrs, off, 0, 0);
+            if constexpr (EPI == 1) {
+              if (ok) {
+                const float d[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                                    __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) { es[r] += d[r]; eq[r] += d[r] * d[r]; }
+              }
+            }
+            if constexpr (EPI == 2) {
+              if (ok) {
+                // producer BN-backward partials from the bf16 dz actually stored
+                const long long row = (ti.ybase + yo[i] / 2) / p.ldy;
+                const uint2 yv = *(const uint2*)(p.bn_y + row * p.bn_ld + n);
+                const float d[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
+                                    __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
+                const float yy[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
+                                     __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int cl = nl + r;
+                  const float gm = (yy[r] * ss_lds[2 * BN + cl] + ss_lds[3 * BN + cl] > 0.f) ? d[r] : 0.f;
+                  es[r] += gm;
+                  eq[r] += gm * (yy[r] - ss_lds[cl]) * ss_lds[BN + cl];
+                }
+              }
+            }
+          }
+          if constexpr (EPI != 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float s = es[r], q = eq[r];
+#pragma unroll
+              for (int o = 1; o < MF; o <<= 1) {  // lanes holding the same channels (same l / MF)
+                s += __shfl_xor(s, o, 64);
+                q += __shfl_xor(q, o, 64);
+              }
+              if ((lane & (MF - 1)) == 0) {
+                atomicAdd(st_lds + nl + r, s);
+                atomicAdd(st_lds + BN + nl + r, q);
+              }
+            }
+          }
+        }
+      }
+    }
+
+    if (!has_next) break;
+    m_tile = next_tile;
+    ti = tn;
+    first_tile = false;
+  }
+  // drain: the trailing fires of the last tile and the epilogue stores
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (EPI != 0) {
+    __syncthreads();
+    const int npad = p.num_n_tiles * BN;
+    for (int t = tid; t < BN; t += NT) {
+      p.stats[(long long)m_slot * 2 * npad + n0 + t] = st_lds[t];
+      p.stats[(long long)m_slot * 2 * npad + npad + n0 + t] = st_lds[BN + t];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
+  const int ks = p.KT * 100 + p.KH * 10 + p.KW;
+  if (p.st != 1 || p.sh != 1 || p.sw != 1) return V4_UNSUPPORTED;
+  if (p.To != p.T || p.Ho != p.H || p.Wo != p.W) return V4_UNSUPPORTED;
+  if (p.Cin % BX_BK || p.Kpad != p.KT * p.KH * p.KW * p.Cin) return V4_UNSUPPORTED;
+  g.KS = ks;
+  g.HW = p.H * p.W;
+  g.fHW = make_fastdiv(g.HW);
+  g.fW = make_fastdiv(p.W);
+  if (ks == 133) {
+    if (p.pt != 0 || p.ph != 1 || p.pw != 1) return V4_UNSUPPORTED;
+    g.W1 = p.W + 1;
+    g.PL = (p.H + 1) * g.W1;
+    g.fPL = make_fastdiv(g.PL);
+    g.fW1 = make_fastdiv(g.W1);
+    g.P = g.tpc = 1;
+    g.ftpc = g.fP = make_fastdiv(1);
+    // box rows of the widest tile: extended span of 256 output rows + one pad row and column on
+    // each side (bounded by the worst alignment: a tile starting at a plane's last column)
+    // e(m + 255) - e(m) = 255 + (row wraps) + (W + 2) (plane wraps): a row wrap skips the shared
+    // pad column, a plane wrap also the shared pad row
+    const long long span = 255 + (255 / p.W + 1) + (255 / g.HW + 1) * (long long)(p.W + 2) + 2 * g.W1 + 3;
+    if (span > BX_ROWS) return V4_UNSUPPORTED;
+    ntiles = (p.M + BX_BM - 1) / BX_BM;
+  } else if (ks == 311) {
+    if (p.pt != 1 || p.ph != 0 || p.pw != 0) return V4_UNSUPPORTED;
+    if (p.T < 1 || BX_BM % p.T) return V4_UNSUPPORTED;
+    g.P = BX_BM / p.T;
+    g.fP = make_fastdiv(g.P);
+    if ((p.T + 2) * g.P > BX_ROWS) return V4_UNSUPPORTED;
+    g.tpc = (g.HW + g.P - 1) / g.P;
+    g.ftpc = make_fastdiv(g.tpc);
+    g.W1 = g.PL = 1;
+    g.fPL = g.fW1 = make_fastdiv(1);
+    ntiles = (p.M / (p.T * g.HW)) * g.tpc;
+  } else {
+    return V4_UNSUPPORTED;
+  }
+  return 0;
+}
+
+bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
+  BoxGeo g;
+  int nt;
+  if (!((impl == 14 && (bn == 64 || bn == 128)) || (impl == 15 && (bn == 64 || bn == 128 || bn == 192)))) return false;
+  return box_geo(p, g, nt) == 0;
+}
+
+template <int BN, int KS, int EPI, int PRO, int MF>
+static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
+  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * BN * BX_BK * 2 + 2 * BN * 4 +
+                     (EPI == 2 ? 16 * BN : 0) + (PRO ? 8 * (size_t)p.Cin : 0);
+  if (lds > 160 * 1024) return V4_UNSUPPORTED;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HIP_RET(hipFuncSetAttribute((const void*)conv_box_kernel<BN, KS, EPI, PRO, MF>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = true;
+  }
+  const int nblocks = p.num_n_tiles * p.grid_m;
+  hipLaunchKernelGGL((conv_box_kernel<BN, KS, EPI, PRO, MF>), dim3(nblocks), dim3(512), lds, stream, p, g);
+  return (int)hipGetLastError();
+}
+
+template <int BN, int KS, int MF>
+static int launch_box_epi(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
+  if (g.pro_ss != nullptr) {
+    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 1, MF>(p, g, stream);
+    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 1, MF>(p, g, stream);
+    return V4_UNSUPPORTED;
+  }
+  if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 0, MF>(p, g, stream);
+  if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 0, MF>(p, g, stream);
+  return launch_box_t<BN, KS, 2, 0, MF>(p, g, stream);
+}
+
+template <int BN, int MF>
+static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
+  if (g.KS == 133) return launch_box_epi<BN, 133, MF>(p, g, stream);
+  return launch_box_epi<BN, 311, MF>(p, g, stream);
+}
+
+// impl 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (N tiles 64 / 128 / 192)
+int launch_fwd_box(ConvParams& p, int bn, int impl, const float* pro_ss, hipStream_t stream) {
+  BoxGeo g;
+  int ntiles = 0;
+  if (box_geo(p, g, ntiles) != 0) return V4_UNSUPPORTED;
+  g.pro_ss = pro_ss;
+  p.num_m_tiles = ntiles;
+  if (impl == 14) {
+    if (bn == 64) return launch_box_bn<64, 16>(p, g, stream);
+    if (bn == 128) return launch_box_bn<128, 16>(p, g, stream);
+  } else if (impl == 15) {
+    if (bn == 64) return launch_box_bn<64, 32>(p, g, stream);
+    if (bn == 128) return launch_box_bn<128, 32>(p, g, stream);
+    if (bn == 192) return launch_box_bn<192, 32>(p, g, stream);
+  }
+  return V4_UNSUPPORTED;
+}

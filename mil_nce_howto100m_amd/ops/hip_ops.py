@@ -192,7 +192,30 @@ _V4 = os.environ.get("MILNCE_V4", "1") != "0"
 _V4_IMPLS = tuple(int(v) for v in os.environ.get("MILNCE_V4_IMPLS", "8,9,10,11,12,13").split(","))
 # 12 / 13: 256-row tiles with 8 waves (one workgroup per CU at N 192 / 128): tuned on 1 or 2
 # workgroups per CU of persistent grid instead of 2 or 3
-_V4_WIDE_M = (12, 13)
+_V4_WIDE_M = (12, 13, 14, 15)  # 8-wave workgroups, one per CU (12 / 13 v4, 14 / 15 box-tiled)
+
+# Box-tiled forward / dgrad (csrc/conv_box.hip): stride-1 same-padded (1,3,3) / (3,1,1) convs over a
+# multiple of 64 channels; the tile's input box is staged once per 64-channel block for every tap.
+# 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (64 / 128 / 192). MILNCE_BOX=0 leaves them out.
+_BOX = os.environ.get("MILNCE_BOX", "1") != "0"
+_BOX_ROWS = 448
+
+
+def _box_ok(bn: int, cin: int, kpad: int, impl: int, geo) -> bool:
+    """Mirror of csrc/conv_box.hip fwd_box_supported; geo = (T, H, W, k, padding)."""
+    if geo is None or impl not in (14, 15):
+        return False
+    if not ((impl == 14 and bn in (64, 128)) or (impl == 15 and bn in (64, 128, 192))):
+        return False
+    T, H, W, k, pad = geo
+    if cin % 64 or kpad != k[0] * k[1] * k[2] * cin:
+        return False
+    if tuple(k) == (1, 3, 3) and tuple(pad) == (0, 1, 1):
+        span = 255 + (255 // W + 1) + (255 // (H * W) + 1) * (W + 2) + 2 * (W + 1) + 3
+        return span <= _BOX_ROWS
+    if tuple(k) == (3, 1, 1) and tuple(pad) == (1, 0, 0):
+        return 256 % T == 0 and (T + 2) * (256 // T) <= _BOX_ROWS
+    return False
 
 
 def _v4_ok(bn: int, cin: int, taps: int, kpad: int, impl: int) -> bool:
@@ -208,13 +231,23 @@ def _v4_ok(bn: int, cin: int, taps: int, kpad: int, impl: int) -> bool:
     return True
 
 
-def _fwd_impls(bn: int, kpad: int, cin: int = 0, taps: int = 0) -> Tuple[int, ...]:
+def _fwd_impls(bn: int, kpad: int, cin: int = 0, taps: int = 0, geo=None) -> Tuple[int, ...]:
     """Forward / dgrad variants the tuner tries for an N tile (csrc/conv.hip launch_v3_impl,
-    csrc/conv_v4.hip); ``cin`` = channels of the gathered operand (0: v3 variants only)."""
+    csrc/conv_v4.hip, csrc/conv_box.hip); ``cin`` = channels of the gathered operand (0: v3
+    variants only); ``geo`` = (T, H, W, k, padding) of a stride-1 conv (box-tiled candidates)."""
     base = _WIDE_IMPLS.get(bn, _IMPLS)
     if _V4 and cin:
         base = base + tuple(i for i in _V4_IMPLS if _v4_ok(bn, cin, taps, kpad, i))
+    if _BOX and cin:
+        base = base + tuple(i for i in (14, 15) if _box_ok(bn, cin, kpad, i, geo))
     return base
+
+
+def _box_geo(plan: "ConvPlan"):
+    """(T, H, W, k, padding) for the box-tiled kernel, or None (strided / resized output)."""
+    if plan.s != (1, 1, 1) or plan.wo_override or (plan.To, plan.Ho, plan.Wo) != (plan.T, plan.H, plan.W):
+        return None
+    return (plan.T, plan.H, plan.W, plan.k, plan.p)
 
 
 def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
@@ -440,7 +473,8 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
         if x.dtype == torch.uint8:
             plan.impl = 2
         else:
-            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps),
+            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
+                                                                  _box_geo(plan)),
                                                plan.M, plan.Npad, plan.bn, rows)
     if rows is not None and rows < plan.grid_m:
         raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
@@ -470,7 +504,8 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
 
     if plan.d_impl == 0:
-        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps),
+        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
+                                                                  _box_geo(plan)),
                                                md, plan.d_Npad, plan.d_bn)
     launch(plan.d_impl, plan.d_grid_m)
     if part is not None:

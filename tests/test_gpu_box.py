@@ -1,0 +1,84 @@
+"""Box-tiled forward / dgrad (csrc/conv_box.hip, impls 14 / 15) against the fp32 reference.
+
+The box kernels sum the taps in (channel block, tap) order instead of v3/v4's (tap, channel
+block), so they are compared with the fp32 conv (bf16-rounded operands) and with v3's BN
+statistics / producer-BN partials, not bitwise. Shapes cover the layouts' edge cases: tiles that
+cross many (clip, frame) planes (small and odd planes), the conv_2c plane (50 x 50), every
+supported T for the temporal box (P = 256 / T positions per tile), N tiles 64 / 128 / 192, and a
+channel count over several 64-wide blocks (box reloads mid-tile).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+CASES = [
+    # B, T, H, W, Cin, Cout, k, p
+    (3, 8, 11, 13, 64, 192, (1, 3, 3), (0, 1, 1)),
+    (2, 8, 50, 50, 64, 192, (1, 3, 3), (0, 1, 1)),
+    (2, 4, 7, 7, 128, 128, (1, 3, 3), (0, 1, 1)),
+    (2, 2, 25, 25, 192, 64, (1, 3, 3), (0, 1, 1)),
+    (3, 8, 9, 9, 192, 192, (3, 1, 1), (1, 0, 0)),
+    (2, 4, 13, 13, 128, 64, (3, 1, 1), (1, 0, 0)),
+    (2, 16, 5, 5, 64, 128, (3, 1, 1), (1, 0, 0)),
+    (2, 8, 25, 25, 256, 192, (3, 1, 1), (1, 0, 0)),
+]
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_conv_box_matches_reference(case):
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(21)
+    B, T, H, W, cin, cout, k, p = case
+    x = torch.randn(B, T, H, W, cin, device=DEV).to(torch.bfloat16)
+    w = torch.randn(cout, cin, *k, device=DEV) * (2.0 / (cin * k[0] * k[1] * k[2])) ** 0.5
+    plan = h.conv_plan(x.shape, w.shape, (1, 1, 1), p)
+    wp, wd = h._pack(w, plan, 0), h._pack(w, plan, 1)
+    dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, cout, device=DEV).to(torch.bfloat16)
+    stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device=DEV)
+    ss = torch.cat([torch.randn(cin, device=DEV) * 0.1, torch.rand(cin, device=DEV) + 0.5,
+                    torch.randn(cin, device=DEV), torch.randn(cin, device=DEV) * 0.2])
+    xr = x.float().requires_grad_(True)
+    yr = F.conv3d(xr.permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).float(), None, 1, p).permute(0, 2, 3, 4, 1)
+    yr.backward(dy.float())
+    geo = h._box_geo(plan)
+    fw = [i for i in (14, 15) if h._box_ok(plan.bn, cin, plan.Kpad, i, geo)]
+    dg = [i for i in (14, 15) if h._box_ok(plan.d_bn, cout, plan.d_Kpad, i, geo)]
+    assert fw, (plan.bn, geo)
+
+    def run(fi, di, grid_wgs):
+        plan.impl, plan.d_impl = fi, di
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, grid_wgs)
+        plan.d_grid_m = h._grid_for(plan.M, plan.d_Npad, plan.d_bn, grid_wgs)
+        y = h.conv_forward_raw(x, wp, plan, stats)
+        st = stats[:plan.grid_m * 2 * plan.Npad].view(plan.grid_m, 2, plan.Npad).double().sum(0)
+        dx = h.conv_dgrad(dy, wd, plan, (x, ss, cin))
+        part, nparts, ps = h.take_bn_partials(dx)
+        pst = part[:nparts * 2 * ps].view(nparts, 2, ps).double().sum(0)
+        return y, st, dx, pst
+
+    ref = run(4, 4, 2)
+    try:
+        for impl in sorted(set(fw) | set(dg)):
+            for wgs in (1, 2):
+                fi = impl if impl in fw else 4
+                di = impl if impl in dg else 4
+                y, st, dx, pst = run(fi, di, wgs)
+                assert _rel(y, yr) < 1e-2, (impl, wgs)
+                assert torch.allclose(st, ref[1], rtol=2e-3, atol=1e-1), ("stats", impl, wgs)
+                assert _rel(dx, xr.grad) < 1e-2, (impl, wgs)
+                assert torch.allclose(pst, ref[3], rtol=2e-2, atol=1.0), ("partials", impl, wgs)
+                # deterministic outputs (the statistics go through LDS atomics: not bitwise)
+                y2, _, dx2, _ = run(fi, di, wgs)
+                assert torch.equal(y, y2) and torch.equal(dx, dx2), (impl, wgs)
+    finally:
+        plan.impl = plan.d_impl = 0
