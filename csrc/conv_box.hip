@@ -22,9 +22,10 @@
 //   * the next box (next channel block, or the next tile's first) is loaded into registers at the
 //     first tap of a block and written to LDS after its last tap; the exact per-wave vmcnt waits
 //     account for the box loads and the epilogue stores in flight (all counts compile-time);
-//   * the epilogue stores bf16 straight from the accumulators (8 B per lane per 4 channels,
-//     buffer stores: out-of-range rows go past num_records, so every wave issues the same count)
-//     and reduces the BN statistics / producer-BN partials through LDS atomics.
+//   * the epilogue stages the tile's bf16 rows in the box region (two 128-row halves); every thread
+//     then owns an 8-channel column chunk: 16-B row stores (buffer stores: out-of-range rows go
+//     past num_records, so every wave issues the same count) and BN statistics / producer-BN
+//     partials accumulated in registers across the thread's tiles (as in v4), reduced once.
 //
 // LDS fragment reads: lane l of a 16x16x32 fragment reads row r0 + (l & 15) at chunk c0 + (l >> 4).
 // With a 160-B pitch (10 chunks) the 16 lanes of each ds_read_b128 bank group hit 4-bank slots
@@ -72,7 +73,13 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int B_INST = BN / RPI / NWAVES;    // DMA pieces per wave per stage
   constexpr int NDMA = B_INST;
   constexpr int NBX = BX_NBX;
-  constexpr int NST = WN / 4;                  // epilogue stores (8 B, 4 channels) per wave per tile
+  // epilogue: column-owner pass over 128-row halves staged in the box region
+  constexpr int LDE = BN + 8;                  // staged row (elements)
+  constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
+  constexpr int RPP = NT / OCPR;               // rows per pass
+  constexpr int EPI_IT = (128 + RPP - 1) / RPP;
+  constexpr int NST = 2 * EPI_IT;              // epilogue stores (16 B) per wave per tile
+  static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BN * BK;
   static_assert(B_INST * RPI * NWAVES == BN, "DMA mapping");
@@ -81,8 +88,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
   bf16_t* ring = box + BX_ROWS * 80;                             // [STAGES][BN][BK]
-  float* st_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // [2][BN] statistics
-  float* ss_lds = st_lds + 2 * BN;                               // EPI 2: [4][BN]; PRO: [2][Cin]
+  float* ss_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // EPI 2: [4][BN]; PRO: [2][Cin]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -97,7 +103,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   const int Cin = p.Cin;
 
   // ---- one-time LDS setup: statistics accumulators, BN constants ----
-  for (int t = tid; t < 2 * BN; t += NT) st_lds[t] = 0.f;
+  float e_s[8], e_q[8];  // epilogue statistics of this thread's column chunk, over all its tiles
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
   if constexpr (EPI == 2) {
     for (int t = tid; t < 4 * BN; t += NT) {
       const int q = t / BN, c = n0 + (t - q * BN);
@@ -373,81 +381,83 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       // barrier publishes it)
       lds_barrier();
       if (!last_cb) box_store(cb + 1);
-      else if (has_next) box_store(0);
     }
 
-    // ---- epilogue: bf16 straight from the accumulators (lane: 4 channels of one row) ----
-    {
-      int rb_unused[4];
-      uint32_t yo[4];
-      frag_rows(ti, rb_unused, yo);
-      const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
-      constexpr int NG = MF == 16 ? 1 : 4;  // runs of 4 channels per lane per fragment
+    // ---- epilogue, two 128-row halves staged in the box region: waves wr 2h, 2h+1 write their
+    // bf16 rows, then every thread owns one 8-channel column chunk and walks rows (16-B coalesced
+    // stores, statistics carried in registers across tiles as in v4) ----
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
+    for (int half = 0; half < 2; ++half) {
+      if ((wr >> 1) == half) {
 #pragma unroll
-        for (int gq = 0; gq < NG; ++gq) {
-          // tile-local channel of this lane's 4-run: 16x16: 4 (l >> 4); 32x32: 8 gq + 4 (l >> 5)
-          const int nl = wc * WN + j * MF + (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4);
-          const int n = n0 + nl;
-          float es[4] = {0.f, 0.f, 0.f, 0.f}, eq[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < TM; ++i) {
+          const int row = (wr & 1) * WM + i * MF + (lane & (MF - 1));  // row within the half
 #pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float v[4];
+          for (int j = 0; j < TN; ++j) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc[j][i][gq * 4 + r];
-            uint2 o;
-            o.x = pack2bf(v[0], v[1]);
-            o.y = pack2bf(v[2], v[3]);
-            const bool ok = (yo[i] != 0x80000000u) & (n < p.Cout);
-            const uint32_t off = ok ? yo[i] + (uint32_t)n * 2 : 0x80000000u;
-            __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, o), yrs, off, 0, 0);
-            if constexpr (EPI == 1) {
-              if (ok) {
-                const float d[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
-                                    __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) { es[r] += d[r]; eq[r] += d[r] * d[r]; }
-              }
-            }
-            if constexpr (EPI == 2) {
-              if (ok) {
-                // producer BN-backward partials from the bf16 dz actually stored
-                const long long row = (ti.ybase + yo[i] / 2) / p.ldy;
-                const uint2 yv = *(const uint2*)(p.bn_y + row * p.bn_ld + n);
-                const float d[4] = {__uint_as_float(o.x << 16), __uint_as_float(o.x & 0xffff0000u),
-                                    __uint_as_float(o.y << 16), __uint_as_float(o.y & 0xffff0000u)};
-                const float yy[4] = {__uint_as_float(yv.x << 16), __uint_as_float(yv.x & 0xffff0000u),
-                                     __uint_as_float(yv.y << 16), __uint_as_float(yv.y & 0xffff0000u)};
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const int cl = nl + r;
-                  const float gm = (yy[r] * ss_lds[2 * BN + cl] + ss_lds[3 * BN + cl] > 0.f) ? d[r] : 0.f;
-                  es[r] += gm;
-                  eq[r] += gm * (yy[r] - ss_lds[cl]) * ss_lds[BN + cl];
-                }
-              }
+            for (int gq = 0; gq < (MF == 16 ? 1 : 4); ++gq) {
+              const int col = wc * WN + j * MF + (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4);
+              uint2 o;
+              o.x = pack2bf(acc[j][i][gq * 4 + 0], acc[j][i][gq * 4 + 1]);
+              o.y = pack2bf(acc[j][i][gq * 4 + 2], acc[j][i][gq * 4 + 3]);
+              *(uint2*)(box + row * LDE + col) = o;
             }
           }
-          if constexpr (EPI != 0) {
+        }
+      }
+      lds_barrier();
+      {
+        const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
+        const int cc = tid % OCPR;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              float s = es[r], q = eq[r];
+        for (int it = 0; it < EPI_IT; ++it) {
+          const int row = tid / OCPR + it * RPP;  // row within the half
+          const int lr = half * 128 + row;
+          const bool act = (tid < RPP * OCPR) & (row < 128);
+          const uint4 dv = *(const uint4*)(box + min(row, 127) * LDE + cc * 8);
+          uint32_t yo;
+          long long grow;  // global output row
+          if constexpr (KS == 133) {
+            grow = ti.m0 + lr;
+            yo = (act && grow < p.M) ? (uint32_t)(lr * p.ldy * 2) : 0x80000000u;
+          } else {
+            const int t = (int)fdiv((uint32_t)lr, g.fP), j = lr - t * g.P;
+            grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
+            yo = (act && ti.p0 + j < g.HW) ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2)
+                                          : 0x80000000u;
+          }
+          const int n = n0 + cc * 8;
+          const bool ok = (yo != 0x80000000u) & (n < p.Cout);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, dv),
+                                                 yrs, ok ? yo + (uint32_t)n * 2 : 0x80000000u, 0, 0);
+          if constexpr (EPI == 1) {
+            if (ok) {
+              float d8[8];
+              unpack8(dv, d8);
 #pragma unroll
-              for (int o = 1; o < MF; o <<= 1) {  // lanes holding the same channels (same l / MF)
-                s += __shfl_xor(s, o, 64);
-                q += __shfl_xor(q, o, 64);
-              }
-              if ((lane & (MF - 1)) == 0) {
-                atomicAdd(st_lds + nl + r, s);
-                atomicAdd(st_lds + BN + nl + r, q);
+              for (int k = 0; k < 8; ++k) { e_s[k] += d8[k]; e_q[k] += d8[k] * d8[k]; }
+            }
+          }
+          if constexpr (EPI == 2) {
+            if (ok) {
+              float d8[8], y8[8];
+              unpack8(dv, d8);
+              unpack8(*(const uint4*)(p.bn_y + grow * p.bn_ld + n), y8);
+#pragma unroll
+              for (int k = 0; k < 8; ++k) {
+                const int cl = cc * 8 + k;
+                const float gm = (y8[k] * ss_lds[2 * BN + cl] + ss_lds[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
+                e_s[k] += gm;
+                e_q[k] += gm * (y8[k] - ss_lds[cl]) * ss_lds[BN + cl];
               }
             }
           }
         }
       }
+      lds_barrier();  // the half's rows are consumed before the region is rewritten
     }
+    // the next tile's first box (its loads were issued at the last block's first tap)
+    if (has_next) box_store(0);
 
     if (!has_next) break;
     m_tile = next_tile;
@@ -457,11 +467,22 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // drain: the trailing fires of the last tile and the epilogue stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (EPI != 0) {
+    // per-thread column sums -> per column chunk over the row groups (fixed order)
     __syncthreads();
-    const int npad = p.num_n_tiles * BN;
-    for (int t = tid; t < BN; t += NT) {
-      p.stats[(long long)m_slot * 2 * npad + n0 + t] = st_lds[t];
-      p.stats[(long long)m_slot * 2 * npad + npad + n0 + t] = st_lds[BN + t];
+    float* red = (float*)smem;  // [2][8][NT] over the box region
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { red[k * NT + tid] = e_s[k]; red[(8 + k) * NT + tid] = e_q[k]; }
+    __syncthreads();
+    if (tid < OCPR) {
+      const int npad = p.num_n_tiles * BN;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s1 = 0.f, s2 = 0.f;
+        for (int j = tid; j < RPP * OCPR; j += OCPR) { s1 += red[k * NT + j]; s2 += red[(8 + k) * NT + j]; }
+        const int col = n0 + tid * 8 + k;
+        p.stats[(long long)m_slot * 2 * npad + col] = s1;
+        p.stats[(long long)m_slot * 2 * npad + npad + col] = s2;
+      }
     }
   }
 }
@@ -517,7 +538,7 @@ bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
 
 template <int BN, int KS, int EPI, int PRO, int MF>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
-  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * BN * BX_BK * 2 + 2 * BN * 4 +
+  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * BN * BX_BK * 2 +
                      (EPI == 2 ? 16 * BN : 0) + (PRO ? 8 * (size_t)p.Cin : 0);
   if (lds > 160 * 1024) return V4_UNSUPPORTED;
   static bool attr_set = false;
