@@ -1986,12 +1986,12 @@ static int launch_fwd(ConvParams& p, int impl, hipStream_t stream) {
 
 // x: input, w: packed weight [Npad][Kpad], y: out [M][ldy], stats: [grid_m][2][Npad] or null.
 // Returns grid_m through *grid_m_out (for sizing the stats buffer, call with y == nullptr).
-MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
-                               const float* bn_ss, int bn_ld,
-                               int B, int T, int H, int W, int Cin, int Cout,
-                               int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
-                               int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
-                               int impl, hipStream_t stream) {
+static int conv_fwd_impl(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
+                         const float* bn_ss, int bn_ld,
+                         int B, int T, int H, int W, int Cin, int Cout,
+                         int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
+                         int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
+                         int impl, const float* pro_ss, void* pro_z, hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
   p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss; p.bn_ld = bn_ld;
@@ -2016,7 +2016,8 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
   p.fCin = make_fastdiv(Cin);
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
-  if (impl == 14 || impl == 15) return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, nullptr, stream);  // conv_box.hip
+  if (impl == 14 || impl == 15)  // conv_box.hip
+    return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, pro_ss, pro_z, stream);
   if (impl >= 8) return x_u8 ? V4_UNSUPPORTED : launch_fwd_v4(p, bn, impl, stream);  // conv_v4.hip
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
     // wide / odd N tiles: LDS-DMA ring variants only, BK 64
@@ -2038,6 +2039,29 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
     if (bn == 128 && bk == 64) return launch_fwd<128, 128, 64, false>(p, impl, stream);
   }
   return (int)hipErrorInvalidValue;
+}
+
+MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
+                               const float* bn_ss, int bn_ld,
+                               int B, int T, int H, int W, int Cin, int Cout,
+                               int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
+                               int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
+                               int impl, hipStream_t stream) {
+  return conv_fwd_impl(x, x_u8, w, y, stats, bn_y, bn_ss, bn_ld, B, T, H, W, Cin, Cout, KT, KH, KW, st, sh, sw, pt,
+                       ph, pw, Kpad, Npad, ldy, bn, bk, grid_m, wo_override, impl, nullptr, nullptr, stream);
+}
+
+// Forward whose input x is the raw conv output of a BN layer: z = relu(x * scale + shift) (pro_ss
+// = that layer's [4][Cin] mean / invstd / scale / shift) is applied while the box-tiled kernel
+// stages its input, and written to pro_z (the consumer's wgrad operand; null: not needed).
+// Box-tiled variants only (impl 14 / 15); anything else returns V4_UNSUPPORTED.
+MILNCE_API int milnce_conv_fwd_pro(const void* x, const void* w, void* y, float* stats, const float* pro_ss,
+                                   void* pro_z, int B, int T, int H, int W, int Cin, int Cout, int KT, int KH,
+                                   int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy, int bn, int grid_m,
+                                   int impl, hipStream_t stream) {
+  if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
+  return conv_fwd_impl(x, 0, w, y, stats, nullptr, nullptr, 0, B, T, H, W, Cin, Cout, KT, KH, KW, 1, 1, 1, pt, ph,
+                       pw, Kpad, Npad, ldy, bn, 64, grid_m, 0, impl, pro_ss, pro_z, stream);
 }
 
 template <int TN_, int TK_, bool U8, bool DEEP = false>

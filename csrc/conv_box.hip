@@ -52,6 +52,7 @@ struct BoxGeo {
   int HW;
   FastDiv fHW, fW, fPL, fW1, ftpc, fP;
   const float* pro_ss;  // [4][Cin] of the input's BN (scale at 2*Cin, shift at 3*Cin) or null
+  bf16_t* pro_z;        // PRO 2: the transformed input z = relu(x * scale + shift), written once
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -79,11 +80,12 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int RPP = NT / OCPR;               // rows per pass
   constexpr int EPI_IT = (128 + RPP - 1) / RPP;
   constexpr int NST = 2 * EPI_IT;              // epilogue stores (16 B) per wave per tile
+  constexpr int ZC = PRO == 2 ? NBX : 0;       // z stores per wave per written box
   static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BN * BK;
   static_assert(B_INST * RPI * NWAVES == BN, "DMA mapping");
-  static_assert(NST + NDMA + NBX <= 63, "vmcnt range");
+  static_assert(NST + ZC + NDMA + NBX <= 63, "vmcnt range");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
@@ -212,11 +214,14 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     for (int k = 0; k < NBX; ++k)
       xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, xo[k], coff, 0));
   };
-  auto box_store = [&](int cb) {
+  // PRO 2: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
+  // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
+  // offsets for the others) so the vmcnt accounting stays exact
+  auto box_store = [&](int cb, const TileInfo& bt, __amdgpu_buffer_rsrc_t zs) {
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       uint4 v = xr[k];
-      if constexpr (PRO) {
+      if constexpr (PRO != 0) {
         if (xo[k] != 0x80000000u) {
           float f[8];
           unpack8(v, f);
@@ -227,7 +232,21 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         }
       }
       *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
+      if constexpr (PRO == 2) {
+        bool own = n_tile == 0 && xo[k] != 0x80000000u;
+        if constexpr (KS == 133) {
+          const int j = xrow0 + 64 * k;
+          own = own && j >= g.W1 + 1 && j <= bt.elast - bt.e0 + g.W1 + 1;
+        }
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
+                                               zs, own ? xo[k] : 0x80000000u,
+                                               __builtin_amdgcn_readfirstlane(cb * BK * 2), 0);
+      }
     }
+  };
+  auto zrsrc = [&](const TileInfo& bt, bool valid) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.pro_z + bt.xbase), (short)0,
+                                             (int)(valid ? bt.xnrec : 0u), 0x00020000);
   };
 
   // ---- per-lane fragment rows of a tile ----
@@ -277,9 +296,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
                                                0x00020000);
 #pragma unroll
   for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + 64 * k);
+  auto zrs = zrsrc(ti, PRO == 2);
   box_load(xrs, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  box_store(0);
+  box_store(0, ti, zrs);
   int gs = 0;  // global stage counter (ring slot = gs % 3)
   fire(0, 0);
   fire(1, 1 % nst_tile);
@@ -311,15 +331,21 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         //     next tile's first stage is fired there too, see below] -> NDMA
         //   * box loads issued at tap 0 of this block after firing stage cb*TAPS+2: younger
         //     than stages up to cb*TAPS+2 -> waits at taps 1, 2
-        //   * epilogue stores of the previous tile: younger than the first two stages of this tile
-        if (cb == 0 && !first_tile) {
-          if (t == 0) bx_wait<NDMA + NST>();
-          else if (t == 1) bx_wait<NST + NDMA + NBX>();
-          else if (t == 2) bx_wait<NBX + NDMA>();
+        //   * epilogue stores of the previous tile (NST) and, with PRO 2, the z stores of the
+        //     box written after them (ZC), or of the box written at the end of the previous block:
+        //     younger than the first two stages of this block
+        if (t == 0) {
+          if (cb == 0 && !first_tile) bx_wait<NDMA + NST + ZC>();
+          else if (cb > 0) bx_wait<NDMA + ZC>();
           else bx_wait<NDMA>();
+        } else if (t == 1) {
+          if (cb == 0 && !first_tile) bx_wait<NST + ZC + NDMA + NBX>();
+          else if (cb > 0) bx_wait<ZC + NDMA + NBX>();
+          else bx_wait<NDMA + NBX>();
+        } else if (t == 2) {
+          bx_wait<NBX + NDMA>();
         } else {
-          if (t == 1 || t == 2) bx_wait<NDMA + NBX>();
-          else bx_wait<NDMA>();
+          bx_wait<NDMA>();
         }
         ring_barrier();
         // fire stage s + 2 (continuing into the next tile: the weights do not depend on the tile)
@@ -340,6 +366,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
             for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
             box_load(nrs, 0);
             xrs = nrs;
+            zrs = zrsrc(tn, PRO == 2 && has_next);
           }
         }
         // ---- MFMAs of stage s: A = weights (ring), B = box rows shifted by the tap ----
@@ -380,7 +407,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       // every wave is done with this box: write the prefetched one (the next iteration's ring
       // barrier publishes it)
       lds_barrier();
-      if (!last_cb) box_store(cb + 1);
+      if (!last_cb) box_store(cb + 1, ti, zrs);
     }
 
     // ---- epilogue, two 128-row halves staged in the box region: waves wr 2h, 2h+1 write their
@@ -457,7 +484,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       lds_barrier();  // the half's rows are consumed before the region is rewritten
     }
     // the next tile's first box (its loads were issued at the last block's first tap)
-    if (has_next) box_store(0);
+    if (has_next) box_store(0, tn, zrs);
 
     if (!has_next) break;
     m_tile = next_tile;
@@ -554,6 +581,11 @@ static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
 
 template <int BN, int KS, int MF>
 static int launch_box_epi(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
+  if (g.pro_ss != nullptr && g.pro_z != nullptr) {
+    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 2, MF>(p, g, stream);
+    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 2, MF>(p, g, stream);
+    return V4_UNSUPPORTED;
+  }
   if (g.pro_ss != nullptr) {
     if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 1, MF>(p, g, stream);
     if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 1, MF>(p, g, stream);
@@ -571,11 +603,12 @@ static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
 }
 
 // impl 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (N tiles 64 / 128 / 192)
-int launch_fwd_box(ConvParams& p, int bn, int impl, const float* pro_ss, hipStream_t stream) {
+int launch_fwd_box(ConvParams& p, int bn, int impl, const float* pro_ss, void* pro_z, hipStream_t stream) {
   BoxGeo g;
   int ntiles = 0;
   if (box_geo(p, g, ntiles) != 0) return V4_UNSUPPORTED;
   g.pro_ss = pro_ss;
+  g.pro_z = (bf16_t*)pro_z;
   p.num_m_tiles = ntiles;
   if (impl == 14) {
     if (bn == 64) return launch_box_bn<64, 16>(p, g, stream);

@@ -62,13 +62,17 @@ class STConv3D(nn.Module):
             self.conv1 = nn.Conv3d(input_dim, output_dim, k, s, p, bias=False)
             self.bn1 = nn.BatchNorm3d(output_dim)
 
-    def forward(self, x, want_gsum: bool = False):
+    def forward(self, x, want_gsum: bool = False, lazy_out: bool = False):
         """Returns z, or (z, per-(clip, channel) sum of z) when ``want_gsum`` (GPU path; the
-        sum feeds the following SelfGating's global mean for free)."""
+        sum feeds the following SelfGating's global mean for free). ``lazy_out``: z feeds only
+        another STConv3D, which may apply this unit's BN + ReLU in its own conv kernel (GPU)."""
         if self.separable:
-            z = ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training)
-            return ops.conv_bn_relu(z, self.conv2.weight, self.bn2, self.s2, self.p2, self.training, want_gsum)
-        return ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training, want_gsum)
+            # the spatial conv's BN + ReLU is applied by the temporal conv where its kernel can
+            z = ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training, lazy_out=True)
+            return ops.conv_bn_relu(z, self.conv2.weight, self.bn2, self.s2, self.p2, self.training, want_gsum,
+                                    lazy_out=lazy_out)
+        return ops.conv_bn_relu(x, self.conv1.weight, self.bn1, self.s1, self.p1, self.training, want_gsum,
+                                lazy_out=lazy_out)
 
 
 class SelfGating(nn.Module):
@@ -243,7 +247,7 @@ class S3D(nn.Module):
             net = net[:, 1:, 1:, 1:, :].contiguous()
         if not pooled:
             net = ops.maxpool_tf_same(net, *self.maxpool_2a)
-        net = self.conv_2b(net)
+        net = self.conv_2b(net, lazy_out=True)  # BN + ReLU applied by conv_2c's kernel where it can
         net, gsum = self.conv_2c(net, want_gsum=True)
         # SelfGating + maxpool_3a (fused on GPU: the full-resolution gate output is never stored)
         net = ops.gated_maxpool_tf_same(net, gsum, self.gating.fc.weight, self.gating.fc.bias, *self.maxpool_3a)

@@ -56,11 +56,14 @@ def _hip():
     return hip_ops
 
 
-def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
+def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False,
+                 lazy_out: bool = False):
     """conv -> BN -> ReLU. With ``want_gsum`` also returns the per-(clip, channel) sum of the
-    output (fp32 [B, C]) that a following SelfGating needs (None on the ATen path)."""
+    output (fp32 [B, C]) that a following SelfGating needs (None on the ATen path).
+    ``lazy_out`` (GPU): the caller feeds the output only to another ``conv_bn_relu``, which may
+    apply this BN + ReLU inside its own kernel (the output is then a placeholder)."""
     if use_hip(x):
-        return _hip().conv_bn_relu(x, weight, bn, stride, padding, training, want_gsum)
+        return _hip().conv_bn_relu(x, weight, bn, stride, padding, training, want_gsum, lazy_out)
     z = aten.conv_bn_relu(x, weight, bn, stride, padding, training)
     return (z, None) if want_gsum else z
 

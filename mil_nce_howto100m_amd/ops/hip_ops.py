@@ -457,8 +457,24 @@ def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
     return best
 
 
-def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: Optional[torch.Tensor]):
+def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: Optional[torch.Tensor],
+                     pro=None):
+    """Raw conv output y (bf16) with the BN-statistics epilogue when ``stats`` is given.
+
+    ``pro = (z_out or None)``: x is a "pro" placeholder (``_pro_z``) standing for
+    relu(y_prod * scale + shift) of its producer BN. A box-tiled variant applies that while
+    staging its input and writes z to ``z_out`` (the wgrad operand); any other variant gets
+    z materialised into ``z_out`` (or a scratch buffer) first."""
     y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=x.device)
+    if pro is not None:
+        z_out = pro[0]
+        yp, ssp, ldp = x._milnce_bn
+        if plan.impl in _BOX_IMPLS and ldp == plan.Cin and x.shape[-1] == plan.Cin:
+            call("milnce_conv_fwd_pro", ptr(yp), ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
+                 plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
+                 plan.Cout, plan.bn, plan.grid_m, plan.impl, stream())
+            return y
+        x = _materialize(x, z_out)
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
@@ -542,10 +558,32 @@ def _is_lazy(t) -> bool:
     return bool(getattr(t, "_milnce_lazy", False))
 
 
-def _materialize(z: torch.Tensor) -> torch.Tensor:
-    """The bf16 relu(y * scale + shift) a lazy placeholder stands for."""
+# BN-ReLU outputs whose only consumer is another conv ("pro" placeholders, ``lazy_out``): the
+# producer skips its bn_relu_apply pass and returns a stride-0 placeholder tagged with (y, ss, ld);
+# the consumer's box-tiled kernel (csrc/conv_box.hip PRO) applies relu(y * scale + shift) while
+# staging its input box and writes z once as a by-product (its wgrad operand): the separate pass
+# (read y, write z) and the consumer's re-read of z become one read of y inside the conv. Other
+# consumer kernels materialise z first (the old cost). MILNCE_PRO_FUSE=0 disables.
+_PRO_FUSE = os.environ.get("MILNCE_PRO_FUSE", "1") != "0"
+_BOX_IMPLS = (14, 15)
+
+
+def _pro_z(shape, device, bn_info) -> torch.Tensor:
+    z = torch.empty((1,), dtype=BF16, device=device).expand(*shape)
+    z._milnce_bn = bn_info
+    z._milnce_pro = True
+    return z
+
+
+def _is_pro(t) -> bool:
+    return bool(getattr(t, "_milnce_pro", False))
+
+
+def _materialize(z: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The bf16 relu(y * scale + shift) a lazy placeholder stands for (into ``out`` if given)."""
     y, ss, ld = z._milnce_bn
-    out = torch.empty(z.shape, dtype=BF16, device=z.device)
+    if out is None:
+        out = torch.empty(z.shape, dtype=BF16, device=z.device)
     B = z.shape[0]
     thw = out.numel() // (B * z.shape[-1])
     call("milnce_bn_relu_apply", ptr(y), ld, ptr(out), z.shape[-1], ptr(ss), z.shape[-1], B, thw, None, stream())
@@ -845,7 +883,7 @@ def _bn_nparts(M: int) -> int:
 
 
 def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
-                   wo_override=0):
+                   wo_override=0, pro=None):
     """conv (statistics epilogue) + BN finalize: returns (plan, raw conv output y, ss)."""
     plan = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
     dev = x.device
@@ -867,7 +905,7 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     if y is None:
         stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
                  if training else None)
-        y = conv_forward_raw(x, wp, plan, stats)
+        y = conv_forward_raw(x, wp, plan, stats, pro)
         nparts = plan.grid_m  # as tuned
     C = plan.Cout
     ss = torch.empty((4 * C,), dtype=F32, device=dev)
@@ -978,16 +1016,25 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
 class _ConvBNReLU(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
-                want_gsum, wo_override=0):
+                want_gsum, wo_override=0, lazy_out=False, need_z=True):
+        pro, x_saved = None, x
+        if _is_pro(x):
+            # x stands for its producer's relu(y * scale + shift): this conv's kernel applies it
+            # and writes z (the wgrad operand) when one is needed
+            x_saved = torch.empty(x.shape, dtype=BF16, device=x.device) if need_z else None
+            pro = (x_saved,)
         plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
-                                     training, wo_override)
+                                     training, wo_override, pro)
         C = plan.Cout
         gsum = _zeros_f32((plan.B, C), x.device) if want_gsum else None
-        lazy = want_gsum and _LAZY_GATE_Z
-        z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
-        call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
-             plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
-        ctx.save_for_backward(x, weight, y, ss, gamma)
+        if lazy_out and not want_gsum and _PRO_FUSE:
+            z = _pro_z(y.shape, y.device, (y, ss, C))  # applied by the consuming conv
+        else:
+            lazy = want_gsum and _LAZY_GATE_Z
+            z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
+            call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
+                 plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
+        ctx.save_for_backward(x_saved, weight, y, ss, gamma)
         ctx.beta = beta  # parameter handle only (its gradient buffer may be written in place)
         ctx.training = bool(training)
         ctx.plan = plan
@@ -1003,7 +1050,7 @@ class _ConvBNReLU(torch.autograd.Function):
     def backward(ctx, dz, *unused):
         x, weight, y, ss, gamma = ctx.saved_tensors
         dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
-        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None
+        return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvBNReLUPool(torch.autograd.Function):
@@ -1056,13 +1103,18 @@ class _ConvBNReLUPool(torch.autograd.Function):
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
 
 
-def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False):
-    if x.dtype not in (torch.uint8, BF16):
-        x = x.to(BF16)
-    x = x.contiguous()
+def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool = False, lazy_out: bool = False):
+    """conv -> BN -> ReLU. ``lazy_out``: the output feeds only another conv_bn_relu, which may
+    apply this BN itself (a "pro" placeholder is returned, see ``_pro_z``)."""
+    if not _is_pro(x):
+        if x.dtype not in (torch.uint8, BF16):
+            x = x.to(BF16)
+        x = x.contiguous()
     momentum = bn.momentum if bn.momentum is not None else 0.1
+    need_z = torch.is_grad_enabled() and weight.requires_grad  # the wgrad reads the (fused) input
     out = _ConvBNReLU.apply(x, weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                            tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum))
+                            tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum), 0,
+                            bool(lazy_out), bool(need_z))
     return out
 
 

@@ -82,3 +82,47 @@ def test_conv_box_matches_reference(case):
                 assert torch.equal(y, y2) and torch.equal(dx, dx2), (impl, wgs)
     finally:
         plan.impl = plan.d_impl = 0
+
+
+@pytest.mark.parametrize("shape,cin,cmid,k", [((2, 8, 50, 50), 64, 192, (3, 3, 3)),
+                                             ((3, 8, 11, 13), 128, 128, (3, 3, 3))])
+def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
+    """A separable S3D-G unit (spatial conv -> BN -> ReLU -> temporal conv) with the spatial BN +
+    ReLU applied inside the temporal conv's box kernel (hip_ops "pro" placeholders, csrc/conv_box.hip
+    PRO 2: z written as the kernel's by-product) is bitwise the unfused path (bn_relu_apply pass,
+    then the same box kernel): outputs, input gradient, every parameter gradient and the running
+    statistics; and in no-grad mode (PRO 1: no z written)."""
+    import copy
+    from mil_nce_howto100m_amd.models.s3dg import STConv3D
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(5)
+    unit = STConv3D(cin, cmid, list(k), padding=1, separable=True).cuda().train()
+    x = torch.randn(*shape, cin, device=DEV).to(torch.bfloat16)
+    g = torch.randn(*shape, cmid, device=DEV).to(torch.bfloat16)
+    old = h._PRO_FUSE
+    res = {}
+    try:
+        for fuse in (False, True, False):
+            h._PRO_FUSE = fuse
+            u = copy.deepcopy(unit)
+            xi = x.clone().requires_grad_(True)
+            out = u(xi)
+            # force the box-tiled kernel on the temporal conv (the tuner picked on the first call)
+            plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
+            plan.impl = 15
+            xi.grad = None
+            u.zero_grad()
+            out = u(xi)
+            out.backward(g)
+            grads = {n: p.grad.clone() for n, p in u.named_parameters()}
+            res[fuse] = (out.detach(), xi.grad.clone(), grads, u.bn1.running_mean.clone(), u.bn2.running_var.clone())
+            with torch.no_grad():
+                res[(fuse, "ng")] = u(x).clone()
+        a, b = res[False], res[True]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        for n in a[2]:
+            assert torch.equal(a[2][n], b[2][n]), n
+        assert torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
+        assert torch.equal(res[(False, "ng")], res[(True, "ng")])
+    finally:
+        h._PRO_FUSE = old
