@@ -45,6 +45,13 @@ static constexpr int BX_ROWS = 448;      // box capacity (rows)
 static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per thread: 7
 static constexpr int BX_STAGES = 3;
 
+// Diagnostic ablations (debug libraries only, tools/gpu/box_ablate.sh; results are garbage):
+// bit 0 box loads read one fixed chunk (L1-hot), bit 1 no weight DMA, bit 2 no epilogue stores /
+// statistics, bit 3 no epilogue at all (no staging either).
+#ifndef BOX_ABLATE
+#define BOX_ABLATE 0
+#endif
+
 struct BoxGeo {
   int KS;          // 133 or 311
   int W1, PL;      // 133: W + 1, (H + 1) * (W + 1)
@@ -138,7 +145,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     const int woff = __builtin_amdgcn_readfirstlane((tap * Cin + cb * BK) * 2);
 #pragma unroll
     for (int i = 0; i < B_INST; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, ob[i],
+      if (!(BOX_ABLATE & 2)) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, ob[i],
                                                woff, 0, 0);
   };
 
@@ -212,7 +219,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
 #pragma unroll
     for (int k = 0; k < NBX; ++k)
-      xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, xo[k], coff, 0));
+      xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (BOX_ABLATE & 1) ? 0u : xo[k], coff, 0));
   };
   // PRO 2: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
@@ -414,7 +421,26 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     // bf16 rows, then every thread owns one 8-channel column chunk and walks rows (16-B coalesced
     // stores, statistics carried in registers across tiles as in v4) ----
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
+    for (int half = 0; half < ((BOX_ABLATE & 8) ? 0 : 2); ++half) {
+      // EPI 2: the producer's raw outputs of this thread's rows, loaded before the staging writes
+      // and the barrier so their latency overlaps them (one load chain, not one per row)
+      uint4 ypre[EPI_IT];
+      if constexpr (EPI == 2) {
+        const int cc = tid % OCPR;
+#pragma unroll
+        for (int it = 0; it < EPI_IT; ++it) {
+          const int lr = half * 128 + min(tid / OCPR + it * RPP, 127);
+          long long grow;
+          if constexpr (KS == 133) {
+            grow = min(ti.m0 + lr, p.M - 1);
+          } else {
+            const int t = (int)fdiv((uint32_t)lr, g.fP), j = min(lr - t * g.P, g.HW - 1 - ti.p0);
+            grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
+          }
+          const int n = min(n0 + cc * 8, p.Cout - 8);
+          ypre[it] = *(const uint4*)(p.bn_y + grow * p.bn_ld + n);
+        }
+      }
       if ((wr >> 1) == half) {
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -454,7 +480,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
                                           : 0x80000000u;
           }
           const int n = n0 + cc * 8;
-          const bool ok = (yo != 0x80000000u) & (n < p.Cout);
+          const bool ok = (yo != 0x80000000u) & (n < p.Cout) & !(BOX_ABLATE & 4);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, dv),
                                                  yrs, ok ? yo + (uint32_t)n * 2 : 0x80000000u, 0, 0);
           if constexpr (EPI == 1) {
@@ -469,7 +495,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
             if (ok) {
               float d8[8], y8[8];
               unpack8(dv, d8);
-              unpack8(*(const uint4*)(p.bn_y + grow * p.bn_ld + n), y8);
+              unpack8(ypre[it], y8);
 #pragma unroll
               for (int k = 0; k < 8; ++k) {
                 const int cl = cc * 8 + k;

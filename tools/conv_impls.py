@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--hw", type=int, default=50)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--impls", type=int, nargs="+", default=[3, 4, 5, 7])
+    ap.add_argument("--producer", type=int, default=0,
+                    help="1: dgrad with the producer-BN partials epilogue (as in the training step)")
     o = ap.parse_args()
     k = tuple(o.k)
     pad = tuple(kk // 2 for kk in k)
@@ -46,6 +48,11 @@ def main():
     stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device="cuda")
     dy = torch.randn(plan.B, plan.To, plan.Ho, plan.Wo, o.cout, device="cuda").to(torch.bfloat16)
     fl = 2.0 * plan.M * plan.Cout * plan.Ktot
+    prod = None
+    if o.producer:  # the producer BN of x: y = x, arbitrary scale / shift
+        ss = torch.cat([torch.zeros(o.cin, device="cuda"), torch.ones(o.cin, device="cuda"),
+                        torch.ones(o.cin, device="cuda"), torch.zeros(o.cin, device="cuda")])
+        prod = (x, ss, o.cin)
     print(f"{tuple(x.shape)} -> {o.cout} k{k}: fwd tile bn {plan.bn} bk {plan.bk}, dgrad tile bn {plan.d_bn} "
           f"bk {plan.d_bk}; {fl / 1e9:.0f} GFLOP", flush=True)
     g0, dg0 = plan.grid_m, plan.d_grid_m
@@ -57,7 +64,7 @@ def main():
         plan.d_grid_m = h._grid_for(plan.B * plan.T * plan.H * plan.W, plan.d_Npad, plan.d_bn, 1) if wide else dg0
         try:
             tf = timeit(lambda: h.conv_forward_raw(x, wp, plan, stats))
-            td = timeit(lambda: h.conv_dgrad(dy, wd, plan))
+            td = timeit(lambda: h.conv_dgrad(dy, wd, plan, prod))
         except Exception as e:  # variant not available for this tile
             print(f"impl {impl}: {e}")
             continue
