@@ -44,7 +44,12 @@ def _run(out, world, chunks):
         env = dict(os.environ)
         env.update({"RANK": str(r), "LOCAL_RANK": str(r), "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world),
                     "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "MILNCE_DEVICE_INDEX": "0",
-                    "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+                    "HSA_ENABLE_IPC_MODE_LEGACY": "0",
+                    # one conv kernel family whatever the batch split: the v3 / v4 variants sum in
+                    # the same order (bitwise equal), the box-tiled ones (csrc/conv_box.hip) in
+                    # another, and at random init the network amplifies bf16-level differences
+                    # between the W=1 and W=2 kernel choices to several % of the gradient
+                    "MILNCE_BOX": "0"})
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, out, str(chunks)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
