@@ -1991,7 +1991,7 @@ static int conv_fwd_impl(const void* x, int x_u8, const void* w, void* y, float*
                          int B, int T, int H, int W, int Cin, int Cout,
                          int KT, int KH, int KW, int st, int sh, int sw, int pt, int ph, int pw,
                          int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
-                         int impl, const float* pro_ss, void* pro_z, hipStream_t stream) {
+                         int impl, const BoxPro& pro, hipStream_t stream) {
   ConvParams p;
   p.x = x; p.w = (const bf16_t*)w; p.y = (bf16_t*)y; p.stats = stats;
   p.bn_y = (const bf16_t*)bn_y; p.bn_ss = bn_ss; p.bn_ld = bn_ld;
@@ -2017,7 +2017,7 @@ static int conv_fwd_impl(const void* x, int x_u8, const void* w, void* y, float*
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
   if (impl == 14 || impl == 15)  // conv_box.hip
-    return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, pro_ss, pro_z, stream);
+    return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, pro, stream);
   if (impl >= 8) return x_u8 ? V4_UNSUPPORTED : launch_fwd_v4(p, bn, impl, stream);  // conv_v4.hip
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
     // wide / odd N tiles: LDS-DMA ring variants only, BK 64
@@ -2048,7 +2048,7 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
                                int Kpad, int Npad, int ldy, int bn, int bk, int grid_m, int wo_override,
                                int impl, hipStream_t stream) {
   return conv_fwd_impl(x, x_u8, w, y, stats, bn_y, bn_ss, bn_ld, B, T, H, W, Cin, Cout, KT, KH, KW, st, sh, sw, pt,
-                       ph, pw, Kpad, Npad, ldy, bn, bk, grid_m, wo_override, impl, nullptr, nullptr, stream);
+                       ph, pw, Kpad, Npad, ldy, bn, bk, grid_m, wo_override, impl, BoxPro(), stream);
 }
 
 // Forward whose input x is the raw conv output of a BN layer: z = relu(x * scale + shift) (pro_ss
@@ -2060,8 +2060,31 @@ MILNCE_API int milnce_conv_fwd_pro(const void* x, const void* w, void* y, float*
                                    int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy, int bn, int grid_m,
                                    int impl, hipStream_t stream) {
   if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
+  BoxPro pro;
+  pro.ss = pro_ss;
+  pro.z = pro_z;
   return conv_fwd_impl(x, 0, w, y, stats, nullptr, nullptr, 0, B, T, H, W, Cin, Cout, KT, KH, KW, 1, 1, 1, pt, ph,
-                       pw, Kpad, Npad, ldy, bn, 64, grid_m, 0, impl, pro_ss, pro_z, stream);
+                       pw, Kpad, Npad, ldy, bn, 64, grid_m, 0, impl, pro, stream);
+}
+
+// dgrad of a conv whose output went through BN -> ReLU, from dz (the gradient of the ReLU output)
+// instead of dy: the box-tiled kernel stages dy = k0 * (dz * mask - k1 - xhat * k2) (y, ss: that
+// BN's raw conv output and [4][C] constants; coef: [3][C] from milnce_bn_bwd_finalize) and writes
+// dy to dy_out (the wgrad operand). part / bn_y / bn_ss / bn_ld: the producer-BN partials of dX as
+// in milnce_conv_fwd. Box-tiled variants with N tiles <= 128 only (else V4_UNSUPPORTED).
+MILNCE_API int milnce_conv_dgrad_bnbwd(const void* dz, const void* wd, void* dx, float* part, const void* bn_y,
+                                       const float* bn_ss, int bn_ld, const void* y, const float* ss,
+                                       const float* coef, void* dy_out, int B, int T, int H, int W, int C,
+                                       int Cx, int KT, int KH, int KW, int pt, int ph, int pw, int Kpad, int Npad,
+                                       int bn, int grid_m, int impl, hipStream_t stream) {
+  if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
+  BoxPro pro;
+  pro.ss = ss;
+  pro.z = dy_out;
+  pro.y = y;
+  pro.coef = coef;
+  return conv_fwd_impl(dz, 0, wd, dx, part, bn_y, bn_ss, bn_ld, B, T, H, W, C, Cx, KT, KH, KW, 1, 1, 1, pt, ph, pw,
+                       Kpad, Npad, Cx, bn, 64, grid_m, 0, impl, pro, stream);
 }
 
 template <int TN_, int TK_, bool U8, bool DEEP = false>

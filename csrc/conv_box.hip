@@ -58,8 +58,13 @@ struct BoxGeo {
   int P, tpc;      // 311: positions per tile (256 / T), tiles per clip
   int HW;
   FastDiv fHW, fW, fPL, fW1, ftpc, fP;
-  const float* pro_ss;  // [4][Cin] of the input's BN (scale at 2*Cin, shift at 3*Cin) or null
-  bf16_t* pro_z;        // PRO 2: the transformed input z = relu(x * scale + shift), written once
+  const float* pro_ss;  // [4][Cin] of the input's BN (mean, invstd, scale, shift) or null
+  bf16_t* pro_z;        // PRO 2 / 3: the transformed input, written once (the wgrad operand)
+  // PRO 3 (dgrad whose input x is dz of a BN layer): that layer's raw conv output y and its
+  // backward coefficients [3][Cin] (k0 = gamma * invstd, k1 = mean(dz * mask), k2 = mean(dz * mask
+  // * xhat)): the staged operand is dy = k0 * (dz * mask - k1 - xhat * k2)
+  const bf16_t* pro_y;
+  const float* pro_coef;
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -87,17 +92,20 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int RPP = NT / OCPR;               // rows per pass
   constexpr int EPI_IT = (128 + RPP - 1) / RPP;
   constexpr int NST = 2 * EPI_IT;              // epilogue stores (16 B) per wave per tile
-  constexpr int ZC = PRO == 2 ? NBX : 0;       // z stores per wave per written box
+  constexpr int ZC = PRO >= 2 ? NBX : 0;       // z stores per wave per written box
+  constexpr int NBL = PRO == 3 ? 2 * NBX : NBX;  // box loads per wave (PRO 3: dz and y)
   static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BN * BK;
   static_assert(B_INST * RPI * NWAVES == BN, "DMA mapping");
-  static_assert(NST + ZC + NDMA + NBX <= 63, "vmcnt range");
+  static_assert(NST + ZC + NDMA + NBL <= 63, "vmcnt range");
+  static_assert(PRO != 3 || BN <= 128, "PRO 3 registers");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
   bf16_t* ring = box + BX_ROWS * 80;                             // [STAGES][BN][BK]
-  float* ss_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // EPI 2: [4][BN]; PRO: [2][Cin]
+  float* ss_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // EPI 2: [4][BN]
+  float* pro_lds = ss_lds + (EPI == 2 ? 4 * BN : 0);             // PRO 1/2: [2][Cin]; PRO 3: [7][Cin]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -121,8 +129,12 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       ss_lds[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
     }
   }
-  if constexpr (PRO) {
-    for (int t = tid; t < 2 * Cin; t += NT) ss_lds[t] = g.pro_ss[2 * Cin + t];  // scale [Cin], shift [Cin]
+  if constexpr (PRO == 1 || PRO == 2) {
+    for (int t = tid; t < 2 * Cin; t += NT) pro_lds[t] = g.pro_ss[2 * Cin + t];  // scale [Cin], shift [Cin]
+  }
+  if constexpr (PRO == 3) {  // mean, invstd, scale, shift, k0, k1, k2
+    for (int t = tid; t < 4 * Cin; t += NT) pro_lds[t] = g.pro_ss[t];
+    for (int t = tid; t < 3 * Cin; t += NT) pro_lds[4 * Cin + t] = g.pro_coef[t];
   }
 
   // ---- weight ring (v4 layout: swizzled chunks, soffset = stage K offset) ----
@@ -213,13 +225,23 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   };
 
   // ---- box staging registers ----
-  uint4 xr[NBX];
+  uint4 xr[NBX], yr[PRO == 3 ? NBX : 1];
   uint32_t xo[NBX];
+  __amdgpu_buffer_rsrc_t yrs_box;  // PRO 3: the producer's y over the same box (same layout as x)
   auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb) {
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
 #pragma unroll
     for (int k = 0; k < NBX; ++k)
       xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (BOX_ABLATE & 1) ? 0u : xo[k], coff, 0));
+    if constexpr (PRO == 3) {
+#pragma unroll
+      for (int k = 0; k < NBX; ++k)
+        yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, xo[k], coff, 0));
+    }
+  };
+  auto yrsrc = [&](const TileInfo& bt, bool valid) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.pro_y + bt.xbase), (short)0,
+                                             (int)(valid ? bt.xnrec : 0u), 0x00020000);
   };
   // PRO 2: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
@@ -228,18 +250,34 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       uint4 v = xr[k];
-      if constexpr (PRO != 0) {
+      if constexpr (PRO == 1 || PRO == 2) {
         if (xo[k] != 0x80000000u) {
           float f[8];
           unpack8(v, f);
           const int c0 = cb * BK + xch * 8;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) f[u] = fmaxf(f[u] * ss_lds[c0 + u] + ss_lds[Cin + c0 + u], 0.f);
+          for (int u = 0; u < 8; ++u) f[u] = fmaxf(f[u] * pro_lds[c0 + u] + pro_lds[Cin + c0 + u], 0.f);
           v = pack8(f);
         }
       }
+      if constexpr (PRO == 3) {
+        if (xo[k] != 0x80000000u) {  // padding rows stay zero (dy is zero-padded)
+          float d[8], yy[8];
+          unpack8(v, d);
+          unpack8(yr[k], yy);
+          const int c0 = cb * BK + xch * 8;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int c = c0 + u;
+            const float gm = (yy[u] * pro_lds[2 * Cin + c] + pro_lds[3 * Cin + c] > 0.f) ? d[u] : 0.f;
+            const float xh = (yy[u] - pro_lds[c]) * pro_lds[Cin + c];
+            d[u] = pro_lds[4 * Cin + c] * (gm - pro_lds[5 * Cin + c] - xh * pro_lds[6 * Cin + c]);
+          }
+          v = pack8(d);
+        }
+      }
       *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
-      if constexpr (PRO == 2) {
+      if constexpr (PRO >= 2) {
         bool own = n_tile == 0 && xo[k] != 0x80000000u;
         if constexpr (KS == 133) {
           const int j = xrow0 + 64 * k;
@@ -303,7 +341,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
                                                0x00020000);
 #pragma unroll
   for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + 64 * k);
-  auto zrs = zrsrc(ti, PRO == 2);
+  auto zrs = zrsrc(ti, PRO >= 2);
+  if constexpr (PRO == 3) yrs_box = yrsrc(ti, true);
   box_load(xrs, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   box_store(0, ti, zrs);
@@ -346,11 +385,11 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           else if (cb > 0) bx_wait<NDMA + ZC>();
           else bx_wait<NDMA>();
         } else if (t == 1) {
-          if (cb == 0 && !first_tile) bx_wait<NST + ZC + NDMA + NBX>();
-          else if (cb > 0) bx_wait<ZC + NDMA + NBX>();
-          else bx_wait<NDMA + NBX>();
+          if (cb == 0 && !first_tile) bx_wait<NST + ZC + NDMA + NBL>();
+          else if (cb > 0) bx_wait<ZC + NDMA + NBL>();
+          else bx_wait<NDMA + NBL>();
         } else if (t == 2) {
-          bx_wait<NBX + NDMA>();
+          bx_wait<NBL + NDMA>();
         } else {
           bx_wait<NDMA>();
         }
@@ -371,9 +410,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
                                                          (int)(has_next ? tn.xnrec : 0u), 0x00020000);
 #pragma unroll
             for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
+            if constexpr (PRO == 3) yrs_box = yrsrc(tn, has_next);
             box_load(nrs, 0);
             xrs = nrs;
-            zrs = zrsrc(tn, PRO == 2 && has_next);
+            zrs = zrsrc(tn, PRO >= 2 && has_next);
           }
         }
         // ---- MFMAs of stage s: A = weights (ring), B = box rows shifted by the tap ----
@@ -592,7 +632,7 @@ bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
 template <int BN, int KS, int EPI, int PRO, int MF>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
   const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * BN * BX_BK * 2 +
-                     (EPI == 2 ? 16 * BN : 0) + (PRO ? 8 * (size_t)p.Cin : 0);
+                     (EPI == 2 ? 16 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
   if (lds > 160 * 1024) return V4_UNSUPPORTED;
   static bool attr_set = false;
   if (!attr_set) {
@@ -607,6 +647,14 @@ static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
 
 template <int BN, int KS, int MF>
 static int launch_box_epi(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
+  if (g.pro_y != nullptr) {  // BN-backward prologue (dgrad), dy written as the by-product
+    if constexpr (BN <= 128) {
+      if (g.pro_ss == nullptr || g.pro_coef == nullptr || g.pro_z == nullptr) return V4_UNSUPPORTED;
+      if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 3, MF>(p, g, stream);
+      if (p.bn_mode == 2) return launch_box_t<BN, KS, 2, 3, MF>(p, g, stream);
+    }
+    return V4_UNSUPPORTED;
+  }
   if (g.pro_ss != nullptr && g.pro_z != nullptr) {
     if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 2, MF>(p, g, stream);
     if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 2, MF>(p, g, stream);
@@ -629,12 +677,14 @@ static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
 }
 
 // impl 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (N tiles 64 / 128 / 192)
-int launch_fwd_box(ConvParams& p, int bn, int impl, const float* pro_ss, void* pro_z, hipStream_t stream) {
+int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream_t stream) {
   BoxGeo g;
   int ntiles = 0;
   if (box_geo(p, g, ntiles) != 0) return V4_UNSUPPORTED;
-  g.pro_ss = pro_ss;
-  g.pro_z = (bf16_t*)pro_z;
+  g.pro_ss = pro.ss;
+  g.pro_z = (bf16_t*)pro.z;
+  g.pro_y = (const bf16_t*)pro.y;
+  g.pro_coef = pro.coef;
   p.num_m_tiles = ntiles;
   if (impl == 14) {
     if (bn == 64) return launch_box_bn<64, 16>(p, g, stream);

@@ -72,6 +72,13 @@ bool fwd_v4_supported(const ConvParams& p, int bn, int impl);
 // box-tiled forward / dgrad (conv_box.hip, impl 14 / 15): stride-1 same-padded (1,3,3) / (3,1,1),
 // Cin % 64 == 0, N tiles 64 / 128 / 192. pro_ss: [4][Cin] BN constants of the input's producer
 // (z = relu(x * scale + shift) applied while staging) or null; pro_z: where z is also written
-// (the consumer's wgrad operand) or null.
-int launch_fwd_box(ConvParams& p, int bn, int impl, const float* pro_ss, void* pro_z, hipStream_t stream);
+// (the consumer's wgrad operand) or null. With pro.y / pro.coef (dgrad): x is dz of that BN and the
+// staged operand is its BN backward dy (written to pro.z).
+struct BoxPro {
+  const float* ss = nullptr;    // [4][Cin] mean / invstd / scale / shift of the input's BN
+  void* z = nullptr;            // transformed input written here (null: not needed)
+  const void* y = nullptr;      // dgrad BN-backward prologue: the BN's raw conv output
+  const float* coef = nullptr;  //   and its backward coefficients [3][Cin]
+};
+int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream_t stream);
 bool fwd_box_supported(const ConvParams& p, int bn, int impl);

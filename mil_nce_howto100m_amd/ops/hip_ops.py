@@ -469,10 +469,29 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     if pro is not None:
         z_out = pro[0]
         yp, ssp, ldp = x._milnce_bn
-        if plan.impl in _BOX_IMPLS and ldp == plan.Cin and x.shape[-1] == plan.Cin:
-            call("milnce_conv_fwd_pro", ptr(yp), ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
-                 plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
-                 plan.Cout, plan.bn, plan.grid_m, plan.impl, stream())
+        fusable = ldp == plan.Cin and x.shape[-1] == plan.Cin
+        zbuf = z_out if z_out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
+        thw_in = plan.T * plan.H * plan.W
+
+        def launch_pro(impl, grid):
+            if impl in _BOX_IMPLS and fusable:
+                call("milnce_conv_fwd_pro", ptr(yp), ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
+                     plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
+                     plan.Cout, plan.bn, grid, impl, stream())
+            else:  # the variant needs z in memory: its timing includes the BN-apply pass
+                call("milnce_bn_relu_apply", ptr(yp), ldp, ptr(zbuf), plan.Cin, ptr(ssp), plan.Cin, plan.B, thw_in,
+                     None, stream())
+                call("milnce_conv_fwd", ptr(zbuf), 0, ptr(wp), ptr(y), ptr(stats), None, None, 0,
+                     plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.s, *plan.p,
+                     plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
+
+        if plan.impl == 0:  # tuned on what each variant costs here (fused prologue vs apply pass + conv)
+            rows_p = stats.numel() // (2 * plan.Npad) if stats is not None else None
+            plan.impl, plan.grid_m = _tune_fwd(launch_pro, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
+                                                                      _box_geo(plan)),
+                                               plan.M, plan.Npad, plan.bn, rows_p)
+        if plan.impl in _BOX_IMPLS and fusable:
+            launch_pro(plan.impl, plan.grid_m)
             return y
         x = _materialize(x, z_out)
     kt, kh, kw = plan.k
@@ -527,6 +546,36 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx
+
+
+def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn, y: torch.Tensor,
+                     ss: torch.Tensor, coef: torch.Tensor, dy_out: torch.Tensor) -> torch.Tensor:
+    """dX of a conv whose output went through BN -> ReLU, from dz (the gradient of the ReLU output):
+    the box-tiled dgrad stages that BN's backward dy = k0 * (dz * mask - k1 - xhat * k2) itself
+    (y / ss: the BN's raw conv output and constants, coef: milnce_bn_bwd_finalize output) and writes
+    dy to ``dy_out`` for the wgrad, so the separate bn_bwd_apply pass (read dz and y, write dy) and
+    the dgrad's read of dy become its reads of dz and y. Requires a box-tiled ``plan.d_impl``."""
+    kt, kh, kw = plan.k
+    dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dz.device)
+    pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
+    part = None
+    if producer_bn is not None:
+        md = plan.B * plan.T * plan.H * plan.W
+        part = torch.empty((_stats_rows(md, plan.d_Npad, plan.d_bn) * 2 * plan.d_Npad,), dtype=F32, device=dz.device)
+    call("milnce_conv_dgrad_bnbwd", ptr(dz), ptr(wd), ptr(dx), ptr(part),
+         ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
+         producer_bn[2] if part is not None else 0, ptr(y), ptr(ss), ptr(coef), ptr(dy_out),
+         plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, pt, ph, pw, plan.d_Kpad, plan.d_Npad,
+         plan.d_bn, plan.d_grid_m, plan.d_impl, stream())
+    if part is not None:
+        attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
+    return dx
+
+
+def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
+    """The dgrad can take over this layer's BN-backward apply (``conv_dgrad_bnbwd``)."""
+    return (_PRO_FUSE and plan.d_impl in _BOX_IMPLS and plan.d_bn <= 128 and _box_geo(plan) is not None
+            and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 64 == 0)
 
 
 _FUSE_BN_BWD = True
@@ -988,7 +1037,13 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
         dw = _stem_pool_wgrad(lazy, x, y, ss, coef, weight, plan)
         return None, dw, dgamma, dbeta
     dy = torch.empty_like(y)
-    if lazy is not None:
+    dx = None
+    if lazy is None and fused is not None and ctx.needs_input_grad[0] and _bnbwd_fusable(plan, dz):
+        # BN-backward apply inside the dgrad's staging (dy written there for the wgrad)
+        call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(plan.M), ptr(gamma), ptr(ss), ptr(dgamma),
+             ptr(dbeta), ptr(coef), int(direct_bn), int(ctx.training), stream())
+        dx = conv_dgrad_bnbwd(dz, _pack(weight, plan, 1), plan, ctx.x_bn, y, ss, coef, dy)
+    elif lazy is not None:
         _bn_bwd_lazy(lazy, plan.B, plan.M, y, C, ss, C, gamma, part, nparts, ps, dgamma, dbeta, coef, dy, C,
                      direct_bn, ctx.training)
     else:
@@ -999,8 +1054,7 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
         _grad_done(gamma)
         _grad_done(beta)
         dgamma = dbeta = None
-    dx = None
-    if ctx.needs_input_grad[0]:
+    if ctx.needs_input_grad[0] and dx is None:
         wd = _pack(weight, plan, 1)
         dx = conv_dgrad(dy, wd, plan, ctx.x_bn)
     dw = None

@@ -89,9 +89,10 @@ def test_conv_box_matches_reference(case):
 def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
     """A separable S3D-G unit (spatial conv -> BN -> ReLU -> temporal conv) with the spatial BN +
     ReLU applied inside the temporal conv's box kernel (hip_ops "pro" placeholders, csrc/conv_box.hip
-    PRO 2: z written as the kernel's by-product) is bitwise the unfused path (bn_relu_apply pass,
-    then the same box kernel): outputs, input gradient, every parameter gradient and the running
-    statistics; and in no-grad mode (PRO 1: no z written)."""
+    PRO 2: z written as the kernel's by-product) and the spatial BN's backward apply inside its
+    dgrad (PRO 3: dy written as the by-product) is bitwise the unfused path (bn_relu_apply /
+    bn_bwd_apply passes, then the same box kernels): outputs, input gradient, every parameter
+    gradient and the running statistics; and in no-grad mode (PRO 1: no z written)."""
     import copy
     from mil_nce_howto100m_amd.models.s3dg import STConv3D
     from mil_nce_howto100m_amd.ops import hip_ops as h
@@ -110,6 +111,11 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
             # force the box-tiled kernel on the temporal conv (the tuner picked on the first call)
             plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
             plan.impl = 15
+            # and on the spatial conv's dgrad: its BN backward (dy) is then staged by that dgrad
+            # (conv_dgrad_bnbwd, PRO 3) when fused
+            plan1 = h.conv_plan(tuple(shape) + (cin,), (cmid, cin, 1, k[1], k[2]), (1, 1, 1), (0, 1, 1))
+            if plan1.d_bn <= 128:
+                plan1.d_impl = 15
             xi.grad = None
             u.zero_grad()
             out = u(xi)
