@@ -572,9 +572,16 @@ def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, produce
     return dx
 
 
+# Opt-in (MILNCE_BNBWD_FUSE=1): measured slower in the step (profiles/r3_box_conv.md): the conv_2c
+# spatial dgrad went 1.42 -> 2.74 ms with the prologue against ~1.1 ms of bn_bwd_apply it replaces
+# (twice the box loads plus seven per-channel constants per staged element, all serial to the MFMA
+# loop at one workgroup per CU); the 25^2 / 13^2 layers came out even.
+_BNBWD_FUSE = os.environ.get("MILNCE_BNBWD_FUSE", "0") == "1"
+
+
 def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
     """The dgrad can take over this layer's BN-backward apply (``conv_dgrad_bnbwd``)."""
-    return (_PRO_FUSE and plan.d_impl in _BOX_IMPLS and plan.d_bn <= 128 and _box_geo(plan) is not None
+    return (_BNBWD_FUSE and _PRO_FUSE and plan.d_impl in _BOX_IMPLS and plan.d_bn <= 128 and _box_geo(plan) is not None
             and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 64 == 0)
 
 

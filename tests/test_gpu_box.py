@@ -100,11 +100,11 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
     unit = STConv3D(cin, cmid, list(k), padding=1, separable=True).cuda().train()
     x = torch.randn(*shape, cin, device=DEV).to(torch.bfloat16)
     g = torch.randn(*shape, cmid, device=DEV).to(torch.bfloat16)
-    old = h._PRO_FUSE
+    old, old_b = h._PRO_FUSE, h._BNBWD_FUSE
     res = {}
     try:
         for fuse in (False, True, False):
-            h._PRO_FUSE = fuse
+            h._PRO_FUSE = h._BNBWD_FUSE = fuse
             u = copy.deepcopy(unit)
             xi = x.clone().requires_grad_(True)
             out = u(xi)
@@ -131,4 +131,4 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
         assert torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
         assert torch.equal(res[(False, "ng")], res[(True, "ng")])
     finally:
-        h._PRO_FUSE = old
+        h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
