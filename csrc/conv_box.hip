@@ -464,22 +464,25 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     for (int half = 0; half < ((BOX_ABLATE & 8) ? 0 : 2); ++half) {
       // EPI 2: the producer's raw outputs of this thread's rows, loaded before the staging writes
       // and the barrier so their latency overlaps them (one load chain, not one per row)
+      // (at most 4 rows ahead: the other half's waves still hold their accumulators here)
+      constexpr int NPRE = EPI_IT < 4 ? EPI_IT : 4;
       uint4 ypre[EPI_IT];
-      if constexpr (EPI == 2) {
+      auto yload = [&](int it) {
         const int cc = tid % OCPR;
-#pragma unroll
-        for (int it = 0; it < EPI_IT; ++it) {
-          const int lr = half * 128 + min(tid / OCPR + it * RPP, 127);
-          long long grow;
-          if constexpr (KS == 133) {
-            grow = min(ti.m0 + lr, p.M - 1);
-          } else {
-            const int t = (int)fdiv((uint32_t)lr, g.fP), j = min(lr - t * g.P, g.HW - 1 - ti.p0);
-            grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
-          }
-          const int n = min(n0 + cc * 8, p.Cout - 8);
-          ypre[it] = *(const uint4*)(p.bn_y + grow * p.bn_ld + n);
+        const int lr = half * 128 + min(tid / OCPR + it * RPP, 127);
+        long long grow;
+        if constexpr (KS == 133) {
+          grow = min(ti.m0 + lr, p.M - 1);
+        } else {
+          const int t = (int)fdiv((uint32_t)lr, g.fP), j = min(lr - t * g.P, g.HW - 1 - ti.p0);
+          grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
         }
+        const int n = min(n0 + cc * 8, p.Cout - 8);
+        return *(const uint4*)(p.bn_y + grow * p.bn_ld + n);
+      };
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int it = 0; it < NPRE; ++it) ypre[it] = yload(it);
       }
       if ((wr >> 1) == half) {
 #pragma unroll
@@ -502,6 +505,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       {
         const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
         const int cc = tid % OCPR;
+        if constexpr (EPI == 2) {
+#pragma unroll
+          for (int it = NPRE; it < EPI_IT; ++it) ypre[it] = yload(it);
+        }
 #pragma unroll
         for (int it = 0; it < EPI_IT; ++it) {
           const int row = tid / OCPR + it * RPP;  // row within the half
