@@ -246,36 +246,62 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // PRO 2: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
   // offsets for the others) so the vmcnt accounting stays exact
-  auto box_store = [&](int cb, const TileInfo& bt, __amdgpu_buffer_rsrc_t zs) {
+  // The prologue transform of the staged chunks, in registers. The per-channel constants of this
+  // thread's 8 channels are read into registers once per call: with the LDS box stores in between,
+  // the compiler could not reuse LDS reads across rows. (1,3,3): applied after tap 3's MFMAs of the
+  // block (the loads have landed there: tap 3's stage was fired after them), so the VALU work
+  // interleaves with the MFMA phases; (3,1,1): right before the store.
+  auto box_xform = [&](int cb) {
+    const int c0 = cb * BK + xch * 8;
+    if constexpr (PRO == 1 || PRO == 2) {
+      float sc[8], sh[8];
 #pragma unroll
-    for (int k = 0; k < NBX; ++k) {
-      uint4 v = xr[k];
-      if constexpr (PRO == 1 || PRO == 2) {
+      for (int u = 0; u < 8; ++u) { sc[u] = pro_lds[c0 + u]; sh[u] = pro_lds[Cin + c0 + u]; }
+#pragma unroll
+      for (int k = 0; k < NBX; ++k) {
         if (xo[k] != 0x80000000u) {
           float f[8];
-          unpack8(v, f);
-          const int c0 = cb * BK + xch * 8;
+          unpack8(xr[k], f);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) f[u] = fmaxf(f[u] * pro_lds[c0 + u] + pro_lds[Cin + c0 + u], 0.f);
-          v = pack8(f);
+          for (int u = 0; u < 8; ++u) f[u] = fmaxf(f[u] * sc[u] + sh[u], 0.f);
+          xr[k] = pack8(f);
         }
       }
-      if constexpr (PRO == 3) {
+    }
+    if constexpr (PRO == 3) {
+      float cm[8], ci[8], cs[8], ch[8], k0[8], k1[8], k2[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + u;
+        cm[u] = pro_lds[c]; ci[u] = pro_lds[Cin + c]; cs[u] = pro_lds[2 * Cin + c]; ch[u] = pro_lds[3 * Cin + c];
+        k0[u] = pro_lds[4 * Cin + c]; k1[u] = pro_lds[5 * Cin + c]; k2[u] = pro_lds[6 * Cin + c];
+      }
+#pragma unroll
+      for (int k = 0; k < NBX; ++k) {
         if (xo[k] != 0x80000000u) {  // padding rows stay zero (dy is zero-padded)
           float d[8], yy[8];
-          unpack8(v, d);
+          unpack8(xr[k], d);
           unpack8(yr[k], yy);
-          const int c0 = cb * BK + xch * 8;
 #pragma unroll
           for (int u = 0; u < 8; ++u) {
-            const int c = c0 + u;
-            const float gm = (yy[u] * pro_lds[2 * Cin + c] + pro_lds[3 * Cin + c] > 0.f) ? d[u] : 0.f;
-            const float xh = (yy[u] - pro_lds[c]) * pro_lds[Cin + c];
-            d[u] = pro_lds[4 * Cin + c] * (gm - pro_lds[5 * Cin + c] - xh * pro_lds[6 * Cin + c]);
+            const float gm = (yy[u] * cs[u] + ch[u] > 0.f) ? d[u] : 0.f;
+            const float xh = (yy[u] - cm[u]) * ci[u];
+            d[u] = k0[u] * (gm - k1[u] - xh * k2[u]);
           }
-          v = pack8(d);
+          xr[k] = pack8(d);
         }
       }
+    }
+  };
+  constexpr int XFORM_TAP = KS == 133 ? 3 : -1;  // -1: at the store
+  // PRO 2 / 3: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
+  // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
+  // offsets for the others) so the vmcnt accounting stays exact
+  auto box_store = [&](int cb, const TileInfo& bt, __amdgpu_buffer_rsrc_t zs) {
+    if constexpr (XFORM_TAP < 0) box_xform(cb);
+#pragma unroll
+    for (int k = 0; k < NBX; ++k) {
+      const uint4 v = xr[k];
       *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
       if constexpr (PRO >= 2) {
         bool own = n_tile == 0 && xo[k] != 0x80000000u;
@@ -345,6 +371,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   if constexpr (PRO == 3) yrs_box = yrsrc(ti, true);
   box_load(xrs, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (XFORM_TAP >= 0) box_xform(0);
   box_store(0, ti, zrs);
   int gs = 0;  // global stage counter (ring slot = gs % 3)
   fire(0, 0);
@@ -450,6 +477,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           __builtin_amdgcn_s_setprio(0);
         }
         ++gs;
+        if constexpr (XFORM_TAP >= 0 && PRO != 0) {
+          if (t == XFORM_TAP) box_xform(last_cb ? 0 : cb + 1);
+        }
       }
       // every wave is done with this box: write the prefetched one (the next iteration's ring
       // barrier publishes it)
