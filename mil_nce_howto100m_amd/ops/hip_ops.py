@@ -572,11 +572,12 @@ def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, produce
     return dx
 
 
-# Opt-in (MILNCE_BNBWD_FUSE=1): measured slower in the step (profiles/r3_box_conv.md): the conv_2c
-# spatial dgrad went 1.42 -> 2.74 ms with the prologue against ~1.1 ms of bn_bwd_apply it replaces
-# (twice the box loads plus seven per-channel constants per staged element, all serial to the MFMA
-# loop at one workgroup per CU); the 25^2 / 13^2 layers came out even.
-_BNBWD_FUSE = os.environ.get("MILNCE_BNBWD_FUSE", "0") == "1"
+# MILNCE_BNBWD_FUSE=0 disables. First version measured slower in the step (conv_2c spatial dgrad
+# 1.42 -> 2.74 ms against ~1.1 ms of bn_bwd_apply removed: seven per-channel constants re-read from
+# LDS per staged element, applied serially after the block's MFMAs); with the constants in
+# registers and the transform after tap 3's MFMAs: 2.35 ms, same-box bench 4285 -> 4303 pairs/s
+# (profiles/r3_box_conv.md).
+_BNBWD_FUSE = os.environ.get("MILNCE_BNBWD_FUSE", "1") != "0"
 
 
 def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
