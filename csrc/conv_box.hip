@@ -115,7 +115,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   const int n_tile = logical % p.num_n_tiles;
   const int m_slot = logical / p.num_n_tiles;
   const int n0 = n_tile * BN;
-  const int ncb = p.Cin / BK;
+  const int ncb = (p.Cin + BK - 1) / BK;  // the last block may be partial (its missing chunks read zero)
   const int nst_tile = ncb * TAPS;  // stages per tile
   const int Cin = p.Cin;
 
@@ -228,15 +228,21 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   uint4 xr[NBX], yr[PRO == 3 ? NBX : 1];
   uint32_t xo[NBX];
   __amdgpu_buffer_rsrc_t yrs_box;  // PRO 3: the producer's y over the same box (same layout as x)
+  // this thread's chunk of channel block cb exists (Cin not a multiple of 64: the last block is
+  // partial; its missing chunks are zero in the box and never transformed or written back)
+  auto chv = [&](int cb) { return cb * BK + xch * 8 < Cin; };
   auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb) {
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
+    const bool cv = chv(cb);
 #pragma unroll
     for (int k = 0; k < NBX; ++k)
-      xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (BOX_ABLATE & 1) ? 0u : xo[k], coff, 0));
+      xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rs, (BOX_ABLATE & 1) ? 0u : (cv ? xo[k] : 0x80000000u), coff, 0));
     if constexpr (PRO == 3) {
 #pragma unroll
       for (int k = 0; k < NBX; ++k)
-        yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, xo[k], coff, 0));
+        yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, cv ? xo[k] : 0x80000000u,
+                                                                                coff, 0));
     }
   };
   auto yrsrc = [&](const TileInfo& bt, bool valid) {
@@ -252,14 +258,15 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // block (the loads have landed there: tap 3's stage was fired after them), so the VALU work
   // interleaves with the MFMA phases; (3,1,1): right before the store.
   auto box_xform = [&](int cb) {
-    const int c0 = cb * BK + xch * 8;
+    const int c0 = min(cb * BK + xch * 8, Cin - 8);  // (clamped: a missing chunk is not transformed)
+    const bool cv = chv(cb);
     if constexpr (PRO == 1 || PRO == 2) {
       float sc[8], sh[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) { sc[u] = pro_lds[c0 + u]; sh[u] = pro_lds[Cin + c0 + u]; }
 #pragma unroll
       for (int k = 0; k < NBX; ++k) {
-        if (xo[k] != 0x80000000u) {
+        if (cv && xo[k] != 0x80000000u) {
           float f[8];
           unpack8(xr[k], f);
 #pragma unroll
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
 #pragma unroll
       for (int k = 0; k < NBX; ++k) {
-        if (xo[k] != 0x80000000u) {  // padding rows stay zero (dy is zero-padded)
+        if (cv && xo[k] != 0x80000000u) {  // padding rows stay zero (dy is zero-padded)
           float d[8], yy[8];
           unpack8(xr[k], d);
           unpack8(yr[k], yy);
@@ -304,7 +311,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       const uint4 v = xr[k];
       *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
       if constexpr (PRO >= 2) {
-        bool own = n_tile == 0 && xo[k] != 0x80000000u;
+        bool own = n_tile == 0 && xo[k] != 0x80000000u && chv(cb);
         if constexpr (KS == 133) {
           const int j = xrow0 + 64 * k;
           own = own && j >= g.W1 + 1 && j <= bt.elast - bt.e0 + g.W1 + 1;
@@ -622,7 +629,10 @@ static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
   const int ks = p.KT * 100 + p.KH * 10 + p.KW;
   if (p.st != 1 || p.sh != 1 || p.sw != 1) return V4_UNSUPPORTED;
   if (p.To != p.T || p.Ho != p.H || p.Wo != p.W) return V4_UNSUPPORTED;
-  if (p.Cin % BX_BK || p.Kpad != p.KT * p.KH * p.KW * p.Cin) return V4_UNSUPPORTED;
+  // a partial last channel block reads weight columns past its tap's (times zero activations):
+  // the last tap's must stay inside the packed row (the SGPR stage offset is not range-checked)
+  const int ncb = (p.Cin + BX_BK - 1) / BX_BK;
+  if (p.Cin % 8 || p.Kpad < (p.KT * p.KH * p.KW - 1) * p.Cin + ncb * BX_BK) return V4_UNSUPPORTED;
   g.KS = ks;
   g.HW = p.H * p.W;
   g.fHW = make_fastdiv(g.HW);

@@ -70,7 +70,7 @@ int launch_fwd_v4(ConvParams& p, int bn, int impl, hipStream_t stream);
 bool fwd_v4_supported(const ConvParams& p, int bn, int impl);
 
 // box-tiled forward / dgrad (conv_box.hip, impl 14 / 15): stride-1 same-padded (1,3,3) / (3,1,1),
-// Cin % 64 == 0, N tiles 64 / 128 / 192. pro_ss: [4][Cin] BN constants of the input's producer
+// Cin % 8 == 0 (a partial last 64-channel block), N tiles 64 / 128 / 192. pro_ss: [4][Cin] BN constants of the input's producer
 // (z = relu(x * scale + shift) applied while staging) or null; pro_z: where z is also written
 // (the consumer's wgrad operand) or null. With pro.y / pro.coef (dgrad): x is dz of that BN and the
 // staged operand is its BN backward dy (written to pro.z).

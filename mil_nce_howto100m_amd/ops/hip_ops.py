@@ -195,7 +195,8 @@ _V4_IMPLS = tuple(int(v) for v in os.environ.get("MILNCE_V4_IMPLS", "8,9,10,11,1
 _V4_WIDE_M = (12, 13, 14, 15)  # 8-wave workgroups, one per CU (12 / 13 v4, 14 / 15 box-tiled)
 
 # Box-tiled forward / dgrad (csrc/conv_box.hip): stride-1 same-padded (1,3,3) / (3,1,1) convs over a
-# multiple of 64 channels; the tile's input box is staged once per 64-channel block for every tap.
+# multiple of 8 channels; the tile's input box is staged once per 64-channel block for every tap (a
+# partial last block is zero-filled: the tuner weighs that MFMA waste against the other variants).
 # 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (64 / 128 / 192). MILNCE_BOX=0 leaves them out.
 _BOX = os.environ.get("MILNCE_BOX", "1") != "0"
 _BOX_ROWS = 448
@@ -208,7 +209,9 @@ def _box_ok(bn: int, cin: int, kpad: int, impl: int, geo) -> bool:
     if not ((impl == 14 and bn in (64, 128)) or (impl == 15 and bn in (64, 128, 192))):
         return False
     T, H, W, k, pad = geo
-    if cin % 64 or kpad != k[0] * k[1] * k[2] * cin:
+    # a partial last 64-channel block is zero-filled; its weight stage (past the tap's columns) must
+    # stay inside the packed row
+    if cin % 8 or kpad < (k[0] * k[1] * k[2] - 1) * cin + _ceil(cin, 64) * 64:
         return False
     if tuple(k) == (1, 3, 3) and tuple(pad) == (0, 1, 1):
         span = 255 + (255 // W + 1) + (255 // (H * W) + 1) * (W + 2) + 2 * (W + 1) + 3
@@ -583,7 +586,7 @@ _BNBWD_FUSE = os.environ.get("MILNCE_BNBWD_FUSE", "1") != "0"
 def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
     """The dgrad can take over this layer's BN-backward apply (``conv_dgrad_bnbwd``)."""
     return (_BNBWD_FUSE and _PRO_FUSE and plan.d_impl in _BOX_IMPLS and plan.d_bn <= 128 and _box_geo(plan) is not None
-            and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 64 == 0)
+            and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 8 == 0)
 
 
 _FUSE_BN_BWD = True

@@ -31,6 +31,11 @@ CASES = [
     (2, 4, 13, 13, 128, 64, (3, 1, 1), (1, 0, 0)),
     (2, 16, 5, 5, 64, 128, (3, 1, 1), (1, 0, 0)),
     (2, 8, 25, 25, 256, 192, (3, 1, 1), (1, 0, 0)),
+    # channel counts that are not multiples of 64: a partial (zero-filled) last channel block
+    (2, 8, 25, 25, 96, 128, (1, 3, 3), (0, 1, 1)),
+    (3, 4, 13, 13, 224, 224, (3, 1, 1), (1, 0, 0)),
+    (2, 4, 13, 13, 24, 64, (1, 3, 3), (0, 1, 1)),
+    (2, 4, 13, 13, 48, 48, (3, 1, 1), (1, 0, 0)),
 ]
 
 
@@ -53,7 +58,7 @@ def test_conv_box_matches_reference(case):
     geo = h._box_geo(plan)
     fw = [i for i in (14, 15) if h._box_ok(plan.bn, cin, plan.Kpad, i, geo)]
     dg = [i for i in (14, 15) if h._box_ok(plan.d_bn, cout, plan.d_Kpad, i, geo)]
-    assert fw, (plan.bn, geo)
+    assert fw or dg, (plan.bn, plan.d_bn, geo)
 
     def run(fi, di, grid_wgs):
         plan.impl, plan.d_impl = fi, di
@@ -85,7 +90,8 @@ def test_conv_box_matches_reference(case):
 
 
 @pytest.mark.parametrize("shape,cin,cmid,k", [((2, 8, 50, 50), 64, 192, (3, 3, 3)),
-                                             ((3, 8, 11, 13), 128, 128, (3, 3, 3))])
+                                             ((3, 8, 11, 13), 128, 128, (3, 3, 3)),
+                                             ((3, 4, 13, 13), 112, 224, (3, 3, 3))])
 def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
     """A separable S3D-G unit (spatial conv -> BN -> ReLU -> temporal conv) with the spatial BN +
     ReLU applied inside the temporal conv's box kernel (hip_ops "pro" placeholders, csrc/conv_box.hip
