@@ -552,15 +552,18 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
 
 
 def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn, y: torch.Tensor,
-                     ss: torch.Tensor, coef: torch.Tensor, dy_out: torch.Tensor) -> torch.Tensor:
+                     ss: torch.Tensor, coef: torch.Tensor, dy_out: torch.Tensor, impl: int = 0,
+                     grid: int = 0, dx: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dX of a conv whose output went through BN -> ReLU, from dz (the gradient of the ReLU output):
     the box-tiled dgrad stages that BN's backward dy = k0 * (dz * mask - k1 - xhat * k2) itself
     (y / ss: the BN's raw conv output and constants, coef: milnce_bn_bwd_finalize output) and writes
     dy to ``dy_out`` for the wgrad, so the separate bn_bwd_apply pass (read dz and y, write dy) and
     the dgrad's read of dy become its reads of dz and y. Requires a box-tiled ``plan.d_impl``."""
     kt, kh, kw = plan.k
-    dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dz.device)
+    if dx is None:
+        dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dz.device)
     pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
+    impl, grid = impl or plan.d_impl, grid or plan.d_grid_m
     part = None
     if producer_bn is not None:
         md = plan.B * plan.T * plan.H * plan.W
@@ -569,10 +572,45 @@ def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, produce
          ptr(producer_bn[0]) if part is not None else None, ptr(producer_bn[1]) if part is not None else None,
          producer_bn[2] if part is not None else 0, ptr(y), ptr(ss), ptr(coef), ptr(dy_out),
          plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, pt, ph, pw, plan.d_Kpad, plan.d_Npad,
-         plan.d_bn, plan.d_grid_m, plan.d_impl, stream())
+         plan.d_bn, grid, impl, stream())
     if part is not None:
-        attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
+        attach_bn_partials(dx, part, grid, plan.d_Npad)
     return dx
+
+
+def _tune_dgrad_bnbwd(plan: ConvPlan, dz, weight, y, ss, gamma, part, nparts, ps, x_bn, training) -> None:
+    """Tune a dgrad whose BN-backward apply the box kernel can take over on what each variant
+    costs here: the fused dgrad (PRO 3) for box-tiled variants, bn_bwd apply pass + dgrad for the
+    others. All runs write scratch buffers (the BN gradients are accumulated in place)."""
+    C, dev = plan.Cout, dz.device
+    wd = _pack(weight, plan, 1)
+    coef = torch.empty((3 * C,), dtype=F32, device=dev)
+    dg, db = torch.empty((C,), dtype=F32, device=dev), torch.empty((C,), dtype=F32, device=dev)
+    call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(plan.M), ptr(gamma), ptr(ss), ptr(dg), ptr(db),
+         ptr(coef), 0, int(training), stream())
+    dy_s = torch.empty_like(y)
+    dx_s = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dev)
+    md = plan.B * plan.T * plan.H * plan.W
+    part_s = (torch.empty((_stats_rows(md, plan.d_Npad, plan.d_bn) * 2 * plan.d_Npad,), dtype=F32, device=dev)
+              if x_bn is not None else None)
+    kt, kh, kw = plan.k
+    pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
+
+    def launch(impl, grid):
+        if impl in _BOX_IMPLS and plan.d_bn <= 128:
+            conv_dgrad_bnbwd(dz, wd, plan, x_bn, y, ss, coef, dy_s, impl, grid, dx_s)
+            return
+        call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps, 1,
+             ptr(dg), ptr(db), ptr(coef), ptr(dy_s), C, 0, int(training), stream())
+        call("milnce_conv_fwd", ptr(dy_s), 0, ptr(wd), ptr(dx_s), ptr(part_s),
+             ptr(x_bn[0]) if part_s is not None else None, ptr(x_bn[1]) if part_s is not None else None,
+             x_bn[2] if part_s is not None else 0,
+             plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
+             plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
+
+    plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
+                                                              _box_geo(plan)),
+                                           md, plan.d_Npad, plan.d_bn)
 
 
 # MILNCE_BNBWD_FUSE=0 disables. First version measured slower in the step (conv_2c spatial dgrad
@@ -1049,6 +1087,9 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
         return None, dw, dgamma, dbeta
     dy = torch.empty_like(y)
     dx = None
+    if (lazy is None and fused is not None and ctx.needs_input_grad[0] and plan.d_impl == 0 and _BNBWD_FUSE
+            and _PRO_FUSE and _box_geo(plan) is not None and dz.dtype == BF16 and plan.Cout % 8 == 0):
+        _tune_dgrad_bnbwd(plan, dz, weight, y, ss, gamma, part, nparts, ps, ctx.x_bn, ctx.training)
     if lazy is None and fused is not None and ctx.needs_input_grad[0] and _bnbwd_fusable(plan, dz):
         # BN-backward apply inside the dgrad's staging (dy written there for the wgrad)
         call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(plan.M), ptr(gamma), ptr(ss), ptr(dgamma),
