@@ -2053,16 +2053,18 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 
 // Forward whose input x is the raw conv output of a BN layer: z = relu(x * scale + shift) (pro_ss
 // = that layer's [4][Cin] mean / invstd / scale / shift) is applied while the box-tiled kernel
-// stages its input, and written to pro_z (the consumer's wgrad operand; null: not needed).
+// stages its input, and written to pro_z (dense; the consumer's wgrad operand; null: not needed).
+// x_ld: x's row stride in elements (x may be a channel slice of a concatenated conv output).
 // Box-tiled variants only (impl 14 / 15); anything else returns V4_UNSUPPORTED.
-MILNCE_API int milnce_conv_fwd_pro(const void* x, const void* w, void* y, float* stats, const float* pro_ss,
-                                   void* pro_z, int B, int T, int H, int W, int Cin, int Cout, int KT, int KH,
-                                   int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy, int bn, int grid_m,
-                                   int impl, hipStream_t stream) {
+MILNCE_API int milnce_conv_fwd_pro(const void* x, int x_ld, const void* w, void* y, float* stats,
+                                   const float* pro_ss, void* pro_z, int B, int T, int H, int W, int Cin, int Cout,
+                                   int KT, int KH, int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy,
+                                   int bn, int grid_m, int impl, hipStream_t stream) {
   if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
   BoxPro pro;
   pro.ss = pro_ss;
   pro.z = pro_z;
+  pro.xld = x_ld;
   return conv_fwd_impl(x, 0, w, y, stats, nullptr, nullptr, 0, B, T, H, W, Cin, Cout, KT, KH, KW, 1, 1, 1, pt, ph,
                        pw, Kpad, Npad, ldy, bn, 64, grid_m, 0, impl, pro, stream);
 }

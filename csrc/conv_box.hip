@@ -65,6 +65,9 @@ struct BoxGeo {
   // * xhat)): the staged operand is dy = k0 * (dz * mask - k1 - xhat * k2)
   const bf16_t* pro_y;
   const float* pro_coef;
+  int xld;              // row stride of x in elements (Cin, or the channel count of a concatenated
+                        // tensor x is a channel slice of); pro_z / pro_y are dense (stride Cin)
+  long long zbytes;     // bytes of the dense pro_z / pro_y tensors
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -164,9 +167,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // ---- tile geometry ----
   const int xch = tid & 7, xrow0 = tid >> 3;  // box staging: chunk, first row (rows xrow0 + 64 k)
   struct TileInfo {
-    long long xbase;     // byte offset of the tile's input base
+    long long xbase;     // byte offset of the tile's input base (rows of xld elements)
+    long long zbase;     // byte offset of the same rows in the dense pro_z / pro_y
     long long ybase;     // element offset of the tile's output base row
-    uint32_t xnrec;
+    uint32_t xnrec, znrec;
     int e0, elast, m0;   // 133: extended index of the first / last output row, first row
     int b, p0;           // 311
   };
@@ -186,7 +190,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       ti.e0 = ext(m0);
       ti.elast = ext(ml);
       const int qlo = (int)fdiv((uint32_t)max(0, ti.e0 - g.W1 - 1), g.fPL);
-      ti.xbase = (long long)qlo * g.HW * Cin * 2;
+      ti.xbase = (long long)qlo * g.HW * g.xld * 2;
+      ti.zbase = (long long)qlo * g.HW * Cin * 2;
       ti.ybase = (long long)m0 * p.ldy;
       ti.b = qlo;
       ti.p0 = 0;
@@ -195,16 +200,19 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       const int pb = m_tile - (int)b * g.tpc;
       ti.b = (int)b;
       ti.p0 = pb * g.P;
-      ti.xbase = (long long)b * p.T * g.HW * Cin * 2;
+      ti.xbase = (long long)b * p.T * g.HW * g.xld * 2;
+      ti.zbase = (long long)b * p.T * g.HW * Cin * 2;
       ti.ybase = (long long)b * p.T * g.HW * p.ldy;
       ti.m0 = ti.e0 = ti.elast = 0;
     }
     const long long remain = p.x_total_bytes - ti.xbase;
     ti.xnrec = remain > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)(remain > 0 ? remain : 0);
+    const long long zrem = g.zbytes - ti.zbase;
+    ti.znrec = zrem > 0x7FFFFFF0LL ? 0x7FFFFFF0u : (uint32_t)(zrem > 0 ? zrem : 0);
     return ti;
   };
-  // byte offset (relative to the tile's xbase, without the channel block) of box row j, or
-  // 0x80000000 (reads zero) for padding / out-of-range rows
+  // input row index of box row j relative to the tile's first row (xbase / zbase), or 0x80000000
+  // (reads zero) for padding / out-of-range rows
   auto box_off = [&](const TileInfo& ti, int j) -> uint32_t {
     if constexpr (KS == 133) {
       const int e = ti.e0 - g.W1 - 1 + j;
@@ -215,12 +223,12 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       const int ww = r - (int)hh * g.W1;
       if (hh == 0 || ww == 0 || (int)q >= p.M / g.HW) return 0x80000000u;
       const int qrel = (int)q - ti.b;
-      return (uint32_t)((((long long)qrel * p.H + (int)hh - 1) * p.W + ww - 1) * Cin * 2 + xch * 16);
+      return (uint32_t)(((long long)qrel * p.H + (int)hh - 1) * p.W + ww - 1);
     } else {
       const int tp = (int)fdiv((uint32_t)j, g.fP), jj = j - tp * g.P;
       const int t_in = tp - 1, pos = ti.p0 + jj;
       if (t_in < 0 || t_in >= p.T || pos >= g.HW || j >= (p.T + 2) * g.P) return 0x80000000u;
-      return (uint32_t)(((long long)t_in * g.HW + pos) * Cin * 2 + xch * 16);
+      return (uint32_t)((long long)t_in * g.HW + pos);
     }
   };
 
@@ -231,23 +239,27 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // this thread's chunk of channel block cb exists (Cin not a multiple of 64: the last block is
   // partial; its missing chunks are zero in the box and never transformed or written back)
   auto chv = [&](int cb) { return cb * BK + xch * 8 < Cin; };
+  // byte offsets of a box row (row index, or the out-of-range marker) in x and in the dense tensors
+  const uint32_t xrow_bytes = (uint32_t)g.xld * 2, zrow_bytes = (uint32_t)Cin * 2;
+  auto xoff = [&](uint32_t r) { return r == 0x80000000u ? r : r * xrow_bytes + (uint32_t)xch * 16; };
+  auto zoff = [&](uint32_t r) { return r == 0x80000000u ? r : r * zrow_bytes + (uint32_t)xch * 16; };
   auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb) {
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
     const bool cv = chv(cb);
 #pragma unroll
     for (int k = 0; k < NBX; ++k)
       xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                            rs, (BOX_ABLATE & 1) ? 0u : (cv ? xo[k] : 0x80000000u), coff, 0));
+                                            rs, (BOX_ABLATE & 1) ? 0u : (cv ? xoff(xo[k]) : 0x80000000u), coff, 0));
     if constexpr (PRO == 3) {
 #pragma unroll
       for (int k = 0; k < NBX; ++k)
-        yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, cv ? xo[k] : 0x80000000u,
+        yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, cv ? zoff(xo[k]) : 0x80000000u,
                                                                                 coff, 0));
     }
   };
   auto yrsrc = [&](const TileInfo& bt, bool valid) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.pro_y + bt.xbase), (short)0,
-                                             (int)(valid ? bt.xnrec : 0u), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.pro_y + bt.zbase), (short)0,
+                                             (int)(valid ? bt.znrec : 0u), 0x00020000);
   };
   // PRO 2: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
@@ -317,14 +329,14 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           own = own && j >= g.W1 + 1 && j <= bt.elast - bt.e0 + g.W1 + 1;
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
-                                               zs, own ? xo[k] : 0x80000000u,
+                                               zs, own ? zoff(xo[k]) : 0x80000000u,
                                                __builtin_amdgcn_readfirstlane(cb * BK * 2), 0);
       }
     }
   };
   auto zrsrc = [&](const TileInfo& bt, bool valid) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.pro_z + bt.xbase), (short)0,
-                                             (int)(valid ? bt.xnrec : 0u), 0x00020000);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.pro_z + bt.zbase), (short)0,
+                                             (int)(valid ? bt.znrec : 0u), 0x00020000);
   };
 
   // ---- per-lane fragment rows of a tile ----
@@ -732,6 +744,14 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
   g.pro_z = (bf16_t*)pro.z;
   g.pro_y = (const bf16_t*)pro.y;
   g.pro_coef = pro.coef;
+  g.xld = pro.xld > 0 ? pro.xld : p.Cin;
+  g.zbytes = (long long)(p.M / (p.To * p.Ho * p.Wo)) * p.T * p.H * p.W * p.Cin * 2;
+  if (g.xld != p.Cin) {
+    if (g.xld < p.Cin || g.xld % 8) return V4_UNSUPPORTED;
+    // x is a channel slice of a wider tensor: its last row ends Cin (not xld) elements in
+    const long long rows = (long long)(p.M / (p.To * p.Ho * p.Wo)) * p.T * p.H * p.W;
+    p.x_total_bytes = ((rows - 1) * g.xld + p.Cin) * 2;
+  }
   p.num_m_tiles = ntiles;
   if (impl == 14) {
     if (bn == 64) return launch_box_bn<64, 16>(p, g, stream);

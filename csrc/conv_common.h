@@ -79,6 +79,7 @@ struct BoxPro {
   void* z = nullptr;            // transformed input written here (null: not needed)
   const void* y = nullptr;      // dgrad BN-backward prologue: the BN's raw conv output
   const float* coef = nullptr;  //   and its backward coefficients [3][Cin]
+  int xld = 0;                  // row stride of x in elements (0: Cin)
 };
 int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream_t stream);
 bool fwd_box_supported(const ConvParams& p, int bn, int impl);

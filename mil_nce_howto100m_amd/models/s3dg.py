@@ -111,8 +111,10 @@ class InceptionBlock(nn.Module):
         # branches 0, 1a, 2a are 1x1x1 units on the same input: one fused GEMM on GPU
         # (and the branch-3 pool reads it too: one fused op owning every read of x)
         units = (self.conv_b0, self.conv_b1_a, self.conv_b2_a)
+        # z1 / z2 feed only the separable units: their BN + ReLU is applied by those convs' kernels
         (z0, z1, z2), s0, pooled = ops.inception_head(x, [u.conv1.weight for u in units],
-                                                      [u.bn1 for u in units], self.training, want_gsum0=g)
+                                                      [u.bn1 for u in units], self.training, want_gsum0=g,
+                                                      lazy_out=(False, True, True))
         b0 = (z0, s0)
         b1 = self.conv_b1_b(z1, want_gsum=g)
         b2 = self.conv_b2_b(z2, want_gsum=g)

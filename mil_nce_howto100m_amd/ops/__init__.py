@@ -88,12 +88,13 @@ def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = Fa
     return [aten.conv_bn_relu(x, w, bn, (1, 1, 1), (0, 0, 0), training) for w, bn in zip(weights, bns)], None
 
 
-def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False):
+def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False, lazy_out=()):
     """Everything an Inception block computes directly from its input: the 1x1x1 conv-BN-ReLU
     units of branches 0/1a/2a and the branch-3 stride-1 max pool. Returns
-    ([z0, z1a, z2a], gating sum of z0 or None, pooled x); one fused op on GPU."""
+    ([z0, z1a, z2a], gating sum of z0 or None, pooled x); one fused op on GPU. ``lazy_out[i]``
+    (GPU): z_i feeds only a ``conv_bn_relu``, which may apply its BN + ReLU (placeholder output)."""
     if use_hip(x):
-        out = _hip().inception_head(x, weights, bns, training, want_gsum0)
+        out = _hip().inception_head(x, weights, bns, training, want_gsum0, lazy_out)
         n = len(weights)
         return list(out[:n]), (out[n] if want_gsum0 else None), out[-1]
     zs = [aten.conv_bn_relu(x, w, bn, (1, 1, 1), (0, 0, 0), training) for w, bn in zip(weights, bns)]

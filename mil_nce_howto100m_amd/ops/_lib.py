@@ -22,7 +22,7 @@ P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
 
 SIGNATURES: Dict[str, list] = {
     "milnce_conv_fwd": [P, I, P, P, P, P, P, I] + [I] * 6 + [I] * 9 + [I] * 8 + [P],
-    "milnce_conv_fwd_pro": [P, P, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 6 + [P],
+    "milnce_conv_fwd_pro": [P, I, P, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 6 + [P],
     "milnce_conv_dgrad_bnbwd": [P, P, P, P, P, P, I, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 5 + [P],
     "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 8 + [P],
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],

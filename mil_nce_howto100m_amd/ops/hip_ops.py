@@ -472,13 +472,13 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     if pro is not None:
         z_out = pro[0]
         yp, ssp, ldp = x._milnce_bn
-        fusable = ldp == plan.Cin and x.shape[-1] == plan.Cin
+        fusable = x.shape[-1] == plan.Cin and ldp % 8 == 0  # y may be a channel slice (row stride ldp)
         zbuf = z_out if z_out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
         thw_in = plan.T * plan.H * plan.W
 
         def launch_pro(impl, grid):
             if impl in _BOX_IMPLS and fusable:
-                call("milnce_conv_fwd_pro", ptr(yp), ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
+                call("milnce_conv_fwd_pro", ptr(yp), ldp, ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
                      plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
                      plan.Cout, plan.bn, grid, impl, stream())
             else:  # the variant needs z in memory: its timing includes the BN-apply pass
@@ -1310,7 +1310,7 @@ class _Conv1x1GroupBNReLU(torch.autograd.Function):
         return (dx, *rest)
 
 
-def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
+def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, lazy_out=()):
     """Forward of the fused 1x1 group (see ``_Conv1x1GroupBNReLU``); ``extra_saved`` tensors are
     appended to the saved tensors (read back by ``_group_backward`` callers)."""
     ws = args[:n]
@@ -1336,11 +1336,14 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved):
              float(hyper[i][1]), int(training), ptr(ss), stream())
         g = _zeros_f32((plan.B, c), dev) if (i == 0 and want_gsum0) else None
         ysl = y2[:, off:off + c]
-        lazy = g is not None and _LAZY_GATE_Z
-        z = (_lazy_z((plan.B, plan.To, plan.Ho, plan.Wo, c), dev, (ysl, ss, ctot)) if lazy
-             else torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, c), dtype=BF16, device=dev))
-        call("milnce_bn_relu_apply", ptr(ysl), ctot, None if lazy else ptr(z), c, ptr(ss), c, plan.B, thw, ptr(g),
-             stream())
+        zshape = (plan.B, plan.To, plan.Ho, plan.Wo, c)
+        if g is None and i < len(lazy_out) and lazy_out[i] and _PRO_FUSE:
+            z = _pro_z(zshape, dev, (ysl, ss, ctot))  # applied by the consuming conv (a channel slice)
+        else:
+            lazy = g is not None and _LAZY_GATE_Z
+            z = _lazy_z(zshape, dev, (ysl, ss, ctot)) if lazy else torch.empty(zshape, dtype=BF16, device=dev)
+            call("milnce_bn_relu_apply", ptr(ysl), ctot, None if lazy else ptr(z), c, ptr(ss), c, plan.B, thw,
+                 ptr(g), stream())
         z._milnce_bn = (ysl, ss, ctot)
         zs.append(z)
         sss.append(ss)
@@ -1443,13 +1446,13 @@ class _InceptionHead(torch.autograd.Function):
     Returns (*branch outputs, [gating sum of branch 0], pooled x)."""
 
     @staticmethod
-    def forward(ctx, x, n, training, want_gsum0, hyper, *args):
+    def forward(ctx, x, n, training, want_gsum0, hyper, lazy_out, *args):
         B, T, H, W, C = x.shape
         pooled = torch.empty_like(x)
         arg = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
         geo = [B, T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0]
         call("milnce_maxpool_fwd", ptr(x), ptr(pooled), ptr(arg), *geo, stream())
-        outs = _group_forward(ctx, x, n, training, want_gsum0, hyper, args, (arg,))
+        outs = _group_forward(ctx, x, n, training, want_gsum0, hyper, args, (arg,), lazy_out)
         ctx.x_gate = bool(getattr(x, "_milnce_gate", False))
         return (*outs, pooled)
 
@@ -1460,6 +1463,7 @@ class _InceptionHead(torch.autograd.Function):
         x = saved[0]
         dpooled = grads[-1]
         dx1, rest = _group_backward(ctx, grads[:-1], saved[:-1])
+        rest = (None,) + tuple(rest)  # lazy_out
         B, T, H, W, C = x.shape
         if dpooled is None or not ctx.needs_input_grad[0]:
             return (dx1, *rest)
@@ -1476,8 +1480,9 @@ class _InceptionHead(torch.autograd.Function):
 _FUSE_HEAD = os.environ.get("MILNCE_FUSE_INCEPTION_HEAD", "1") != "0"
 
 
-def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False):
-    """Fused 1x1 group + branch-3 pool on the Inception input; see ``_InceptionHead``."""
+def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False, lazy_out=()):
+    """Fused 1x1 group + branch-3 pool on the Inception input; see ``_InceptionHead``.
+    ``lazy_out[i]``: branch i's output feeds only a conv that may apply its BN + ReLU itself."""
     if x.dtype != BF16:
         x = x.to(BF16)
     x = x.contiguous()
@@ -1489,7 +1494,8 @@ def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False):
     for bn in bns:
         args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
     hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
-    return _InceptionHead.apply(x, len(weights), bool(training), bool(want_gsum0), hyper, *args)
+    return _InceptionHead.apply(x, len(weights), bool(training), bool(want_gsum0), hyper,
+                                tuple(bool(v) for v in lazy_out), *args)
 
 
 def take_gate_sums(dout: torch.Tensor):

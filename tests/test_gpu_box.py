@@ -138,3 +138,40 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
         assert torch.equal(res[(False, "ng")], res[(True, "ng")])
     finally:
         h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
+
+
+def test_inception_head_prologue_fusion():
+    """An Inception block whose head outputs z1a / z2a (channel slices of the fused 1x1 GEMM output,
+    row stride = all three branches) are applied by the separable units' box kernels (x_ld != Cin)
+    matches the unfused block: output, input gradient and every parameter gradient, up to the
+    float-atomic order of the gating sums."""
+    import copy
+    from mil_nce_howto100m_amd.models.s3dg import InceptionBlock
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(7)
+    shape = (2, 8, 11, 11)
+    blk = InceptionBlock(192, 64, 96, 128, 16, 32, 32).cuda().train()
+    x = torch.randn(*shape, 192, device=DEV).to(torch.bfloat16)
+    g = torch.randn(*shape, blk.output_dim, device=DEV).to(torch.bfloat16)
+    old, old_b = h._PRO_FUSE, h._BNBWD_FUSE
+    res = {}
+    try:
+        for fuse in (False, True):
+            h._PRO_FUSE = h._BNBWD_FUSE = fuse
+            b = copy.deepcopy(blk)
+            xi = x.clone().requires_grad_(True)
+            b(xi).sum().backward()  # tune
+            for cin, cout in ((96, 128), (16, 32)):  # the spatial convs reading z1a / z2a: box-tiled
+                plan = h.conv_plan(tuple(shape) + (cin,), (cout, cin, 1, 3, 3), (1, 1, 1), (0, 1, 1))
+                plan.impl = 15
+            xi.grad = None
+            b.zero_grad()
+            out = b(xi)
+            out.backward(g)
+            res[fuse] = (out.detach().float(), xi.grad.float(), {n: p.grad.clone() for n, p in b.named_parameters()})
+        (o0, x0, g0), (o1, x1, g1) = res[False], res[True]
+        assert _rel(o1, o0) < 2e-3 and _rel(x1, x0) < 5e-3
+        for n in g0:
+            assert _rel(g1[n], g0[n]) < 1e-2, n
+    finally:
+        h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
