@@ -833,9 +833,10 @@ def _wgrad_tiles_for(Cout: int, tk: int) -> List[int]:
 _W_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_W_OCCS", "4,2,8,16").split(","))
 _HALO_WGRAD = os.environ.get("MILNCE_HALO_WGRAD", "1") != "0"
 _HALO_KERNELS = ((1, 3, 3), (3, 1, 1))
-# (3,1,1) is implemented too but measures slower than the im2col kernel (3 taps amortise the
-# per-box cost less: tools/halo_bench.py), so the autotuner only offers the spatial one
-_HALO_TUNED = ((1, 3, 3),)
+# The (3,1,1) kernel measured slower than the im2col kernel in round 2 (3 taps amortise the
+# per-box cost less: tools/halo_bench.py); it is in the tuner's candidates now (channel chunks of
+# 64 and 128), which keeps the im2col kernel where that still wins. MILNCE_HALO_T311=0: spatial only
+_HALO_TUNED = ((1, 3, 3), (3, 1, 1)) if os.environ.get("MILNCE_HALO_T311", "1") == "1" else ((1, 3, 3),)
 
 
 def _halo_wgrad_supported(plan: ConvPlan, x: torch.Tensor) -> bool:
@@ -957,6 +958,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                             cands.append((tn, impl, occ, tk))
             if _halo_wgrad_ok(plan, x):
                 cands += [(64, 164, occ, 0) for occ in _HALO_OCCS]
+                if plan.k == (3, 1, 1) and plan.Cin % 128 == 0:  # temporal boxes also take 128-channel chunks
+                    cands += [(64, 228, occ, 0) for occ in _HALO_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4, plan.w_tk)
