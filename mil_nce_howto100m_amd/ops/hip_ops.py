@@ -833,10 +833,10 @@ def _wgrad_tiles_for(Cout: int, tk: int) -> List[int]:
 _W_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_W_OCCS", "4,2,8,16").split(","))
 _HALO_WGRAD = os.environ.get("MILNCE_HALO_WGRAD", "1") != "0"
 _HALO_KERNELS = ((1, 3, 3), (3, 1, 1))
-# The (3,1,1) kernel measured slower than the im2col kernel in round 2 (3 taps amortise the
-# per-box cost less: tools/halo_bench.py); it is in the tuner's candidates now (channel chunks of
-# 64 and 128), which keeps the im2col kernel where that still wins. MILNCE_HALO_T311=0: spatial only
-_HALO_TUNED = ((1, 3, 3), (3, 1, 1)) if os.environ.get("MILNCE_HALO_T311", "1") == "1" else ((1, 3, 3),)
+# The (3,1,1) kernel measured slower than the im2col kernel (3 taps amortise the per-box cost less:
+# tools/halo_bench.py); offered to the tuner (channel chunks of 64 and 128) with MILNCE_HALO_T311=1,
+# it was never picked in the step (same-box A/B round 3: 4271 / 4278 vs 4277 / 4277 pairs/s)
+_HALO_TUNED = ((1, 3, 3), (3, 1, 1)) if os.environ.get("MILNCE_HALO_T311", "0") == "1" else ((1, 3, 3),)
 
 
 def _halo_wgrad_supported(plan: ConvPlan, x: torch.Tensor) -> bool:
