@@ -47,7 +47,8 @@ static constexpr int BX_STAGES = 3;
 
 // Diagnostic ablations (debug libraries only, tools/gpu/box_ablate.sh; results are garbage):
 // bit 0 box loads read one fixed chunk (L1-hot), bit 1 no weight DMA, bit 2 no epilogue stores /
-// statistics, bit 3 no epilogue at all (no staging either).
+// statistics, bit 3 no epilogue at all (no staging either), bit 4 epilogue stores issued out of
+// range (no memory traffic), bit 5 no forward statistics (stores kept).
 #ifndef BOX_ABLATE
 #define BOX_ABLATE 0
 #endif
@@ -578,9 +579,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           const int n = n0 + cc * 8;
           const bool ok = (yo != 0x80000000u) & (n < p.Cout) & !(BOX_ABLATE & 4);
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, dv),
-                                                 yrs, ok ? yo + (uint32_t)n * 2 : 0x80000000u, 0, 0);
+                                                 yrs, (ok && !(BOX_ABLATE & 16)) ? yo + (uint32_t)n * 2 : 0x80000000u,
+                                                 0, 0);
           if constexpr (EPI == 1) {
-            if (ok) {
+            if (ok && !(BOX_ABLATE & 32)) {
               float d8[8];
               unpack8(dv, d8);
 #pragma unroll
