@@ -88,7 +88,10 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
 // ---------------------------------------------------------------------------------------
 // z = relu(y*scale + shift). Grid (splits, B): block handles rows of one clip so the gating
 // channel sums can be reduced in LDS and committed with one atomic per channel per block.
-__global__ __launch_bounds__(256) void bn_relu_apply_kernel(
+// WRITE = false (bn_relu_gsum_kernel): the SelfGating channel sums only, a read-only reduction
+// (the lazy gate inputs' z is applied by the gate_scale pass / the consumer instead).
+template <bool WRITE>
+__device__ __forceinline__ void bn_relu_apply_body(
     const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
     int C, int rows_per_b, int rows_per_block, float* __restrict__ gsum) {
   __shared__ float red[256 * 8];
@@ -128,7 +131,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
           f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
           acc[k] += f[k];
         }
-        if (z != nullptr) *(uint4*)(z + (base + r) * ldz + c0) = pack8(f);  // z == null: gating sums only
+        if constexpr (WRITE) *(uint4*)(z + (base + r) * ldz + c0) = pack8(f);
       }
     }
   }
@@ -145,6 +148,18 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
       atomicAdd(gsum + (long long)b * C + c0 + k, s);
     }
   }
+}
+
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(
+    const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
+    int C, int rows_per_b, int rows_per_block, float* __restrict__ gsum) {
+  bn_relu_apply_body<true>(y, ldy, z, ldz, ss, C, rows_per_b, rows_per_block, gsum);
+}
+
+__global__ __launch_bounds__(256) void bn_relu_gsum_kernel(
+    const bf16_t* __restrict__ y, int ldy, const float* __restrict__ ss, int C, int rows_per_b,
+    int rows_per_block, float* __restrict__ gsum) {
+  bn_relu_apply_body<false>(y, ldy, nullptr, 0, ss, C, rows_per_b, rows_per_block, gsum);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -300,8 +315,14 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
   // enough blocks to fill 256 CUs instead of a couple of long serial blocks per CU.
   const int splits = pick_splits(rows_per_b, 4 * BN_U * (256 / (C / 8)));
   const int rpb = (rows_per_b + splits - 1) / splits;
-  hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy,
-                     (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, gsum);
+  if (z == nullptr) {  // gating sums only
+    if (gsum == nullptr) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_relu_gsum_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy, ss, C,
+                       rows_per_b, rpb, gsum);
+  } else {
+    hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy,
+                       (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, gsum);
+  }
   return (int)hipGetLastError();
 }
 

@@ -33,6 +33,7 @@
 // slot sets), so shifted taps stay conflict-free (the w-wrap inside a fragment can cost one).
 #include "conv_common.h"
 
+#include <algorithm>
 #include <type_traits>
 
 static constexpr int BX_BM = 256;        // output rows per tile: 4 waves along M x 64 rows
@@ -69,6 +70,7 @@ struct BoxGeo {
   int xld;              // row stride of x in elements (Cin, or the channel count of a concatenated
                         // tensor x is a channel slice of); pro_z / pro_y are dense (stride Cin)
   long long zbytes;     // bytes of the dense pro_z / pro_y tensors
+  int prefire;          // fire a tile's stage 2 in the previous tile's epilogue (MILNCE_BOX_PREFIRE)
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -87,7 +89,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int KSTEPS = BK / (MF == 16 ? 32 : 16);
   constexpr int TAPS = KS == 133 ? 9 : 3;
   constexpr int CPR = BK / 8, RPI = 64 / CPR;  // B ring: 8 rows (1 KiB) per DMA instruction
-  constexpr int B_INST = BN / RPI / NWAVES;    // DMA pieces per wave per stage
+  // weight stage rows: BN rounded up to the 64 rows one DMA round of 8 waves covers (N tiles of
+  // 96 / 160 load 128 / 192 rows; the extra rows are never read)
+  constexpr int BNR = (BN + 63) / 64 * 64;
+  constexpr int B_INST = BNR / RPI / NWAVES;   // DMA pieces per wave per stage
   constexpr int NDMA = B_INST;
   constexpr int NBX = BX_NBX;
   // epilogue: column-owner pass over 128-row halves staged in the box region
@@ -100,8 +105,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int NBL = PRO == 3 ? 2 * NBX : NBX;  // box loads per wave (PRO 3: dz and y)
   static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
   static_assert(WN % MF == 0, "wave tile");
-  constexpr int STAGE_ELEMS = BN * BK;
-  static_assert(B_INST * RPI * NWAVES == BN, "DMA mapping");
+  constexpr int STAGE_ELEMS = BNR * BK;
+  static_assert(B_INST * RPI * NWAVES == BNR, "DMA mapping");
   static_assert(NST + ZC + NDMA + NBL <= 63, "vmcnt range");
   static_assert(PRO != 3 || BN <= 128, "PRO 3 registers");
 
@@ -360,8 +365,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         }
       } else {
         const int t = (int)fdiv((uint32_t)lr, g.fP), j = lr - t * g.P;
-        rb[i] = lr;
-        yo[i] = (ti.p0 + j < g.HW) ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2) : 0x80000000u;
+        const bool v = t < p.T && ti.p0 + j < g.HW;  // rows past T * P idle
+        rb[i] = t < p.T ? lr : 0;
+        yo[i] = v ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2) : 0x80000000u;
       }
     }
   };
@@ -426,23 +432,28 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         //     than stages up to cb*TAPS+2 -> waits at taps 1, 2
         //   * epilogue stores of the previous tile (NST) and, with PRO 2, the z stores of the
         //     box written after them (ZC), or of the box written at the end of the previous block:
-        //     younger than the first two stages of this block
+        //     younger than the first two stages of this block, and than the third on a tile after
+        //     the first (its stage 2 was fired in the previous epilogue, before the stores, so the
+        //     stores have three taps to drain instead of two)
+        const bool carried = cb == 0 && !first_tile && g.prefire;
         if (t == 0) {
-          if (cb == 0 && !first_tile) bx_wait<NDMA + NST + ZC>();
+          if (carried) bx_wait<2 * NDMA + NST + ZC>();
           else if (cb > 0) bx_wait<NDMA + ZC>();
           else bx_wait<NDMA>();
         } else if (t == 1) {
-          if (cb == 0 && !first_tile) bx_wait<NST + ZC + NDMA + NBL>();
+          if (carried) bx_wait<NST + ZC + NDMA + NBL>();
           else if (cb > 0) bx_wait<ZC + NDMA + NBL>();
           else bx_wait<NDMA + NBL>();
         } else if (t == 2) {
-          bx_wait<NBL + NDMA>();
+          if (carried) bx_wait<NST + ZC + NBL + NDMA>();
+          else bx_wait<NBL + NDMA>();
         } else {
           bx_wait<NDMA>();
         }
         ring_barrier();
-        // fire stage s + 2 (continuing into the next tile: the weights do not depend on the tile)
-        {
+        // fire stage s + 2 (continuing into the next tile: the weights do not depend on the tile;
+        // stage 2 of a carried tile is already in flight)
+        if (!(t == 0 && carried)) {
           int s2 = s + 2;
           if (s2 >= nst_tile) s2 -= nst_tile;
           if (s2 >= nst_tile) s2 = 0;  // nst_tile == 1 (not used by the supported shapes)
@@ -524,7 +535,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         if constexpr (KS == 133) {
           grow = min(ti.m0 + lr, p.M - 1);
         } else {
-          const int t = (int)fdiv((uint32_t)lr, g.fP), j = min(lr - t * g.P, g.HW - 1 - ti.p0);
+          const int t0 = (int)fdiv((uint32_t)lr, g.fP), t = min(t0, p.T - 1);
+          const int j = min(lr - t0 * g.P, g.HW - 1 - ti.p0);
           grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
         }
         const int n = min(n0 + cc * 8, p.Cout - 8);
@@ -552,6 +564,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         }
       }
       lds_barrier();
+      // every wave is past the tile's last MFMAs: the last stage's ring slot is free for the next
+      // tile's stage 2, fired ahead of the stores (see the waits at taps 0-2)
+      if (half == 0 && g.prefire) fire((gs + 2) % BX_STAGES, 2);
       {
         const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
         const int cc = tid % OCPR;
@@ -573,7 +588,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           } else {
             const int t = (int)fdiv((uint32_t)lr, g.fP), j = lr - t * g.P;
             grow = (long long)(ti.b * p.T + t) * g.HW + ti.p0 + j;
-            yo = (act && ti.p0 + j < g.HW) ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2)
+            yo = (act && t < p.T && ti.p0 + j < g.HW) ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2)
                                           : 0x80000000u;
           }
           const int n = n0 + cc * 8;
@@ -606,6 +621,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         }
       }
       lds_barrier();  // the half's rows are consumed before the region is rewritten
+    }
+    if constexpr ((BOX_ABLATE & 8) != 0) {
+      lds_barrier();
+      if (g.prefire) fire((gs + 2) % BX_STAGES, 2);
     }
     // the next tile's first box (its loads were issued at the last block's first tap)
     if (has_next) box_store(0, tn, zrs);
@@ -668,10 +687,12 @@ static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
     ntiles = (p.M + BX_BM - 1) / BX_BM;
   } else if (ks == 311) {
     if (p.pt != 1 || p.ph != 0 || p.pw != 0) return V4_UNSUPPORTED;
-    if (p.T < 1 || BX_BM % p.T) return V4_UNSUPPORTED;
-    g.P = BX_BM / p.T;
+    // P positions of every frame per tile, T * P <= 256 output rows (T = 2: P = 112, the last 32
+    // rows of the tile idle) and (T + 2) * P box rows
+    if (p.T < 1) return V4_UNSUPPORTED;
+    g.P = std::min(BX_BM / p.T, BX_ROWS / (p.T + 2));
+    if (g.P < 1) return V4_UNSUPPORTED;
     g.fP = make_fastdiv(g.P);
-    if ((p.T + 2) * g.P > BX_ROWS) return V4_UNSUPPORTED;
     g.tpc = (g.HW + g.P - 1) / g.P;
     g.ftpc = make_fastdiv(g.tpc);
     g.W1 = g.PL = 1;
@@ -686,13 +707,15 @@ static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
 bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
   BoxGeo g;
   int nt;
-  if (!((impl == 14 && (bn == 64 || bn == 128)) || (impl == 15 && (bn == 64 || bn == 128 || bn == 192)))) return false;
+  if (!((impl == 14 && (bn == 64 || bn == 96 || bn == 128 || bn == 160)) ||
+        (impl == 15 && (bn == 64 || bn == 128 || bn == 192))))
+    return false;
   return box_geo(p, g, nt) == 0;
 }
 
 template <int BN, int KS, int EPI, int PRO, int MF>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
-  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * BN * BX_BK * 2 +
+  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * ((BN + 63) / 64 * 64) * BX_BK * 2 +
                      (EPI == 2 ? 16 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
   if (lds > 160 * 1024) return V4_UNSUPPORTED;
   static bool attr_set = false;
@@ -737,7 +760,7 @@ static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
   return launch_box_epi<BN, 311, MF>(p, g, stream);
 }
 
-// impl 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (N tiles 64 / 128 / 192)
+// impl 14: 16x16x32 MFMA (N tiles 64 / 96 / 128 / 160), 15: 32x32x16 (N tiles 64 / 128 / 192)
 int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream_t stream) {
   BoxGeo g;
   int ntiles = 0;
@@ -747,6 +770,12 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
   g.pro_y = (const bf16_t*)pro.y;
   g.pro_coef = pro.coef;
   g.xld = pro.xld > 0 ? pro.xld : p.Cin;
+  static int prefire = -1;
+  if (prefire < 0) {
+    const char* e = getenv("MILNCE_BOX_PREFIRE");
+    prefire = e ? atoi(e) != 0 : 1;
+  }
+  g.prefire = prefire;
   g.zbytes = (long long)(p.M / (p.To * p.Ho * p.Wo)) * p.T * p.H * p.W * p.Cin * 2;
   if (g.xld != p.Cin) {
     if (g.xld < p.Cin || g.xld % 8) return V4_UNSUPPORTED;
@@ -757,7 +786,9 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
   p.num_m_tiles = ntiles;
   if (impl == 14) {
     if (bn == 64) return launch_box_bn<64, 16>(p, g, stream);
+    if (bn == 96) return launch_box_bn<96, 16>(p, g, stream);
     if (bn == 128) return launch_box_bn<128, 16>(p, g, stream);
+    if (bn == 160) return launch_box_bn<160, 16>(p, g, stream);
   } else if (impl == 15) {
     if (bn == 64) return launch_box_bn<64, 32>(p, g, stream);
     if (bn == 128) return launch_box_bn<128, 32>(p, g, stream);

@@ -197,18 +197,23 @@ _V4_WIDE_M = (12, 13, 14, 15)  # 8-wave workgroups, one per CU (12 / 13 v4, 14 /
 # Box-tiled forward / dgrad (csrc/conv_box.hip): stride-1 same-padded (1,3,3) / (3,1,1) convs over a
 # multiple of 8 channels; the tile's input box is staged once per 64-channel block for every tap (a
 # partial last block is zero-filled: the tuner weighs that MFMA waste against the other variants).
-# 14: 16x16x32 MFMA (N tiles 64 / 128), 15: 32x32x16 (64 / 128 / 192). MILNCE_BOX=0 leaves them out.
+# 14: 16x16x32 MFMA (N tiles 64 / 96 / 128 / 160), 15: 32x32x16 (64 / 128 / 192). MILNCE_BOX=0 leaves
+# them out.
 _BOX = os.environ.get("MILNCE_BOX", "1") != "0"
 _BOX_ROWS = 448
+# N tiles 96 / 160 and temporal tiles of T * P < 256 rows (T = 2); MILNCE_BOX_EXT=0 leaves them out
+_BOX_EXT = os.environ.get("MILNCE_BOX_EXT", "1") != "0"
 
 
 def _box_ok(bn: int, cin: int, kpad: int, impl: int, geo) -> bool:
     """Mirror of csrc/conv_box.hip fwd_box_supported; geo = (T, H, W, k, padding)."""
     if geo is None or impl not in (14, 15):
         return False
-    if not ((impl == 14 and bn in (64, 128)) or (impl == 15 and bn in (64, 128, 192))):
+    if not ((impl == 14 and bn in (64, 96, 128, 160)) or (impl == 15 and bn in (64, 128, 192))):
         return False
     T, H, W, k, pad = geo
+    if not _BOX_EXT and (bn in (96, 160) or (tuple(k) == (3, 1, 1) and 256 % T)):
+        return False
     # a partial last 64-channel block is zero-filled; its weight stage (past the tap's columns) must
     # stay inside the packed row
     if cin % 8 or kpad < (k[0] * k[1] * k[2] - 1) * cin + _ceil(cin, 64) * 64:
@@ -217,7 +222,7 @@ def _box_ok(bn: int, cin: int, kpad: int, impl: int, geo) -> bool:
         span = 255 + (255 // W + 1) + (255 // (H * W) + 1) * (W + 2) + 2 * (W + 1) + 3
         return span <= _BOX_ROWS
     if tuple(k) == (3, 1, 1) and tuple(pad) == (1, 0, 0):
-        return 256 % T == 0 and (T + 2) * (256 // T) <= _BOX_ROWS
+        return min(256 // T, _BOX_ROWS // (T + 2)) >= 1  # P positions per frame and tile
     return False
 
 

@@ -4,7 +4,7 @@ The box kernels sum the taps in (channel block, tap) order instead of v3/v4's (t
 block), so they are compared with the fp32 conv (bf16-rounded operands) and with v3's BN
 statistics / producer-BN partials, not bitwise. Shapes cover the layouts' edge cases: tiles that
 cross many (clip, frame) planes (small and odd planes), the conv_2c plane (50 x 50), every
-supported T for the temporal box (P = 256 / T positions per tile), N tiles 64 / 128 / 192, and a
+supported T for the temporal box (P = min(256 / T, 448 / (T + 2)) positions per tile), N tiles 64 / 96 / 128 / 160 / 192, and a
 channel count over several 64-wide blocks (box reloads mid-tile).
 """
 import pytest
@@ -36,6 +36,14 @@ CASES = [
     (3, 4, 13, 13, 224, 224, (3, 1, 1), (1, 0, 0)),
     (2, 4, 13, 13, 24, 64, (1, 3, 3), (0, 1, 1)),
     (2, 4, 13, 13, 48, 48, (3, 1, 1), (1, 0, 0)),
+    # N tiles of 96 / 160 (impl 14: the weight stage rows are padded to 128 / 192)
+    (2, 8, 25, 25, 64, 96, (1, 3, 3), (0, 1, 1)),
+    (3, 4, 13, 13, 96, 160, (1, 3, 3), (0, 1, 1)),
+    (2, 8, 13, 13, 160, 160, (3, 1, 1), (1, 0, 0)),
+    (2, 4, 7, 7, 96, 320, (3, 1, 1), (1, 0, 0)),
+    # T = 2: P = 112 positions per frame, the tile's last 32 rows idle
+    (3, 2, 7, 7, 192, 384, (3, 1, 1), (1, 0, 0)),
+    (2, 2, 11, 11, 96, 160, (3, 1, 1), (1, 0, 0)),
 ]
 
 
@@ -89,9 +97,14 @@ def test_conv_box_matches_reference(case):
         plan.impl = plan.d_impl = 0
 
 
+def _box_impl(bn):
+    return 15 if bn in (64, 128, 192) else 14
+
+
 @pytest.mark.parametrize("shape,cin,cmid,k", [((2, 8, 50, 50), 64, 192, (3, 3, 3)),
                                              ((3, 8, 11, 13), 128, 128, (3, 3, 3)),
-                                             ((3, 4, 13, 13), 112, 224, (3, 3, 3))])
+                                             ((3, 4, 13, 13), 112, 224, (3, 3, 3)),
+                                             ((3, 4, 13, 13), 96, 160, (3, 3, 3))])
 def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
     """A separable S3D-G unit (spatial conv -> BN -> ReLU -> temporal conv) with the spatial BN +
     ReLU applied inside the temporal conv's box kernel (hip_ops "pro" placeholders, csrc/conv_box.hip
@@ -116,12 +129,12 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
             out = u(xi)
             # force the box-tiled kernel on the temporal conv (the tuner picked on the first call)
             plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
-            plan.impl = 15
+            plan.impl = _box_impl(plan.bn)
             # and on the spatial conv's dgrad: its BN backward (dy) is then staged by that dgrad
             # (conv_dgrad_bnbwd, PRO 3) when fused
             plan1 = h.conv_plan(tuple(shape) + (cin,), (cmid, cin, 1, k[1], k[2]), (1, 1, 1), (0, 1, 1))
             if plan1.d_bn <= 128:
-                plan1.d_impl = 15
+                plan1.d_impl = _box_impl(plan1.d_bn)
             xi.grad = None
             u.zero_grad()
             out = u(xi)
