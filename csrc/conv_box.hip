@@ -44,7 +44,6 @@ template <int MF> struct BoxPitch { static constexpr int v = 80; };
 template <> struct BoxPitch<32> { static constexpr int v = 72; };
 static constexpr int BX_ROWS = 448;      // box capacity (rows)
 static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per thread: 7
-static constexpr int BX_STAGES = 3;
 
 // Diagnostic ablations (debug libraries only, tools/gpu/box_ablate.sh; results are garbage):
 // bit 0 box loads read one fixed chunk (L1-hot), bit 1 no weight DMA, bit 2 no epilogue stores /
@@ -70,7 +69,6 @@ struct BoxGeo {
   int xld;              // row stride of x in elements (Cin, or the channel count of a concatenated
                         // tensor x is a channel slice of); pro_z / pro_y are dense (stride Cin)
   long long zbytes;     // bytes of the dense pro_z / pro_y tensors
-  int prefire;          // fire a tile's stage 2 in the previous tile's epilogue (MILNCE_BOX_PREFIRE)
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -78,6 +76,78 @@ template <int N>
 __device__ __forceinline__ void bx_wait() {
   static_assert(N >= 0 && N <= 63, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// vmcnt wait for a count that folds to a constant once the tap loop is unrolled (the search
+// disappears; a count left at run time would cost a branch chain per tap)
+template <int LO, int HI>
+__device__ __forceinline__ void bx_wait_bs(uint32_t n) {
+  if constexpr (LO == HI) {
+    bx_wait<LO>();
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= (uint32_t)MID) bx_wait_bs<LO, MID>(n);
+    else bx_wait_bs<MID + 1, HI>(n);
+  }
+}
+__device__ __forceinline__ void bx_wait_c(int n) { bx_wait_bs<0, 63>((uint32_t)n); }
+
+// Exact vmcnt counts of the box kernel's weight-stage waits. At tap t of a channel block the wave
+// waits for stage t of the block; every vector-memory op it issued after that stage's DMA may still
+// be outstanding (vmcnt retires in issue order). Issue order per tap: wait, barrier, DMA of stage
+// t + STG - 1 (none at tap 0 of a later tile's first block: fired ahead in the epilogue), box
+// loads P(t). Block ends: the box's z stores (ZC); tile ends: the epilogue (EPI 2 y loads, the
+// prefire after the first half's barrier, the stores), then the z stores. Cases: 0 = first block
+// of the first tile (STG - 1 stages fired in the prologue), 1 = a later block of the same tile,
+// 2 = the first block of a later tile.
+struct BoxWaits {
+  int y[3][9];
+};
+__host__ __device__ constexpr BoxWaits make_box_waits(int TAPS, int STG, int NDMA, int P0, int PT, int NPT,
+                                                      int EPI_IT, int NPRE, bool EPI2, int ZC) {
+  // P(u): box loads at tap u = P0 at tap 0, PT at taps 1 .. NPT-1 (P0 = PT when spread)
+  BoxWaits w{};
+  for (int c = 0; c < 3; ++c) {
+    for (int t = 0; t < TAPS; ++t) {
+      auto P = [&](int u) { return u == 0 ? P0 : (u < NPT ? PT : 0); };
+      const int g = t - (STG - 1);  // tap of this block that fired stage t (< 0: earlier)
+      const int epi_after_pre = (EPI2 ? 2 * EPI_IT - NPRE : 0) + 2 * EPI_IT;
+      const int epi_all = (EPI2 ? 2 * EPI_IT : 0) + NDMA + 2 * EPI_IT;
+      int y = 0;
+      if (c == 2 && t == STG - 1) {  // prefired in the previous tile's epilogue
+        y = epi_after_pre + ZC + P(0);
+        for (int h = 1; h < t; ++h) y += NDMA + P(h);
+      } else if (g >= 0) {
+        y = P(g);
+        for (int h = g + 1; h < t; ++h) y += NDMA + P(h);
+      } else if (c == 0) {  // fired in the prologue
+        y = (STG - 2 - t) * NDMA;
+        for (int h = 0; h < t; ++h) y += NDMA + P(h);
+      } else {  // fired at tap TAPS + g of the previous block
+        const int gp = TAPS + g;
+        y = P(gp);
+        for (int h = gp + 1; h < TAPS; ++h) y += NDMA + P(h);
+        y += (c == 2 ? epi_all : 0) + ZC;
+        for (int h = 0; h < t; ++h) y += (c == 2 && h == 0 ? 0 : NDMA) + P(h);
+      }
+      w.y[c][t] = y;
+    }
+  }
+  return w;
+}
+
+// weight ring depth by N tile (stage rows rounded up to 64): as deep as the LDS next to the box
+// allows. A box load issued at tap t is waited for by tap t + stages at the latest.
+// (3,1,1) blocks have 3 taps: at most 4 stages, so a stage's DMA is always issued within the
+// previous block (the wait tables above assume it)
+__host__ __device__ constexpr int box_stages(int bn, int ks) {
+  return bn <= 64 ? (ks == 133 ? 8 : 4) : bn <= 128 ? 4 : 3;
+}
+__host__ __device__ constexpr int box_waits_max(const BoxWaits& w, int taps) {
+  int m = 0;
+  for (int c = 0; c < 3; ++c)
+    for (int t = 0; t < taps; ++t) m = w.y[c][t] > m ? w.y[c][t] : m;
+  return m;
 }
 
 template <int BN, int KS, int EPI, int PRO, int MF>
@@ -106,14 +176,23 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BNR * BK;
+  constexpr int STG = box_stages(BN, KS);      // weight ring stages
   static_assert(B_INST * RPI * NWAVES == BNR, "DMA mapping");
-  static_assert(NST + ZC + NDMA + NBL <= 63, "vmcnt range");
+  // box loads of one block: spread over the first taps of a (1,3,3) block (one x / y row chunk
+  // per tap, so each has the ring's depth in taps to land and the loads do not arrive as one
+  // burst), all at tap 0 of a (3,1,1) block (3 taps)
+  constexpr int LPP = PRO == 3 ? 2 : 1;        // loads per box piece (PRO 3: dz and y)
+  constexpr int NPRE = EPI_IT < 4 ? EPI_IT : 4;  // EPI 2: y rows loaded before a half's barrier
+  static_assert(STG - 1 <= TAPS && (KS != 133 || NBX <= TAPS), "wait tables");
+  constexpr BoxWaits kWaits = KS == 133 ? make_box_waits(TAPS, STG, NDMA, LPP, LPP, NBX, EPI_IT, NPRE, EPI == 2, ZC)
+                                        : make_box_waits(TAPS, STG, NDMA, NBX * LPP, 0, 1, EPI_IT, NPRE, EPI == 2, ZC);
+  static_assert(box_waits_max(kWaits, TAPS) <= 63, "vmcnt range");
   static_assert(PRO != 3 || BN <= 128, "PRO 3 registers");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
-  bf16_t* ring = box + BX_ROWS * 80;                             // [STAGES][BN][BK]
-  float* ss_lds = (float*)(ring + BX_STAGES * STAGE_ELEMS);      // EPI 2: [4][BN]
+  bf16_t* ring = box + BX_ROWS * 80;                             // [STG][BNR][BK]
+  float* ss_lds = (float*)(ring + STG * STAGE_ELEMS);            // EPI 2: [4][BN]
   float* pro_lds = ss_lds + (EPI == 2 ? 4 * BN : 0);             // PRO 1/2: [2][Cin]; PRO 3: [7][Cin]
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -249,16 +328,16 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   const uint32_t xrow_bytes = (uint32_t)g.xld * 2, zrow_bytes = (uint32_t)Cin * 2;
   auto xoff = [&](uint32_t r) { return r == 0x80000000u ? r : r * xrow_bytes + (uint32_t)xch * 16; };
   auto zoff = [&](uint32_t r) { return r == 0x80000000u ? r : r * zrow_bytes + (uint32_t)xch * 16; };
-  auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb) {
+  // box pieces k0 .. k1-1 of channel block cb (PRO 3: each an x (dz) and a y chunk)
+  auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb, int k0, int k1) {
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
     const bool cv = chv(cb);
 #pragma unroll
-    for (int k = 0; k < NBX; ++k)
+    for (int k = 0; k < NBX; ++k) {  // (constant bounds: xr stays in registers; k0 / k1 fold per tap)
+      if (k < k0 || k >= k1) continue;
       xr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
                                             rs, (BOX_ABLATE & 1) ? 0u : (cv ? xoff(xo[k]) : 0x80000000u), coff, 0));
-    if constexpr (PRO == 3) {
-#pragma unroll
-      for (int k = 0; k < NBX; ++k)
+      if constexpr (PRO == 3)
         yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, cv ? zoff(xo[k]) : 0x80000000u,
                                                                                 coff, 0));
     }
@@ -275,7 +354,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   // the compiler could not reuse LDS reads across rows. (1,3,3): applied after tap 3's MFMAs of the
   // block (the loads have landed there: tap 3's stage was fired after them), so the VALU work
   // interleaves with the MFMA phases; (3,1,1): right before the store.
-  auto box_xform = [&](int cb) {
+  auto box_xform = [&](int cb, int pk0, int pk1) {
     const int c0 = min(cb * BK + xch * 8, Cin - 8);  // (clamped: a missing chunk is not transformed)
     const bool cv = chv(cb);
     if constexpr (PRO == 1 || PRO == 2) {
@@ -284,6 +363,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       for (int u = 0; u < 8; ++u) { sc[u] = pro_lds[c0 + u]; sh[u] = pro_lds[Cin + c0 + u]; }
 #pragma unroll
       for (int k = 0; k < NBX; ++k) {
+        if (k < pk0 || k >= pk1) continue;
         if (cv && xo[k] != 0x80000000u) {
           float f[8];
           unpack8(xr[k], f);
@@ -303,6 +383,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
 #pragma unroll
       for (int k = 0; k < NBX; ++k) {
+        if (k < pk0 || k >= pk1) continue;
         if (cv && xo[k] != 0x80000000u) {  // padding rows stay zero (dy is zero-padded)
           float d[8], yy[8];
           unpack8(xr[k], d);
@@ -318,12 +399,14 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
     }
   };
-  constexpr int XFORM_TAP = KS == 133 ? 3 : -1;  // -1: at the store
+  // (1,3,3): piece k is transformed after tap k + XF_LAG's MFMAs (or at the block's last tap):
+  // far enough behind its load for wide N tiles, at the block's end for 64-wide ones (short taps)
+  constexpr int XF_LAG = KS == 133 ? (BN >= 128 ? 2 : TAPS) : -1;  // -1: at the store
   // PRO 2 / 3: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
   // offsets for the others) so the vmcnt accounting stays exact
   auto box_store = [&](int cb, const TileInfo& bt, __amdgpu_buffer_rsrc_t zs) {
-    if constexpr (XFORM_TAP < 0) box_xform(cb);
+    if constexpr (XF_LAG < 0) box_xform(cb, 0, NBX);
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       const uint4 v = xr[k];
@@ -395,13 +478,13 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + 64 * k);
   auto zrs = zrsrc(ti, PRO >= 2);
   if constexpr (PRO == 3) yrs_box = yrsrc(ti, true);
-  box_load(xrs, 0);
+  box_load(xrs, 0, 0, NBX);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (XFORM_TAP >= 0) box_xform(0);
+  if constexpr (XF_LAG >= 0) box_xform(0, 0, NBX);
   box_store(0, ti, zrs);
-  int gs = 0;  // global stage counter (ring slot = gs % 3)
-  fire(0, 0);
-  fire(1, 1 % nst_tile);
+  int gs = 0;  // global stage counter (ring slot = gs % STG)
+#pragma unroll
+  for (int i = 0; i < STG - 1; ++i) fire(i, i % nst_tile);
   bool first_tile = true;
 
   typedef typename std::conditional<MF == 16, f32x4, f32x16>::type acc_t;
@@ -425,57 +508,36 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
       for (int t = 0; t < TAPS; ++t) {
         const int s = cb * TAPS + t;  // stage within the tile
-        // wait for stage s: count the wave's younger vector-memory ops (exact, in issue order)
-        //   * stage s+1 (fired one iteration ago) unless s is the tile's last stage [never: the
-        //     next tile's first stage is fired there too, see below] -> NDMA
-        //   * box loads issued at tap 0 of this block after firing stage cb*TAPS+2: younger
-        //     than stages up to cb*TAPS+2 -> waits at taps 1, 2
-        //   * epilogue stores of the previous tile (NST) and, with PRO 2, the z stores of the
-        //     box written after them (ZC), or of the box written at the end of the previous block:
-        //     younger than the first two stages of this block, and than the third on a tile after
-        //     the first (its stage 2 was fired in the previous epilogue, before the stores, so the
-        //     stores have three taps to drain instead of two)
-        const bool carried = cb == 0 && !first_tile && g.prefire;
-        if (t == 0) {
-          if (carried) bx_wait<2 * NDMA + NST + ZC>();
-          else if (cb > 0) bx_wait<NDMA + ZC>();
-          else bx_wait<NDMA>();
-        } else if (t == 1) {
-          if (carried) bx_wait<NST + ZC + NDMA + NBL>();
-          else if (cb > 0) bx_wait<ZC + NDMA + NBL>();
-          else bx_wait<NDMA + NBL>();
-        } else if (t == 2) {
-          if (carried) bx_wait<NST + ZC + NBL + NDMA>();
-          else bx_wait<NBL + NDMA>();
-        } else {
-          bx_wait<NDMA>();
-        }
+        // wait for stage s (the oldest in flight; exact counts, see BoxWaits): the ops issued
+        // after its DMA -- later stages, box loads, the previous tile's epilogue stores and z
+        // stores -- drain only when a stage fired after them is waited for
+        const bool carried = cb == 0 && !first_tile;
+        if (cb > 0) bx_wait_c(kWaits.y[1][t]);
+        else if (first_tile) bx_wait_c(kWaits.y[0][t]);
+        else bx_wait_c(kWaits.y[2][t]);
         ring_barrier();
-        // fire stage s + 2 (continuing into the next tile: the weights do not depend on the tile;
-        // stage 2 of a carried tile is already in flight)
-        if (!(t == 0 && carried)) {
-          int s2 = s + 2;
-          if (s2 >= nst_tile) s2 -= nst_tile;
-          if (s2 >= nst_tile) s2 = 0;  // nst_tile == 1 (not used by the supported shapes)
-          fire((gs + 2) % BX_STAGES, s2);
-        }
-        if (t == 0) {
-          // prefetch the next box: next channel block of this tile, or the next tile's block 0
-          if (!last_cb) {
-            box_load(xrs, cb + 1);
-          } else {
-            auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + tn.xbase), (short)0,
-                                                         (int)(has_next ? tn.xnrec : 0u), 0x00020000);
+        // fire stage s + STG - 1 into the slot read at the previous tap (continuing into the next
+        // tile: the weights do not depend on the tile); a carried tile's first one is in flight
+        if (!(t == 0 && carried)) fire((gs + STG - 1) % STG, (s + STG - 1) % nst_tile);
+        if (t == 0 && last_cb) {
+          // the next box is the next tile's block 0
+          auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + tn.xbase), (short)0,
+                                                       (int)(has_next ? tn.xnrec : 0u), 0x00020000);
 #pragma unroll
-            for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
-            if constexpr (PRO == 3) yrs_box = yrsrc(tn, has_next);
-            box_load(nrs, 0);
-            xrs = nrs;
-            zrs = zrsrc(tn, PRO >= 2 && has_next);
-          }
+          for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
+          if constexpr (PRO == 3) yrs_box = yrsrc(tn, has_next);
+          xrs = nrs;
+          zrs = zrsrc(tn, PRO >= 2 && has_next);
+        }
+        // prefetch pieces of the next box (next channel block of this tile, or the next tile's
+        // block 0)
+        if constexpr (KS == 133) {
+          if (t < NBX) box_load(xrs, last_cb ? 0 : cb + 1, t, t + 1);
+        } else {
+          if (t == 0) box_load(xrs, last_cb ? 0 : cb + 1, 0, NBX);
         }
         // ---- MFMAs of stage s: A = weights (ring), B = box rows shifted by the tap ----
-        const bf16_t* bsh = ring + (gs % BX_STAGES) * STAGE_ELEMS;
+        const bf16_t* bsh = ring + (gs % STG) * STAGE_ELEMS;
         int shift;
         if constexpr (KS == 133) shift = (t / 3) * g.W1 + (t % 3);
         else shift = t * g.P;
@@ -508,8 +570,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           __builtin_amdgcn_s_setprio(0);
         }
         ++gs;
-        if constexpr (XFORM_TAP >= 0 && PRO != 0) {
-          if (t == XFORM_TAP) box_xform(last_cb ? 0 : cb + 1);
+        if constexpr (XF_LAG >= 0 && PRO != 0) {
+          // pieces whose transform falls on this tap (the block's last tap takes the rest)
+          const int ka = max(t - XF_LAG, 0), kb = t == TAPS - 1 ? NBX : t - XF_LAG + 1;
+          if (kb > ka) box_xform(last_cb ? 0 : cb + 1, ka, kb);
         }
       }
       // every wave is done with this box: write the prefetched one (the next iteration's ring
@@ -526,7 +590,6 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       // EPI 2: the producer's raw outputs of this thread's rows, loaded before the staging writes
       // and the barrier so their latency overlaps them (one load chain, not one per row)
       // (at most 4 rows ahead: the other half's waves still hold their accumulators here)
-      constexpr int NPRE = EPI_IT < 4 ? EPI_IT : 4;
       uint4 ypre[EPI_IT];
       auto yload = [&](int it) {
         const int cc = tid % OCPR;
@@ -565,8 +628,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
       lds_barrier();
       // every wave is past the tile's last MFMAs: the last stage's ring slot is free for the next
-      // tile's stage 2, fired ahead of the stores (see the waits at taps 0-2)
-      if (half == 0 && g.prefire) fire((gs + 2) % BX_STAGES, 2);
+      // tile's stage STG - 1, fired ahead of the stores (so the stores drain behind it)
+      if (half == 0) fire((gs + STG - 1) % STG, (STG - 1) % nst_tile);
       {
         const auto yrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.y + ti.ybase), (short)0, 0x7FFFFFF0, 0x00020000);
         const int cc = tid % OCPR;
@@ -624,7 +687,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     }
     if constexpr ((BOX_ABLATE & 8) != 0) {
       lds_barrier();
-      if (g.prefire) fire((gs + 2) % BX_STAGES, 2);
+      fire((gs + STG - 1) % STG, (STG - 1) % nst_tile);
     }
     // the next tile's first box (its loads were issued at the last block's first tap)
     if (has_next) box_store(0, tn, zrs);
@@ -715,7 +778,7 @@ bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
 
 template <int BN, int KS, int EPI, int PRO, int MF>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
-  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)BX_STAGES * ((BN + 63) / 64 * 64) * BX_BK * 2 +
+  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)box_stages(BN, KS) * ((BN + 63) / 64 * 64) * BX_BK * 2 +
                      (EPI == 2 ? 16 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
   if (lds > 160 * 1024) return V4_UNSUPPORTED;
   static bool attr_set = false;
@@ -770,12 +833,7 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
   g.pro_y = (const bf16_t*)pro.y;
   g.pro_coef = pro.coef;
   g.xld = pro.xld > 0 ? pro.xld : p.Cin;
-  static int prefire = -1;
-  if (prefire < 0) {
-    const char* e = getenv("MILNCE_BOX_PREFIRE");
-    prefire = e ? atoi(e) != 0 : 1;
-  }
-  g.prefire = prefire;
+
   g.zbytes = (long long)(p.M / (p.To * p.Ho * p.Wo)) * p.T * p.H * p.W * p.Cin * 2;
   if (g.xld != p.Cin) {
     if (g.xld < p.Cin || g.xld % 8) return V4_UNSUPPORTED;

@@ -14,11 +14,14 @@ for r in 1 2; do
   done
 done > $D/bench.txt 2>&1
 grep -v amdgpu.ids $D/bench.txt
-for v in "$A" "$B"; do
+for arm in a b; do
+  if [ $arm = a ]; then v=$A; else v=$B; fi
+  # label: the value itself when it is a plain word, else the arm (a / b)
+  case "$v" in *[!A-Za-z0-9_.-]*|"") L=$arm ;; *) L=$v ;; esac
   export $VAR=$v
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof_$v -o run --output-format csv -- python bench.py --steps 3 --warmup 2 > $D/prof_$v.log 2>&1 || { tail -20 $D/prof_$v.log; exit 1; }
-  T=$(find $D/prof_$v -name "run_kernel_trace.csv" | head -1)
-  python tools/kstats.py $T --skip 3 --top 60 > $D/kstats_$v.txt
-  head -3 $D/kstats_$v.txt
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof_$L -o run --output-format csv -- python bench.py --steps 3 --warmup 2 > $D/prof_$L.log 2>&1 || { tail -20 $D/prof_$L.log; exit 1; }
+  T=$(find $D/prof_$L -name "run_kernel_trace.csv" | head -1)
+  python tools/kstats.py $T --skip 3 --top 60 > $D/kstats_$L.txt
+  head -3 $D/kstats_$L.txt
 done
 find $D -name "*.csv" -size +20M -delete
