@@ -410,6 +410,7 @@ _TUNE_MARGIN = float(os.environ.get("MILNCE_TUNE_MARGIN", "0.97"))  # another va
 # variant timed on L2 / Infinity-Cache-resident repeats of its own inputs can lose inside the step
 # (e.g. the 256-row dgrad with the producer-BN epilogue: 1.33 ms warm, 1.95 ms in the step).
 _TUNE_FLUSH = os.environ.get("MILNCE_TUNE_FLUSH", "1") != "0"
+_TUNE_ROUNDS = max(1, int(os.environ.get("MILNCE_TUNE_ROUNDS", "3")))
 _FLUSH_BUF: Dict[int, torch.Tensor] = {}
 
 
@@ -424,8 +425,8 @@ def _tune_flush_buffer() -> torch.Tensor:
 def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
     """Time each kernel variant on the real operands (outputs are simply overwritten) and keep
     the fastest; run once per conv shape and direction, then cached in the plan. Each variant
-    is timed over >= ~0.5 ms of repetitions, and the default wins unless another is >= 3 %
-    faster, so the choice is stable from run to run."""
+    is timed over >= ~0.5 ms of repetitions (at least one per round), and the default wins unless
+    another is >= 3 % faster, so the choice is stable from run to run."""
     if not _AUTOTUNE:
         return _DEFAULT_IMPL
     s = torch.cuda.current_stream()
@@ -453,11 +454,18 @@ def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
             total += a.elapsed_time(b)
         return total / reps
 
-    times = {}
+    # variants interleaved over _TUNE_ROUNDS rounds, median per variant: a clock or cache drift
+    # during the tuning of one shape cannot favour whichever variant happened to run first
+    reps = {}
     for impl in impls:
         launch(impl)  # warm (first launch sets kernel attributes)
         t0 = timed(impl, 1)
-        times[impl] = timed(impl, max(2, min(50, int(0.5 / max(t0, 1e-3)))))
+        reps[impl] = max(1, min(50, int(0.5 / max(t0, 1e-3))) // _TUNE_ROUNDS)
+    samples = {impl: [] for impl in impls}
+    for _ in range(_TUNE_ROUNDS):
+        for impl in impls:
+            samples[impl].append(timed(impl, reps[impl]))
+    times = {impl: sorted(v)[len(v) // 2] for impl, v in samples.items()}
     best = min(times, key=times.get)
     default = _DEFAULT_IMPL if default is None else default
     if default in times and times[best] > _TUNE_MARGIN * times[default]:
