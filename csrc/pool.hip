@@ -928,7 +928,10 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
   const S1Geo s = s1_geo(p, G, nchunk);
   const int n = (s.rows + 1) * G;
   uint4* dys = s1_lds;                   // 2 * n
-  float4* m2s = (float4*)(s1_lds + 2 * n);  // 2 * n float4 (8 floats per slot)
+  // fp32 m2 as two planes of float4 (channels 0-3 | 4-7): 16-B lane stride, bank-conflict free
+  // (one 32-B slot per lane halved the LDS rate: SQ_LDS_BANK_CONFLICT / IDX_ACTIVE was 0.5)
+  float4* m2lo = (float4*)(s1_lds + 2 * n);  // n float4
+  float4* m2hi = m2lo + n;                   // n float4
   uint2* cds = (uint2*)(s1_lds + 4 * n);    // 2 * n
   const size_t clip = (size_t)s.b * s.rows * p.W * p.C;
   const int nbytes = s.rows * p.W * p.C * 2;
@@ -980,12 +983,12 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
         v += (vtm && code(c2, k, 4) == 2u) ? g2[k] : 0.f;
         m2[k] = v;
       }
-      m2s[2 * me] = make_float4(m2[0], m2[1], m2[2], m2[3]);
-      m2s[2 * me + 1] = make_float4(m2[4], m2[5], m2[6], m2[7]);
+      m2lo[me] = make_float4(m2[0], m2[1], m2[2], m2[3]);
+      m2hi[me] = make_float4(m2[4], m2[5], m2[6], m2[7]);
       lds_barrier();
       // h stage: candidates are the m2 cells at h+1 (dh=0), h (dh=1), h-1 (dh=2)
       const uint2 h0 = cds[buf + ihp], h2 = cds[buf + ihm];
-      const float4 p0a = m2s[2 * ihp], p0b = m2s[2 * ihp + 1], p2a = m2s[2 * ihm], p2b = m2s[2 * ihm + 1];
+      const float4 p0a = m2lo[ihp], p0b = m2hi[ihp], p2a = m2lo[ihm], p2b = m2hi[ihm];
       const float q0[8] = {p0a.x, p0a.y, p0a.z, p0a.w, p0b.x, p0b.y, p0b.z, p0b.w};
       const float q2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
 #pragma unroll
