@@ -399,9 +399,11 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
     }
   };
-  // (1,3,3): piece k is transformed after tap k + XF_LAG's MFMAs (or at the block's last tap):
-  // far enough behind its load for wide N tiles, at the block's end for 64-wide ones (short taps)
-  constexpr int XF_LAG = KS == 133 ? (BN >= 128 ? 2 : TAPS) : -1;  // -1: at the store
+  // (1,3,3): the pieces are transformed after the block's last tap (XF_LAG = TAPS), when the loads
+  // of every piece have long landed: same-box A/Bs against transforming piece k after tap k + 2 / 3
+  // (interleaved with the MFMA phases): 128-wide dgrad 0.437 -> 0.403 ms, conv_2c spatial dgrad
+  // 2.98 (lag 3) -> 2.5 ms -- a transform waits for its piece's load, i.e. drains the vmcnt queue
+  constexpr int XF_LAG = KS == 133 ? TAPS : -1;  // -1: at the store
   // PRO 2 / 3: the tile's own rows of the transformed input go to pro_z (same layout as x, so the
   // same offsets) from the workgroups of N tile 0; every wave issues NBX stores (out-of-range
   // offsets for the others) so the vmcnt accounting stays exact
