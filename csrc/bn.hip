@@ -257,12 +257,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
   if (rr >= rpi) return;
   const int c0 = cc * 8;
-  float sc[8], sh[8], mean[8], istd[8], k0[8], k1[8], k2[8];
+  BnBwdC q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = c0 + k;
-    mean[k] = ss[c]; istd[k] = ss[C + c]; sc[k] = ss[2 * C + c]; sh[k] = ss[3 * C + c];
-    k0[k] = coef[c]; k1[k] = coef[C + c]; k2[k] = coef[2 * C + c];
+    q[k] = bn_bwd_const(ss[c], ss[C + c], ss[2 * C + c], ss[3 * C + c], coef[c], coef[C + c], coef[2 * C + c]);
   }
   const long long r_begin = (long long)blockIdx.x * rows_per_block;
   const long long r_end = min(M, r_begin + rows_per_block);
@@ -283,11 +282,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       unpack8(gv[u], g);
       unpack8(yv[u], v);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? g[k] : 0.f;
-        const float xh = (v[k] - mean[k]) * istd[k];
-        o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
-      }
+      for (int k = 0; k < 8; ++k) o[k] = bn_bwd_elem(g[k], v[k], q[k]);
       *(uint4*)(dy + r * lddy + c0) = pack8(o);
     }
   }
@@ -376,12 +371,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_gate_kernel(
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
   if (rr >= rpi) return;
   const int c0 = cc * 8, b = blockIdx.y;
-  float sc[8], sh[8], mean[8], istd[8], k0[8], k1[8], k2[8], gg[8], dm[8];
+  BnBwdC q[8];
+  float gg[8], dm[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = c0 + k;
-    mean[k] = ss[c]; istd[k] = ss[C + c]; sc[k] = ss[2 * C + c]; sh[k] = ss[3 * C + c];
-    k0[k] = coef[c]; k1[k] = coef[C + c]; k2[k] = coef[2 * C + c];
+    q[k] = bn_bwd_const(ss[c], ss[C + c], ss[2 * C + c], ss[3 * C + c], coef[c], coef[C + c], coef[2 * C + c]);
     gg[k] = g[(size_t)b * ldg + c];
     dm[k] = dmean[(size_t)b * ldg + c] * inv_thw;
   }
@@ -407,9 +402,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_gate_kernel(
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float dz = bf2f(f2bf(fmaf(d[k], gg[k], dm[k])));  // the value gate_bwd_apply reduced
-        const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? dz : 0.f;
-        const float xh = (v[k] - mean[k]) * istd[k];
-        o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
+        o[k] = bn_bwd_elem(dz, v[k], q[k]);
       }
       *(uint4*)(dy + row * lddy + c0) = pack8(o);
     }

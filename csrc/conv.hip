@@ -1459,9 +1459,9 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const int ch = c * 8 + k;
-            const float gm = (yv[k] * bnc[128 + ch] + bnc[192 + ch] > 0.f) ? dz[k] : 0.f;
-            const float xh = (yv[k] - bnc[ch]) * bnc[64 + ch];
-            o[k] = bnc[256 + ch] * (gm - bnc[320 + ch] - xh * bnc[384 + ch]);
+            const BnBwdC q = bn_bwd_const(bnc[ch], bnc[64 + ch], bnc[128 + ch], bnc[192 + ch], bnc[256 + ch],
+                                          bnc[320 + ch], bnc[384 + ch]);
+            o[k] = bn_bwd_elem(dz[k], yv[k], q);
           }
           *slot = pack8(o);
         }

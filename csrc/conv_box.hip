@@ -374,12 +374,12 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       }
     }
     if constexpr (PRO == 3) {
-      float cm[8], ci[8], cs[8], ch[8], k0[8], k1[8], k2[8];
+      BnBwdC q[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int c = c0 + u;
-        cm[u] = pro_lds[c]; ci[u] = pro_lds[Cin + c]; cs[u] = pro_lds[2 * Cin + c]; ch[u] = pro_lds[3 * Cin + c];
-        k0[u] = pro_lds[4 * Cin + c]; k1[u] = pro_lds[5 * Cin + c]; k2[u] = pro_lds[6 * Cin + c];
+        q[u] = bn_bwd_const(pro_lds[c], pro_lds[Cin + c], pro_lds[2 * Cin + c], pro_lds[3 * Cin + c],
+                            pro_lds[4 * Cin + c], pro_lds[5 * Cin + c], pro_lds[6 * Cin + c]);
       }
 #pragma unroll
       for (int k = 0; k < NBX; ++k) {
@@ -389,11 +389,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           unpack8(xr[k], d);
           unpack8(yr[k], yy);
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float gm = (yy[u] * cs[u] + ch[u] > 0.f) ? d[u] : 0.f;
-            const float xh = (yy[u] - cm[u]) * ci[u];
-            d[u] = k0[u] * (gm - k1[u] - xh * k2[u]);
-          }
+          for (int u = 0; u < 8; ++u) d[u] = bn_bwd_elem(d[u], yy[u], q[u]);
           xr[k] = pack8(d);
         }
       }

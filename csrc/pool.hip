@@ -502,13 +502,13 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     v = pack8(q);
   };
   // BN backward constants of this thread's channels (APPLY): dy = k0 * (dz*mask - k1 - xhat*k2)
-  float bsc[8], bsh[8], bmu[8], bis[8], k0[8], k1[8], k2[8];
+  BnBwdC bq[8];
   if constexpr (MODE == POOL_BWD_APPLY) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int c = active ? c0 + k : 0;
-      bmu[k] = bn_ss[c]; bis[k] = bn_ss[p.C + c]; bsc[k] = bn_ss[2 * p.C + c]; bsh[k] = bn_ss[3 * p.C + c];
-      k0[k] = coef[c]; k1[k] = coef[p.C + c]; k2[k] = coef[2 * p.C + c];
+      bq[k] = bn_bwd_const(bn_ss[c], bn_ss[p.C + c], bn_ss[2 * p.C + c], bn_ss[3 * p.C + c], coef[c],
+                           coef[p.C + c], coef[2 * p.C + c]);
     }
   }
   auto bn_apply = [&](uint32_t ps, uint4& v, const uint4* ypre = nullptr) {
@@ -516,11 +516,7 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
     unpack8(v, dz);
     unpack8(ypre != nullptr ? *ypre : *(const uint4*)(bn_y + (size_t)ps * bn_ld + c0), yv);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float gm = (yv[k] * bsc[k] + bsh[k] > 0.f) ? dz[k] : 0.f;
-      const float xh = (yv[k] - bmu[k]) * bis[k];
-      o[k] = k0[k] * (gm - k1[k] - xh * k2[k]);
-    }
+    for (int k = 0; k < 8; ++k) o[k] = bn_bwd_elem(dz[k], yv[k], bq[k]);
     v = pack8(o);
   };
   // one input position's epilogue (the quad path; the pair loop below interleaves two of them)
