@@ -93,7 +93,7 @@ def _loss_grad(tr, batch, v, t, aten):
     return float(loss), v.grad, t.grad
 
 
-def _compare(extra, make_batch, chunks=0):
+def _compare(extra, make_batch, chunks=0, video_tol=0.15):
     """Same weights, same batch: (1) the HIP towers' embeddings equal the ATen/MIOpen ones to bf16
     accuracy; (2) on the SAME embeddings the loss and its gradient w.r.t. the embeddings (the HIP
     soft-DTW / MIL-NCE kernels vs the ATen formulas) agree to fp32 accuracy; (3) the whole
@@ -114,8 +114,10 @@ def _compare(extra, make_batch, chunks=0):
     va, ta = _embed(tr_a, batch, chunks, aten=True)
     print(f"embeddings rel diff: video {rel(vh, va):.4f} text {rel(th, ta):.4f}")
     # bf16 conv outputs stored before train-mode BN lose precision where |mean| >> std; both bf16
-    # paths carry that (each is 5-9 % from a CPU fp32 forward at these shapes, tools/debug/grad_ab.py)
-    assert rel(vh, va) < 0.15 and rel(th, ta) < 0.02
+    # paths carry that (each is 5-9 % from a CPU fp32 forward at these shapes, tools/debug/grad_ab.py;
+    # HIP vs ATen measured 0.053 at the flagship shapes, 0.088 / 0.098 at the 96^2 ones). The
+    # per-block fp32 bounds are in tests/test_gpu_fulldepth.py.
+    assert rel(vh, va) < video_tol and rel(th, ta) < 0.02
     lh, gvh, gth = _loss_grad(tr, batch, vh, th, aten=False)
     la, gva, gta = _loss_grad(tr, batch, vh, th, aten=True)
     print(f"loss on the same embeddings: hip {lh:.6f} aten {la:.6f}; d/dv {rel(gvh, gva):.2e} d/dt {rel(gth, gta):.2e}")
@@ -172,4 +174,5 @@ def test_flagship_shapes_hip_matches_aten():
     def mk(args):
         return SyntheticClips(64, 16, 200, 4, args.max_words, args.vocab_size, device=torch.device("cuda")).batch(0)
 
-    _compare(["--batch_size", "64", "--num_frames", "16", "--video_size", "200", "--num_candidates", "4"], mk)
+    _compare(["--batch_size", "64", "--num_frames", "16", "--video_size", "200", "--num_candidates", "4"], mk,
+             video_tol=0.08)
