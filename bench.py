@@ -94,7 +94,8 @@ def main():
         # setup, not a training step: one forward/backward so per-shape conv autotuning
         # (first use of each conv plan) does not land inside the timed region
         trainer.model.train()
-        trainer.forward_loss(data.batch(0)).backward()
+        with trainer.tune_region():
+            trainer.forward_loss(data.batch(0)).backward()
         trainer.bucketer.finish()
         trainer.bucketer.zero()
     for _ in range(opts.warmup):
@@ -114,6 +115,12 @@ def main():
     dt = time.perf_counter() - t0
     dt = pdist.all_reduce_max(dt)
     final_loss = float(losses[-1].item()) if losses else float("nan")
+    # kernel plan of every rank (ops/tune_sync: rank 0 tunes, the others launch its choices)
+    from mil_nce_howto100m_amd.ops import tune_sync
+    hashes = [tune_sync.plan_hash()]
+    if ctx.world_size > 1:
+        hashes = [None] * ctx.world_size
+        torch.distributed.all_gather_object(hashes, tune_sync.plan_hash())
     comm = None
     if ctx.world_size > 1:
         # after the timed region: the step's collectives alone at the step's sizes (xGMI record)
@@ -171,6 +178,7 @@ def main():
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
         }
+        out["plan_hash"] = hashes[0] if len(set(hashes)) == 1 else hashes
         if comm is not None:
             out["comm"] = comm
         if cuda:

@@ -79,8 +79,12 @@ __device__ __forceinline__ void dist_grad(int kind, float s, float a, float b, f
       const float sq = a + b - 2.f * s;
       float dDsq = sq >= 0.f ? 1.f : 0.f;
       if (kind == DK_EUCLID) {
+        // d exp(r) / d sq = exp(r) / 2r is unbounded as r -> 0, and dX = ds Y + ca X would then
+        // cancel two huge fp32 terms (normalize=True's self cells are exactly zero distances):
+        // below the fp32 cancellation level of sq the subgradient is zero (the float64 oracle's
+        // clamp gives the same at identical rows)
         const float r = sqrtf(fmaxf(sq, 0.f) + 1e-12f);
-        dDsq *= expf(r) / (2.f * r);
+        dDsq = sq > 1e-6f * (a + b) + 1e-12f ? dDsq * expf(r) / (2.f * r) : 0.f;
       }
       ds = -2.f * dDsq;
       da = dDsq;

@@ -86,6 +86,10 @@ class NativeLibraryError(RuntimeError):
     pass
 
 
+class UnsupportedVariant(NativeLibraryError):
+    """A kernel variant declined the shape (status -1, csrc/conv_common.h V4_UNSUPPORTED)."""
+
+
 def lib():
     global _lib
     if _lib is not None:
@@ -116,6 +120,8 @@ def call(name: str, *args) -> None:
     global _calls
     fn = getattr(lib(), name)
     rc = fn(*args)
+    if rc == -1:
+        raise UnsupportedVariant(f"{name}: the requested kernel variant does not support this shape")
     if rc != 0:
         raise NativeLibraryError(f"{name} failed with hipError {rc}")
     if _DEBUG_SYNC:

@@ -15,8 +15,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from . import aten, grad_sink
-from ._lib import call, lib, ptr, stream
+from . import aten, grad_sink, tune_sync
+from ._lib import UnsupportedVariant, call, lib, ptr, stream
 
 BF16 = torch.bfloat16
 F32 = torch.float32
@@ -87,6 +87,12 @@ def _zeros_f32(shape: Tuple[int, ...], device: torch.device) -> torch.Tensor:
 
 def _ceil(a: int, b: int) -> int:
     return (a + b - 1) // b
+
+
+def _plan_sig(plan) -> str:
+    """Problem identity of a conv plan for rank-consistent tuning (tune_sync)."""
+    return (f"|B{plan.B}T{plan.T}H{plan.H}W{plan.W}|{plan.Cin}>{plan.Cout}|k{plan.k}s{plan.s}p{plan.p}"
+            f"|wo{plan.wo_override}")
 
 
 # =========================================================================================
@@ -168,16 +174,18 @@ def _stats_rows(M: int, npad: int, bn: int) -> int:
 
 
 def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
-              max_rows: Optional[int] = None) -> Tuple[int, int]:
+              max_rows: Optional[int] = None, sig: str = "") -> Tuple[int, int]:
     """(impl, grid) of the fastest (kernel variant, persistent grid) pair; launch(impl, grid).
-    Grids with more partial-statistics rows than ``max_rows`` (the caller's buffer) are skipped."""
+    Grids with more partial-statistics rows than ``max_rows`` (the caller's buffer) are skipped.
+    ``sig`` names the problem for rank-consistent tuning (tune_sync)."""
     wgs = tuple(w for w in dict.fromkeys((_FWD_WGS_PER_CU,) + _FWD_WGS_TUNE)
                 if w == _FWD_WGS_PER_CU or max_rows is None or _grid_for(M, npad, bn, w) <= max_rows)
     code = {(i, w): 10 * i + w for i in plan_impls if i not in _V4_WIDE_M for w in wgs}
     code.update({(i, w): 10 * i + w for i in plan_impls if i in _V4_WIDE_M for w in (1, 2)})
     inv = {v: k for k, v in code.items()}
     best = _tune(lambda c: launch(inv[c][0], _grid_for(M, npad, bn, inv[c][1])), tuple(code.values()),
-                 default=code.get((_DEFAULT_IMPL, _FWD_WGS_PER_CU)))
+                 default=code.get((_DEFAULT_IMPL, _FWD_WGS_PER_CU)),
+                 sig=f"{sig}|M{M}|N{npad}|bn{bn}|{sorted(code.values())}")
     if best not in inv:  # autotune off: the default variant on the default grid
         return best, _grid_for(M, npad, bn, _FWD_WGS_PER_CU)
     impl, w = inv[best]
@@ -422,13 +430,23 @@ def _tune_flush_buffer() -> torch.Tensor:
     return buf
 
 
-def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
+def release_tuning_buffers() -> None:
+    """Free the cold-cache flush buffer (384 MiB per device) once the step's shapes are tuned."""
+    _FLUSH_BUF.clear()
+
+
+def _tune(launch, impls=_IMPLS, default: Optional[int] = None, sig: str = "") -> int:
     """Time each kernel variant on the real operands (outputs are simply overwritten) and keep
     the fastest; run once per conv shape and direction, then cached in the plan. Each variant
     is timed over >= ~0.5 ms of repetitions (at least one per round), and the default wins unless
-    another is >= 3 % faster, so the choice is stable from run to run."""
+    another is >= 3 % faster, so the choice is stable from run to run. Under data parallelism
+    (tune_sync.region) only rank 0 times; every rank launches rank 0's choice."""
     if not _AUTOTUNE:
         return _DEFAULT_IMPL
+    return tune_sync.decide(sig or f"impls{tuple(impls)}", lambda: _tune_local(launch, impls, default))
+
+
+def _tune_local(launch, impls, default: Optional[int]) -> int:
     s = torch.cuda.current_stream()
     flush = _tune_flush_buffer() if _TUNE_FLUSH else None
 
@@ -458,9 +476,15 @@ def _tune(launch, impls=_IMPLS, default: Optional[int] = None) -> int:
     # during the tuning of one shape cannot favour whichever variant happened to run first
     reps = {}
     for impl in impls:
-        launch(impl)  # warm (first launch sets kernel attributes)
+        try:
+            launch(impl)  # warm (first launch sets kernel attributes)
+        except UnsupportedVariant:  # a variant whose own checks (e.g. its LDS budget) decline the shape
+            continue
         t0 = timed(impl, 1)
-        reps[impl] = max(1, min(50, int(0.5 / max(t0, 1e-3))) // _TUNE_ROUNDS)
+        reps[impl] = max(1, min(50 if flush is None else 18, int(0.5 / max(t0, 1e-3))) // _TUNE_ROUNDS)
+    if not reps:
+        raise UnsupportedVariant(f"no kernel variant of {tuple(impls)} supports this shape")
+    impls = tuple(reps)
     samples = {impl: [] for impl in impls}
     for _ in range(_TUNE_ROUNDS):
         for impl in impls:
@@ -505,7 +529,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
             rows_p = stats.numel() // (2 * plan.Npad) if stats is not None else None
             plan.impl, plan.grid_m = _tune_fwd(launch_pro, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
                                                                       _box_geo(plan)),
-                                               plan.M, plan.Npad, plan.bn, rows_p)
+                                               plan.M, plan.Npad, plan.bn, rows_p, sig="fwdpro" + _plan_sig(plan))
         if plan.impl in _BOX_IMPLS and fusable:
             launch_pro(plan.impl, plan.grid_m)
             return y
@@ -526,7 +550,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
         else:
             plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
                                                                   _box_geo(plan)),
-                                               plan.M, plan.Npad, plan.bn, rows)
+                                               plan.M, plan.Npad, plan.bn, rows, sig="fwd" + _plan_sig(plan))
     if rows is not None and rows < plan.grid_m:
         raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
                          f"(allocate _stats_rows(M, Npad, bn) rows)")
@@ -557,7 +581,8 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
     if plan.d_impl == 0:
         plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
                                                                   _box_geo(plan)),
-                                               md, plan.d_Npad, plan.d_bn)
+                                               md, plan.d_Npad, plan.d_bn,
+                                               sig=("dgradp" if part is not None else "dgrad") + _plan_sig(plan))
     launch(plan.d_impl, plan.d_grid_m)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
@@ -623,7 +648,8 @@ def _tune_dgrad_bnbwd(plan: ConvPlan, dz, weight, y, ss, gamma, part, nparts, ps
 
     plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
                                                               _box_geo(plan)),
-                                           md, plan.d_Npad, plan.d_bn)
+                                           md, plan.d_Npad, plan.d_bn,
+                                           sig=("dgradbnp" if x_bn is not None else "dgradbn") + _plan_sig(plan))
 
 
 # MILNCE_BNBWD_FUSE=0 disables. First version measured slower in the step (conv_2c spatial dgrad
@@ -977,7 +1003,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4, plan.w_tk)
             best = _tune(lambda c: launch_with(*inv[c], scratch, 0), tuple(code.values()),
-                         default=code.get(default))
+                         default=code.get(default), sig=f"wgrad{_plan_sig(plan)}|{sorted(cands)}")
             tn, impl, occ, tk = inv[best]
             plan.w_tn, plan.w_impl, plan.w_occ = tn, impl, occ
             if impl < 100:

@@ -171,6 +171,15 @@ def launch_local(script: str, argv: Sequence[str], nprocs: int, poll_s: float = 
     return rc if rc >= 0 else 128 - rc
 
 
+def _device_flag(argv: Sequence[str]) -> str:
+    """--device as argparse reads it (``--device cpu``, ``--device=cpu``, unambiguous prefixes)."""
+    import argparse
+    ap = argparse.ArgumentParser(add_help=False, allow_abbrev=True)
+    ap.add_argument("--device", default="auto")
+    known, _ = ap.parse_known_args(list(argv))
+    return known.device
+
+
 def run_per_gpu(script: str, argv: Sequence[str], run) -> int:
     """Entry-point process model shared by ``main_distributed.py`` and the ``eval_*.py`` scripts:
     under torchrun (``WORLD_SIZE`` set) or on CPU run this process as one rank; otherwise start
@@ -179,7 +188,7 @@ def run_per_gpu(script: str, argv: Sequence[str], run) -> int:
     argv = list(argv)
     if "WORLD_SIZE" in os.environ:
         return run(argv)
-    if "--device" in argv and argv.index("--device") + 1 < len(argv) and argv[argv.index("--device") + 1] == "cpu":
+    if _device_flag(argv) == "cpu":
         return run(argv)
     n = count_gpus_no_init()
     if n <= 1:

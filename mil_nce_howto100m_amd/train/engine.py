@@ -80,6 +80,14 @@ class Trainer:
         self.criterion = build_loss(args)
         self.global_step = 0
         self.timer = StepTimer(bool(getattr(args, "phase_timers", 0)), self.device)
+        # kernel autotuning (first use of each conv shape) decided by rank 0 for every rank
+        from ..ops import tune_sync
+        self._tune_synced = ctx.world_size > 1 and tune_sync.configure_from_process_group()
+
+    def tune_region(self):
+        """Context of a DP step: every kernel-variant choice made inside is rank 0's (ops/tune_sync)."""
+        from ..ops import tune_sync
+        return tune_sync.region(self._tune_synced)
 
     # ---------------------------------------------------------------------------------
     def forward_loss(self, batch: Dict[str, torch.Tensor]) -> torch.Tensor:
@@ -126,15 +134,18 @@ class Trainer:
             from ..ops import hip_ops
             hip_ops.zero_arena_begin(self.ctx.device)
         try:
-            if chunks > 1:
-                loss = self._grad_cache_backward(batch, chunks)
-            else:
-                loss = self.forward_loss(batch)
-                with self.timer.phase("backward"):
-                    loss.backward()
+            with self.tune_region():
+                if chunks > 1:
+                    loss = self._grad_cache_backward(batch, chunks)
+                else:
+                    loss = self.forward_loss(batch)
+                    with self.timer.phase("backward"):
+                        loss.backward()
         finally:
             if arena:
                 hip_ops.zero_arena_end()
+                if self.global_step == 0:
+                    hip_ops.release_tuning_buffers()  # every shape of the step is tuned by now
         with self.timer.phase("allreduce_wait"):
             self.bucketer.finish()
         with self.timer.phase("optimizer"):
@@ -151,25 +162,44 @@ class Trainer:
     def grad_cache_chunks(self, video_batch: Optional[torch.Tensor] = None) -> int:
         """Micro-batches of the step: --grad_cache_chunks if set (0/1: one-shot), else (-1) the
         reference's one-shot step whenever its activations fit the device, else the fewest
-        GradCache chunks that do. Resolved once, on the first batch."""
+        GradCache chunks that do. Resolved once, on the first batch, and collectively: every rank
+        uses the largest count any rank needs (GradCache normalises BatchNorm per micro-batch, so
+        ranks with different counts would contribute gradients of different BN statistics)."""
         req = int(getattr(self.args, "grad_cache_chunks", 0) or 0)
         if req >= 0:
             return req
         if getattr(self, "_auto_chunks", None) is not None:
             return self._auto_chunks
         chunks = 0
-        if self.device.type == "cuda" and video_batch is not None:
+        if video_batch is not None:
             v = video_batch
             b = v.shape[0]
             t, h, w = (v.shape[1], v.shape[2], v.shape[3]) if v.shape[-1] in (3, 4) and v.dim() == 5 else \
                 (v.shape[2], v.shape[3], v.shape[4])
             est = self.GIB_PER_CLIP_32F200 * b * (t / 32.0) * (h * w / 200.0 ** 2) * 2 ** 30
-            free, total = torch.cuda.mem_get_info(self.device)
-            budget = 0.9 * total - (total - free)  # what this step may still allocate
-            if est > budget > 0:
-                chunks = int(min(b, -(-est // budget)))
+            budget = self._memory_budget()
+            if budget is not None:
+                if budget <= est / b:
+                    raise RuntimeError(f"--grad_cache_chunks -1: {budget / 2 ** 30:.2f} GiB left for the step, less than "
+                                       f"one clip's activations ({est / b / 2 ** 30:.3f} GiB); free device memory or "
+                                       f"lower --batch_size")
+                if est > budget:
+                    chunks = int(min(b, -(-est // budget)))
+        if self.ctx.world_size > 1:
+            chunks = int(pdist.all_reduce_max(float(chunks)))
         self._auto_chunks = chunks if chunks > 1 else 0
+        if self.ctx.is_main and getattr(self.args, "checkpoint_dir", ""):  # a real run's log, not bench / tests
+            log(f"grad_cache_chunks -1 resolved to {self._auto_chunks} "
+                f"({'one-shot step' if self._auto_chunks == 0 else 'GradCache micro-batches'})", self.args, 0)
         return self._auto_chunks
+
+    def _memory_budget(self) -> Optional[float]:
+        """Bytes this step may still allocate while keeping 10 % of the device free (None: no device
+        memory model, e.g. CPU)."""
+        if self.device.type != "cuda":
+            return None
+        free, total = torch.cuda.mem_get_info(self.device)
+        return 0.9 * total - (total - free)
 
     def _grad_cache_backward(self, batch: Dict[str, torch.Tensor], chunks: int) -> torch.Tensor:
         """GradCache two-pass step: the loss still sees every rank's

@@ -54,11 +54,12 @@ def main():
     tr.bucketer.zero()
     hip_ops.zero_arena_begin(ctx.device)
     try:
-        if chunks > 1:
-            loss = tr._grad_cache_backward(batch(0), chunks)
-        else:
-            loss = tr.forward_loss(batch(0))
-            loss.backward()
+        with tr.tune_region():  # kernel choices: rank 0's, on every rank
+            if chunks > 1:
+                loss = tr._grad_cache_backward(batch(0), chunks)
+            else:
+                loss = tr.forward_loss(batch(0))
+                loss.backward()
     finally:
         hip_ops.zero_arena_end()
     tr.bucketer.finish()
@@ -71,6 +72,9 @@ def main():
     torch.cuda.synchronize()
     flat_p = torch.cat([p.detach().reshape(-1).float().cpu() for p in tr.model.parameters()])
     torch.save(flat_p, os.path.join(out, f"param_w{W}_r{r}.pt"))
+    from mil_nce_howto100m_amd.ops import tune_sync
+    res["plan_hash"] = tune_sync.plan_hash()
+    res["tune_decisions"] = tune_sync.decisions()
     if W > 1:
         from mil_nce_howto100m_amd.parallel.comm_probe import probe
         res["comm"] = probe(tr.bucketer.flat.numel(), tr.bucketer.buckets, b_local * 3, 512, torch.float32,

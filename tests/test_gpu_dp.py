@@ -37,7 +37,7 @@ def _port():
     return p
 
 
-def _run(out, world, chunks):
+def _run(out, world, chunks, production=False):
     port = _port()
     procs = []
     for r in range(world):
@@ -50,6 +50,8 @@ def _run(out, world, chunks):
                     # another, and at random init the network amplifies bf16-level differences
                     # between the W=1 and W=2 kernel choices to several % of the gradient
                     "MILNCE_BOX": "0"})
+        if production:  # the bench's kernel set (box-tiled variants included)
+            env.pop("MILNCE_BOX")
         procs.append(subprocess.Popen([sys.executable, "-u", WORKER, out, str(chunks)], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
@@ -94,3 +96,19 @@ def test_two_ranks_on_gpu_match_single_process(chunks):
         assert r0[k] == r1[k]
     c = r0["comm"]
     assert c["world_size"] == 2 and c["buckets"] >= 2 and c["allreduce_ms"] > 0 and c["allgather_ms"] > 0
+
+
+def test_two_ranks_production_kernels_rank_consistent():
+    """Production defaults (box-tiled kernels in the tuner, as in bench.py): rank 0 tunes and every
+    rank launches its choices (ops/tune_sync), so both ranks hold the same plan and, after two real
+    train steps, bitwise identical parameters and losses."""
+    with tempfile.TemporaryDirectory() as out:
+        _run(out, 2, 0, production=True)
+        (r0, g0, p0), (r1, g1, p1) = _load(out, 2, 0), _load(out, 2, 1)
+    assert r0["plan_hash"] is not None and r0["plan_hash"] == r1["plan_hash"]
+    assert r0["tune_decisions"] == r1["tune_decisions"] > 0
+    assert torch.equal(g0, g1)
+    assert r0["loss"] == r1["loss"]
+    for k in ("train_loss1", "train_loss2"):
+        assert r0[k] == r1[k]
+    assert torch.equal(p0, p1)

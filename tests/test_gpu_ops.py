@@ -710,6 +710,29 @@ def test_softdtw_vs_cpu_oracle(dist, B, N, M, bw):
     assert rel_err(x.grad.cpu(), xc.grad) < 1e-3 and rel_err(y.grad.cpu(), yc.grad) < 1e-3
 
 
+def test_softdtw_euclidean_normalized_identical_rows():
+    """normalize=True puts exactly-zero distances on the xx / yy self cells (and identical rows make
+    x == y cells): the euclidean exp(||x - y||) gradient there is a zero subgradient on the GPU
+    (csrc/softdtw.hip dist_grad), finite and equal to the float64 oracle's."""
+    from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
+    torch.manual_seed(11)
+    base = torch.randn(3, 6, 16) * 0.2
+    x = base.clone().to(DEV).requires_grad_(True)
+    y = base.clone().to(DEV)
+    y[:, 3:] += 0.1 * torch.randn(3, 3, 16, device=DEV)  # half the rows identical, half not
+    y.requires_grad_(True)
+    sd = SoftDTW(True, gamma=0.1, normalize=True, dist_func="euclidean")
+    out = sd(x, y)
+    xc = x.detach().cpu().double().requires_grad_(True)
+    yc = y.detach().cpu().double().requires_grad_(True)
+    outc = sd(xc, yc)
+    assert torch.allclose(out.cpu().double(), outc, rtol=1e-3, atol=1e-3)
+    out.sum().backward()
+    outc.sum().backward()
+    assert torch.isfinite(x.grad).all() and torch.isfinite(y.grad).all()
+    assert rel_err(x.grad.cpu(), xc.grad) < 1e-2 and rel_err(y.grad.cpu(), yc.grad) < 1e-2
+
+
 @pytest.mark.parametrize("dist", ["negative_dot", "cosine"])
 def test_softdtw_pairwise_matches_batched(dist):
     """All b*b pairs from one GEMM with the distance fused (pairs layout: X / Y rows and their

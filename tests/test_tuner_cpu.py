@@ -72,7 +72,7 @@ def test_forward_tuner_pairs_variants_with_grid_sizes(monkeypatch):
     M, npad, bn = 256 * 8 * 50 * 50, 64, 64  # conv_2c dgrad: one 64-wide N tile
     seen = []
 
-    def fake_tune(launch, codes, default=None):
+    def fake_tune(launch, codes, default=None, sig=""):
         for c in codes:
             launch(c)
         return max(codes)  # the last (variant, grid) pair
