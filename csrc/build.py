@@ -32,7 +32,8 @@ ARCH = os.environ.get("MILNCE_ARCH", "gfx950")
 
 def flags(mode: str):
     f = ["--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-I" + HERE, "-Wno-unused-result"]
-    f += {"debug": ["-O1", "-g"], "check": ["-O3", "-DMILNCE_KCHECK"]}.get(mode, ["-O3"])
+    f += {"debug": ["-O1", "-g"], "check": ["-O3", "-DMILNCE_KCHECK"],
+          "trace": ["-O3", "-DBOX_TRACE=1"]}.get(mode, ["-O3"])
     return f
 
 
@@ -85,9 +86,10 @@ if __name__ == "__main__":
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 4))
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--check", action="store_true", help="build with the KASSERT kernel checks")
+    ap.add_argument("--trace", action="store_true", help="box conv phase timestamps (tools/box_trace.py)")
     a = ap.parse_args()
     try:
-        build(a.jobs, mode="check" if a.check else ("debug" if a.debug else "release"))
+        build(a.jobs, mode="check" if a.check else ("trace" if a.trace else ("debug" if a.debug else "release")))
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -52,6 +52,12 @@ static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per threa
 #ifndef BOX_ABLATE
 #define BOX_ABLATE 0
 #endif
+// Phase-timestamp diagnostics (libmilnce_hip_trace.so, tools/box_trace.py): every wave of the first
+// 64 workgroups records s_memtime at fixed points of its first tiles (lane e of two VGPRs holds
+// event e, so recording costs a compare and a select and no memory traffic until the kernel end).
+#ifndef BOX_TRACE
+#define BOX_TRACE 0
+#endif
 
 struct BoxGeo {
   int KS;          // 133 or 311
@@ -69,6 +75,7 @@ struct BoxGeo {
   int xld;              // row stride of x in elements (Cin, or the channel count of a concatenated
                         // tensor x is a channel slice of); pro_z / pro_y are dense (stride Cin)
   long long zbytes;     // bytes of the dense pro_z / pro_y tensors
+  uint32_t* trace;      // BOX_TRACE builds: per-wave phase timestamps (tools/box_trace.py), else null
 };
 
 // vmcnt wait with a runtime choice among compile-time counts (the counts must be exact)
@@ -199,6 +206,21 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 1, wc = wave & 1;
   const int nblocks = p.num_n_tiles * p.grid_m;
+  uint32_t tr_v0 = 0, tr_v1 = 0;
+  int tr_n = 0;
+  const unsigned long long tr_base = BOX_TRACE ? __builtin_amdgcn_s_memtime() : 0ull;
+  auto tev = [&]() {
+    if constexpr (BOX_TRACE != 0) {
+      if (tr_n < 128) {
+        const uint32_t t = (uint32_t)(__builtin_amdgcn_s_memtime() - tr_base);
+        if (lane == (tr_n & 63)) {
+          if (tr_n < 64) tr_v0 = t;
+          else tr_v1 = t;
+        }
+      }
+      ++tr_n;
+    }
+  };
   const int logical = xcd_remap(blockIdx.x, nblocks);
   const int n_tile = logical % p.num_n_tiles;
   const int m_slot = logical / p.num_n_tiles;
@@ -467,6 +489,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   }
 
   __syncthreads();  // setup writes visible
+  tev();
 
   // ---- prologue: first tile's box (cb 0), synchronously; first two weight stages ----
   TileInfo ti = tile_info(m_tile);
@@ -513,7 +536,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         if (cb > 0) bx_wait_c(kWaits.y[1][t]);
         else if (first_tile) bx_wait_c(kWaits.y[0][t]);
         else bx_wait_c(kWaits.y[2][t]);
+        tev();  // W: weight stage landed (this wave's share)
         ring_barrier();
+        tev();  // B: every wave at the ring barrier
         // fire stage s + STG - 1 into the slot read at the previous tap (continuing into the next
         // tile: the weights do not depend on the tile); a carried tile's first one is in flight
         if (!(t == 0 && carried)) fire((gs + STG - 1) % STG, (s + STG - 1) % nst_tile);
@@ -568,6 +593,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           __builtin_amdgcn_s_setprio(0);
         }
         ++gs;
+        tev();  // M: the tap's fragment reads and MFMAs issued
         if constexpr (XF_LAG >= 0 && PRO != 0) {
           // pieces whose transform falls on this tap (the block's last tap takes the rest)
           const int ka = max(t - XF_LAG, 0), kb = t == TAPS - 1 ? NBX : t - XF_LAG + 1;
@@ -577,7 +603,11 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       // every wave is done with this box: write the prefetched one (the next iteration's ring
       // barrier publishes it)
       lds_barrier();
-      if (!last_cb) box_store(cb + 1, ti, zrs);
+      tev();  // X: block end, every wave done with the box
+      if (!last_cb) {
+        box_store(cb + 1, ti, zrs);
+        tev();  // S: next block's box written
+      }
     }
 
     // ---- epilogue, two 128-row halves staged in the box region: waves wr 2h, 2h+1 write their
@@ -625,6 +655,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         }
       }
       lds_barrier();
+      tev();  // H1: the half's rows staged
       // every wave is past the tile's last MFMAs: the last stage's ring slot is free for the next
       // tile's stage STG - 1, fired ahead of the stores (so the stores drain behind it)
       if (half == 0) fire((gs + STG - 1) % STG, (STG - 1) % nst_tile);
@@ -681,7 +712,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           }
         }
       }
+      tev();  // H2: the half's stores issued
       lds_barrier();  // the half's rows are consumed before the region is rewritten
+      tev();  // H3
     }
     if constexpr ((BOX_ABLATE & 8) != 0) {
       lds_barrier();
@@ -689,6 +722,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     }
     // the next tile's first box (its loads were issued at the last block's first tap)
     if (has_next) box_store(0, tn, zrs);
+    tev();  // N: next tile's box written
 
     if (!has_next) break;
     m_tile = next_tile;
@@ -697,6 +731,15 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   }
   // drain: the trailing fires of the last tile and the epilogue stores
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (BOX_TRACE != 0) {
+    tev();  // end
+    if (g.trace != nullptr && blockIdx.x < 64) {
+      uint32_t* tb = g.trace + ((size_t)blockIdx.x * NWAVES + wave) * 130;
+      tb[lane] = tr_v0;
+      tb[64 + lane] = tr_v1;
+      if (lane == 0) { tb[128] = (uint32_t)tr_n; tb[129] = (uint32_t)ncb; }
+    }
+  }
   if constexpr (EPI != 0) {
     // per-thread column sums -> per column chunk over the row groups (fixed order)
     __syncthreads();
@@ -822,8 +865,16 @@ static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
 }
 
 // impl 14: 16x16x32 MFMA (N tiles 64 / 96 / 128 / 160), 15: 32x32x16 (N tiles 64 / 128 / 192)
+static uint32_t* g_box_trace = nullptr;
+// BOX_TRACE builds: the buffer ([64 workgroups][8 waves][130] uint32) the next box launches record to
+MILNCE_API int milnce_box_set_trace(void* buf) {
+  g_box_trace = (uint32_t*)buf;
+  return BOX_TRACE ? 0 : (int)hipErrorNotSupported;
+}
+
 int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream_t stream) {
   BoxGeo g;
+  g.trace = g_box_trace;
   int ntiles = 0;
   if (box_geo(p, g, ntiles) != 0) return V4_UNSUPPORTED;
   g.pro_ss = pro.ss;

@@ -176,7 +176,8 @@ template <int KT, int KH, int KW, int ST, int SH, int SW, bool BN = false, bool 
 __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, const bf16_t* __restrict__ x,
                                                      bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
                                                      uint32_t nout_chunks, const float* __restrict__ ss = nullptr,
-                                                     const float* __restrict__ gate = nullptr) {
+                                                     const float* __restrict__ gate = nullptr,
+                                                     bf16_t* __restrict__ yr = nullptr) {
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nout_chunks; i += gridDim.x * blockDim.x) {
     uint32_t r = fdiv(i, d.fcpr);
     const int c0 = (int)(i - r * d.fcpr.d) * 8;
@@ -204,12 +205,14 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
           const size_t off = in[t] ? ((size_t)(ti * p.H + hi) * p.W + wi) * p.C : 0;
           v[t] = *(const uint4*)(xb + off);
         }
-    float best[8], sc[8], sh[8], gv[8];
+    float best[8], sc[8], sh[8], gv[8], braw[8];
     uint32_t bi[8];
+    bool have_real = false;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       best[k] = -INFINITY;
       bi[k] = 0;
+      braw[k] = 0.f;
       if constexpr (BN) {
         sc[k] = ss[2 * p.C + c0 + k];
         sh[k] = ss[3 * p.C + c0 + k];
@@ -218,8 +221,14 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
     }
 #pragma unroll
     for (int t = 0; t < KT * KH * KW; ++t) {
-      float f[8];
+      float f[8], raw[8];
       unpack8(v[t], f);
+      if constexpr (BN && !GATE) {
+        // yr: the raw conv output at each arg-max (any real window cell when the maximum is a zero
+        // pad candidate: every real cell's z is 0 then, so its BN mask is off like the pad's)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) raw[k] = f[k];
+      }
       if constexpr (BN) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f)));  // = the stored z
@@ -234,7 +243,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
         const bool gt = val > best[k];
         best[k] = gt ? val : best[k];
         bi[k] = gt ? (uint32_t)t : bi[k];
+        if constexpr (BN && !GATE) braw[k] = ((gt && in[t]) || (in[t] && !have_real)) ? raw[k] : braw[k];
       }
+      have_real |= in[t];
     }
     const size_t o = (size_t)i * 8;
     *(uint4*)(y + o) = pack8(best);
@@ -242,6 +253,9 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
     a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
     a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
     *(uint2*)(arg + o) = a;
+    if constexpr (BN && !GATE) {
+      if (yr != nullptr) *(uint4*)(yr + o) = pack8(braw);  // exact: bf16 values
+    }
   }
 }
 
@@ -1132,7 +1146,7 @@ static bool is_s1_333(const PoolParams& p) {
 static bool g_pool_quad = true;
 
 static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s,
-                             const float* bn_ss = nullptr, const float* gate = nullptr) {
+                             const float* bn_ss = nullptr, const float* gate = nullptr, void* yr = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
   if (bn_ss != nullptr) {
@@ -1145,7 +1159,8 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
                            (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);               \
       else                                                                                                       \
         hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, false>), dim3(grid), dim3(256), 0, s, p, d,    \
-                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, nullptr);            \
+                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, nullptr,             \
+                           (bf16_t*)yr);                                                                         \
       return true;                                                                                               \
     }
     MILNCE_POOL_SHAPES(X)
@@ -1286,14 +1301,17 @@ MILNCE_API int milnce_maxpool_fwd(const void* x, void* y, void* arg, int B, int 
 
 // Train-mode BN + ReLU + max pool in one pass over the raw conv output (specialised window
 // shapes only; returns hipErrorInvalidValue otherwise).
+// yr (optional, pooled shape): the raw conv output x at each output's arg-max, so the BN-backward
+// partial sums of the pool input's BN can be taken over the pooled tensors (the consumer's dgrad
+// epilogue, csrc/conv.hip EPI 2) instead of a gather pass over the full-resolution x.
 MILNCE_API int milnce_bn_relu_maxpool_fwd(const void* x, const float* ss, void* y, void* arg, int B, int T, int H,
                                           int W, int C, int To, int Ho, int Wo, int kt, int kh, int kw, int st,
                                           int sh, int sw, int pt0, int pt1, int ph0, int ph1, int pw0, int pw1,
-                                          int zero_pad, hipStream_t stream) {
+                                          int zero_pad, void* yr, hipStream_t stream) {
   if (C % 8) return (int)hipErrorInvalidValue;
   PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
   const long long n = (long long)B * To * Ho * Wo * (C / 8);
-  if (!pool_fwd_special(p, x, y, arg, n, stream, ss)) return (int)hipErrorInvalidValue;
+  if (!pool_fwd_special(p, x, y, arg, n, stream, ss, nullptr, yr)) return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

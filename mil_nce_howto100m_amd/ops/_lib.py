@@ -42,7 +42,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_avgpool_bwd": [P, I, I, I, P, P],
     "milnce_maxpool_fwd": [P, P, P] + [I] * 21 + [P],
     "milnce_maxpool_bwd": [P, P, P] + [I] * 21 + [P, I, P, P, I, P],
-    "milnce_bn_relu_maxpool_fwd": [P, P, P, P] + [I] * 21 + [P],
+    "milnce_bn_relu_maxpool_fwd": [P, P, P, P] + [I] * 21 + [P, P],
     "milnce_maxpool_s1_bwd_fused": [P, P, P, P, P, P] + [I] * 5 + [P],
     "milnce_set_pool_s1_impl": [I],
     "milnce_set_pool_s1_maxthr": [I],
@@ -74,6 +74,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_rowstat": [P, L, I, I, P, P],
     "milnce_rowscale_add": [P, P, P, L, I, P],
     "milnce_dtw_path": [P, I, I, I, P, P, P],
+    "milnce_box_set_trace": [P],
 }
 
 # entry points that return something other than an int status

@@ -682,6 +682,12 @@ _LAZY_GATE_Z = os.environ.get("MILNCE_LAZY_GATE_Z", "1") != "0"
 #    ms/step; with the per-position gather it was 78.6 vs 78.3).
 _LAZY_GATE_DZ = os.environ.get("MILNCE_LAZY_GATE_DZ", "1") != "0"
 _LAZY_POOL_DZ = os.environ.get("MILNCE_LAZY_POOL_DZ", "1") != "0"
+# The stem's BN-backward partial sums from the pooled side: maxpool_2a's forward also stores the raw
+# stem output at each arg-max (yr, pooled shape) and tags its output with (yr, ss), so conv_2b's
+# dgrad epilogue (producer-BN partials, EPI 2) reduces sum_o dout_o mask(yr_o) (1, xhat(yr_o)) --
+# the same sums over the full-resolution dz -- and the partials-only gather pass over the stem
+# output (dout, arg-max and the 2.6 GB stem output read) disappears. MILNCE_POOL_YR=0 disables.
+_POOL_YR = os.environ.get("MILNCE_POOL_YR", "1") != "0"
 
 
 def _lazy_z(shape, device, bn_info) -> torch.Tensor:
@@ -1221,7 +1227,12 @@ class _ConvBNReLUPool(torch.autograd.Function):
         arg = torch.empty((B, To, Ho, Wo, C), dtype=torch.uint8, device=x.device)
         geo = [B, T, H, W, C, To, Ho, Wo, *pool_k, *pool_s, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
                pads[2][0], pads[2][1], 1]
-        call("milnce_bn_relu_maxpool_fwd", ptr(y), ptr(ss), ptr(out), ptr(arg), *geo, stream())
+        # the raw conv output at each arg-max: the consumer's dgrad epilogue then emits this BN's
+        # backward partial sums over the pooled gradient (see _POOL_YR)
+        yr = torch.empty_like(out) if (_POOL_YR and training and _FUSE_BN_BWD) else None
+        call("milnce_bn_relu_maxpool_fwd", ptr(y), ptr(ss), ptr(out), ptr(arg), *geo, ptr(yr), stream())
+        if yr is not None:
+            out._milnce_bn = (yr, ss, C)
         ctx.save_for_backward(x, weight, y, ss, gamma, arg)
         ctx.beta = beta
         ctx.training = bool(training)
@@ -1234,8 +1245,15 @@ class _ConvBNReLUPool(torch.autograd.Function):
         x, weight, y, ss, gamma, arg = ctx.saved_tensors
         geo = ctx.geo
         B, T, H, W, C = geo[:5]
+        pre = take_bn_partials(dout)  # from the consumer's dgrad epilogue over (dout, yr)
         dout = dout.contiguous()
         nparts = int(max(1, min(2048, _ceil(B * T * H * W * (C // 8), 256))))
+        if pre is not None and _LAZY_POOL_DZ:
+            # sum_i dz_i mask_i (1, xhat_i) = sum_o dout_o mask(yr_o) (1, xhat(yr_o)): no partials pass
+            dz = _lazy_dz((B, T, H, W, C), dout.device, ("pool", dout, arg, geo, None, None, nparts))
+            attach_bn_partials(dz, *pre)
+            dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
+            return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None
         part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
         if _LAZY_POOL_DZ and _FUSE_BN_BWD:
             # BN partial sums only; the BN backward re-gathers dz and applies itself in one pass

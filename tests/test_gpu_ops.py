@@ -606,6 +606,41 @@ def test_stem_bn_relu_pool_fused_matches_unfused():
     assert torch.equal(bns[0].running_mean, bns[1].running_mean)
 
 
+def _stem_pool_conv2b_grads(h, pool_yr, S=40):
+    old = h._POOL_YR
+    h._POOL_YR = pool_yr
+    try:
+        torch.manual_seed(19)
+        u8 = torch.randint(0, 256, (2, 6, S, S, 4), dtype=torch.uint8, device=DEV)
+        u8[..., 3] = 0
+        x = h.prepare_stem_input(u8, native=True, keep_u8=False)
+        conv = nn.Conv3d(3, 64, (3, 7, 7), 2, (1, 3, 3), bias=False).to(DEV)
+        conv2b = nn.Conv3d(64, 64, 1, bias=False).to(DEV)
+        bn1, bn2 = nn.BatchNorm3d(64).to(DEV), nn.BatchNorm3d(64).to(DEV)
+        with torch.no_grad():  # a BN whose mask cuts a real fraction of the values
+            bn1.bias.uniform_(-0.5, 0.5)
+            bn1.weight.uniform_(0.5, 1.5)
+        pooled = h.stem_conv_bn_relu_pool(x, conv.weight, bn1, True, (1, 3, 3), (1, 2, 2))
+        z = h.conv_bn_relu(pooled, conv2b.weight, bn2, (1, 1, 1), (0, 0, 0), True)
+        g = torch.randn(z.shape, device=DEV).to(torch.bfloat16)
+        z.backward(g)
+        return [pooled.detach().float(), conv.weight.grad, bn1.weight.grad, bn1.bias.grad, conv2b.weight.grad]
+    finally:
+        h._POOL_YR = old
+
+
+def test_stem_bn_partials_from_pooled_side():
+    """maxpool_2a stores the raw stem output at each arg-max and conv_2b's dgrad epilogue reduces the
+    stem BN's backward partial sums over (dout, yr) instead of a gather pass over the full-resolution
+    stem output: same forward, gradients equal up to the bf16 rounding of the gathered dz sums."""
+    h = hip()
+    a = _stem_pool_conv2b_grads(h, True)
+    b = _stem_pool_conv2b_grads(h, False)
+    assert torch.equal(a[0], b[0])
+    for u, v in zip(a[1:], b[1:]):
+        assert torch.isfinite(u).all() and rel_err(u, v) < 1e-2, rel_err(u, v)
+
+
 @pytest.mark.parametrize("S,u8", [(64, True), (64, False), (200, True)])
 def test_stem_wgrad_from_pool_gradient(S, u8):
     """Stem wgrad straight from the maxpool_2a backward (dy rebuilt per item from the pooled
