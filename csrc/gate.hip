@@ -98,6 +98,61 @@ __global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float
   }
 }
 
+// gsum[b, c] += sum over this block's rows of relu(y * scale + shift) for every (lazy) segment:
+// the SelfGating input sums of all branches of an Inception block in one pass (bn.hip
+// bn_relu_gsum_kernel per branch otherwise: four launches of a quarter of the work each, whose
+// ramp / tail dominated the small Mixed_4 / Mixed_5 planes). Same per-element value as that kernel
+// (fp32 relu before any bf16 rounding). Grid (splits, B); every thread owns one 8-channel chunk of
+// the concat row and walks rows of clip b with BN_U loads in flight.
+constexpr int GS_U = 4;
+__global__ __launch_bounds__(256) void gate_gsum_kernel(SegTable t, int Ctot, int thw, int rows_per_block,
+                                                        float* __restrict__ gsum) {
+  __shared__ float red[256 * 8];
+  const int cpr = Ctot >> 3, rpi = 256 / cpr, tid = threadIdx.x;
+  const int cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < rpi;
+  const int c = cc * 8;
+  const int s = seg_of(t, active ? c : 0);
+  const int C = t.off[s + 1] - t.off[s], cl = c - t.off[s];
+  const int b = blockIdx.y;
+  float sc[8], sh[8], acc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = active ? t.bn_ss[s][2 * C + cl + k] : 0.f;
+    sh[k] = active ? t.bn_ss[s][3 * C + cl + k] : 0.f;
+    acc[k] = 0.f;
+  }
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
+  if (active && r_begin + rr < r_end) {
+    const int ld = t.bn_ld[s];
+    const bf16_t* ys = t.bn_y[s] + (size_t)b * thw * ld + cl;
+    for (int r0 = r_begin + rr; r0 < r_end; r0 += GS_U * rpi) {
+      uint4 v[GS_U];
+#pragma unroll
+      for (int u = 0; u < GS_U; ++u) v[u] = *(const uint4*)(ys + (size_t)min(r0 + u * rpi, r_end - 1) * ld);
+#pragma unroll
+      for (int u = 0; u < GS_U; ++u) {
+        if (r0 + u * rpi >= r_end) break;
+        float f[8];
+        unpack8(v[u], f);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += fmaxf(f[k] * sc[k] + sh[k], 0.f);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
+  __syncthreads();
+  if (rr == 0 && active) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = acc[k];
+      for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
+      atomicAdd(gsum + (size_t)b * Ctot + c + k, v);
+    }
+  }
+}
+
 // dg[b, c] += sum over this block's rows of dout[r, c] * z[r, c]   (grid: splits x B)
 __global__ __launch_bounds__(256) void gate_bwd_reduce_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                               int Ctot, int thw, int rows_per_block,
@@ -438,10 +493,12 @@ static int grid_for(long long n) {
 
 // lazy (may be null): per-branch flag; a lazy branch's z is read as relu(bn_y * scale + shift)
 // from (bn_y[i], bn_ld[i], bn_ss[i]) instead of z[i].
+// gsum_pass != 0: gsum (zeroed by the caller) is first filled by ONE gate_gsum_kernel pass over
+// every branch's raw conv output (all branches must be lazy).
 MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z, const float* const* w,
-                               const float* const* bias, const float* gsum, int B, int thw, float* mean, float* g,
+                               const float* const* bias, float* gsum, int B, int thw, float* mean, float* g,
                                void* out, const int* lazy, const void* const* bn_y, const float* const* bn_ss,
-                               const int* bn_ld, hipStream_t stream) {
+                               const int* bn_ld, int gsum_pass, hipStream_t stream) {
   SegTable t = make_table(nseg, widths, z, nullptr, w, bias, nullptr, nullptr);
   for (int i = 0; i < nseg && lazy != nullptr; ++i) {
     t.lazy[i] = lazy[i];
@@ -452,6 +509,19 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
     }
   }
   const int Ctot = t.off[nseg];
+  if (gsum_pass) {
+    for (int i = 0; i < nseg; ++i)
+      if (lazy == nullptr || !lazy[i]) return (int)hipErrorInvalidValue;
+    if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
+    // >= ~4 workgroups per CU over the batch, >= 16 row iterations per thread
+    const int rpi = 256 / (Ctot / 8);
+    int splits = (1024 + B - 1) / B;
+    const int smax = (thw + 16 * rpi - 1) / (16 * rpi);
+    if (splits > smax) splits = smax;
+    if (splits < 1) splits = 1;
+    const int rpb = (thw + splits - 1) / splits;
+    hipLaunchKernelGGL(gate_gsum_kernel, dim3(splits, B), dim3(256), 0, stream, t, Ctot, thw, rpb, gsum);
+  }
   int cmax = 0;
   for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
   hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum,

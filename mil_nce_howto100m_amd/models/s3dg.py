@@ -112,13 +112,15 @@ class InceptionBlock(nn.Module):
         # (and the branch-3 pool reads it too: one fused op owning every read of x)
         units = (self.conv_b0, self.conv_b1_a, self.conv_b2_a)
         # z1 / z2 feed only the separable units: their BN + ReLU is applied by those convs' kernels
+        # the branches' SelfGating sums are taken in one pass over the block (ops.GSUM_DEFER)
+        gs = ops.GSUM_DEFER if g else False
         (z0, z1, z2), s0, pooled = ops.inception_head(x, [u.conv1.weight for u in units],
-                                                      [u.bn1 for u in units], self.training, want_gsum0=g,
+                                                      [u.bn1 for u in units], self.training, want_gsum0=gs,
                                                       lazy_out=(False, True, True))
         b0 = (z0, s0)
-        b1 = self.conv_b1_b(z1, want_gsum=g)
-        b2 = self.conv_b2_b(z2, want_gsum=g)
-        b3 = self.conv_b3_b(pooled, want_gsum=g)
+        b1 = self.conv_b1_b(z1, want_gsum=gs)
+        b2 = self.conv_b2_b(z2, want_gsum=gs)
+        b3 = self.conv_b3_b(pooled, want_gsum=gs)
         if not g:
             return torch.cat((z0, b1, b2, b3), dim=-1)
         gates = (self.gating_b0, self.gating_b1, self.gating_b2, self.gating_b3)

@@ -20,6 +20,11 @@ from . import aten
 _FORCE_ATEN = os.environ.get("MILNCE_OPS", "") == "aten"
 
 
+# want_gsum value of the Inception branches: their SelfGating sums may be computed by one pass over
+# the whole block inside gate_concat instead of one pass per branch (hip_ops.GSUM_DEFER)
+GSUM_DEFER = 2
+
+
 def use_hip(t: torch.Tensor) -> bool:
     return t.is_cuda and not _FORCE_ATEN
 

@@ -33,7 +33,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
     "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, I, I, P],
-    "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, P],
+    "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P],
     "milnce_gate_bwd_reduce": [I, P, P, P, P, I, I, P, P],
     "milnce_gate_fc_bwd": [I, P, P, P, P, P, P, P, I, I, P, P],
     "milnce_pool_set_quad": [I],
@@ -75,6 +75,8 @@ SIGNATURES: Dict[str, list] = {
     "milnce_rowscale_add": [P, P, P, L, I, P],
     "milnce_dtw_path": [P, I, I, I, P, P, P],
     "milnce_box_set_trace": [P],
+    "milnce_twgrad_plan": [I] * 8 + [P, P],
+    "milnce_twgrad": [P, I, P, P, P, I] + [I] * 9 + [P],
 }
 
 # entry points that return something other than an int status

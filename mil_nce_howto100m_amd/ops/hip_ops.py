@@ -672,6 +672,15 @@ _FUSE_BN_BWD = True
 # the gating sums, returns a stride-0 placeholder tagged with (y, ss, ld), and the gate applies
 # relu(y * scale + shift) while scaling (csrc/gate.hip lazy segments).
 _LAZY_GATE_Z = os.environ.get("MILNCE_LAZY_GATE_Z", "1") != "0"
+# want_gsum == GSUM_DEFER (the Inception branches): a lazy branch's SelfGating sums are not computed
+# by its own gsum-only pass but by ONE pass over all four branches of the block inside gate_concat
+# (csrc/gate.hip gate_gsum_kernel). MILNCE_BATCH_GSUM=0 keeps the per-branch passes.
+GSUM_DEFER = 2
+_BATCH_GSUM = os.environ.get("MILNCE_BATCH_GSUM", "1") != "0"
+
+
+def _defer_gsum(want) -> bool:
+    return _BATCH_GSUM and int(want) == GSUM_DEFER
 # Gradients that only feed their producer's BN backward are not stored either ("lazy dz"):
 #  * SelfGating inputs: the gate backward computes only the BN partial sums and the BN backward
 #    rebuilds dz = bf16(dout * g + dmean / thw) from dout (milnce_bn_bwd_gate);
@@ -925,6 +934,43 @@ def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: Optional[torch.Tensor], 
     return slab, geo[1], _ceil(plan.Cout, 64) * 64, kt * kh * kw * plan.Cin
 
 
+# Temporal box wgrad (csrc/conv_twgrad.hip): (3,1,1) / stride 1 / padding (1,0,0) convs, output tiles
+# of 64 / 128 / 192 channels x 64 input channels x 3 taps, boxes of 64 (frame, position) rows with
+# their 3-frame halo staged once through a counted 3-deep LDS-DMA ring. In the wgrad tuner next to
+# the im2col / halo kernels (impl codes 1000 + N tile); MILNCE_TWGRAD=0 leaves it out.
+_TWGRAD = os.environ.get("MILNCE_TWGRAD", "1") != "0"
+_TW_OCCS = (1, 2)
+_TW_SPLITS: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
+
+
+def _twgrad_ok(plan: ConvPlan, x: torch.Tensor) -> bool:
+    return (_TWGRAD and x.dtype == BF16 and plan.k == (3, 1, 1) and plan.s == (1, 1, 1) and plan.p == (1, 0, 0)
+            and not plan.wo_override and plan.Cin % 8 == 0 and plan.Cin == plan.Cin_p and plan.Cout % 8 == 0)
+
+
+def _tw_tiles(cout: int) -> Tuple[int, ...]:
+    """Output tiles worth trying: no more than one 64-wide tile of padding."""
+    return tuple(bn for bn in (192, 128, 64) if _ceil(cout, bn) * bn - cout < 64)
+
+
+def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accumulate: int, occ: int = 1):
+    """Temporal box wgrad; with ``target`` None only the split slab is filled and
+    (slab, splits, Npad, Kpad) of the pending reduction is returned."""
+    key = (id(plan), bn, occ)
+    geo = _TW_SPLITS.get(key)
+    if geo is None:
+        floats, splits = ctypes.c_longlong(0), ctypes.c_int(0)
+        rc = lib().milnce_twgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, bn, occ * _NUM_CU,
+                                      ctypes.byref(floats), ctypes.byref(splits))
+        if rc != 0:
+            raise RuntimeError(f"temporal wgrad plan failed ({rc}) for {plan}")
+        geo = _TW_SPLITS[key] = (int(floats.value), int(splits.value))
+    slab = torch.empty((geo[0],), dtype=F32, device=dy.device)
+    call("milnce_twgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target) if target is not None else None,
+         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, bn, geo[1], stream())
+    return slab, geo[1], _ceil(plan.Cout, bn) * bn, 3 * plan.Cin
+
+
 # Deferred slab reductions (conv_wgrad(defer=True)): the split-K reduce of a parameter's wgrad is
 # a small latency-bound kernel (~17 us, 58 per flagship step) that nothing in the backward pass
 # waits for, so it can run on a side stream overlapping the next layer's kernels; grad_sink.drain()
@@ -980,6 +1026,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     def launch_with(tn, impl, occ, tk, target, accumulate):
         """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
         (slab, splits, Npad, Kpad) returned for the caller's reduction."""
+        if impl >= 1000:  # temporal box wgrad, N tile impl - 1000
+            return _twgrad(dy, x, plan, impl - 1000, target, accumulate, occ)
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
             return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, tk, occ)
@@ -1005,6 +1053,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 cands += [(64, 164, occ, 0) for occ in _HALO_OCCS]
                 if plan.k == (3, 1, 1) and plan.Cin % 128 == 0:  # temporal boxes also take 128-channel chunks
                     cands += [(64, 228, occ, 0) for occ in _HALO_OCCS]
+            if _twgrad_ok(plan, x):
+                cands += [(bn, 1000 + bn, occ, 0) for bn in _tw_tiles(plan.Cout) for occ in _TW_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4, plan.w_tk)
@@ -1184,10 +1234,13 @@ class _ConvBNReLU(torch.autograd.Function):
         if lazy_out and not want_gsum and _PRO_FUSE:
             z = _pro_z(y.shape, y.device, (y, ss, C))  # applied by the consuming conv
         else:
-            lazy = want_gsum and _LAZY_GATE_Z
+            lazy = bool(want_gsum) and _LAZY_GATE_Z
             z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
-            call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
-                 plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
+            if lazy and _defer_gsum(want_gsum):
+                gsum._milnce_gsum_deferred = True  # summed with the block's other branches (gate_concat)
+            else:
+                call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
+                     plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
         ctx.save_for_backward(x_saved, weight, y, ss, gamma)
         ctx.beta = beta  # parameter handle only (its gradient buffer may be written in place)
         ctx.training = bool(training)
@@ -1279,7 +1332,7 @@ def conv_bn_relu(x, weight, bn, stride, padding, training: bool, want_gsum: bool
     momentum = bn.momentum if bn.momentum is not None else 0.1
     need_z = torch.is_grad_enabled() and weight.requires_grad  # the wgrad reads the (fused) input
     out = _ConvBNReLU.apply(x, weight, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                            tuple(stride), tuple(padding), momentum, bn.eps, bool(training), bool(want_gsum), 0,
+                            tuple(stride), tuple(padding), momentum, bn.eps, bool(training), int(want_gsum), 0,
                             bool(lazy_out), bool(need_z))
     return out
 
@@ -1402,8 +1455,11 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
         else:
             lazy = g is not None and _LAZY_GATE_Z
             z = _lazy_z(zshape, dev, (ysl, ss, ctot)) if lazy else torch.empty(zshape, dtype=BF16, device=dev)
-            call("milnce_bn_relu_apply", ptr(ysl), ctot, None if lazy else ptr(z), c, ptr(ss), c, plan.B, thw,
-                 ptr(g), stream())
+            if lazy and _defer_gsum(want_gsum0):
+                g._milnce_gsum_deferred = True  # summed with the block's other branches (gate_concat)
+            else:
+                call("milnce_bn_relu_apply", ptr(ysl), ctot, None if lazy else ptr(z), c, ptr(ss), c, plan.B, thw,
+                     ptr(g), stream())
         z._milnce_bn = (ysl, ss, ctot)
         zs.append(z)
         sss.append(ss)
@@ -1493,7 +1549,7 @@ def conv1x1_group_bn_relu(x, weights, bns, training: bool, want_gsum0: bool = Fa
     for bn in bns:
         args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
     hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
-    return _Conv1x1GroupBNReLU.apply(x, len(weights), bool(training), bool(want_gsum0), hyper, *args)
+    return _Conv1x1GroupBNReLU.apply(x, len(weights), bool(training), int(want_gsum0), hyper, *args)
 
 
 class _InceptionHead(torch.autograd.Function):
@@ -1554,7 +1610,7 @@ def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False, la
     for bn in bns:
         args += [bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.num_batches_tracked]
     hyper = tuple((bn.momentum if bn.momentum is not None else 0.1, bn.eps) for bn in bns)
-    return _InceptionHead.apply(x, len(weights), bool(training), bool(want_gsum0), hyper,
+    return _InceptionHead.apply(x, len(weights), bool(training), int(want_gsum0), hyper,
                                 tuple(bool(v) for v in lazy_out), *args)
 
 
@@ -1621,11 +1677,12 @@ class _GateConcat(torch.autograd.Function):
         out = torch.empty((B, T, H, W, ctot), dtype=BF16, device=dev)
         lazy = [int(_is_lazy(z)) for z in zs]
         bn_info = [z._milnce_bn if _is_lazy(z) else (None, None, 0) for z in zs]
+        gsum_pass = int(bool(getattr(gsum, "_milnce_gsum_deferred", False)))  # all branches summed here
         call("milnce_gate_fwd", nseg, _arr(ctypes.c_int, widths), _arr(ctypes.c_void_p, [ptr(z) for z in zs]),
              _arr(ctypes.c_void_p, [ptr(w) for w in ws]), _arr(ctypes.c_void_p, [ptr(b) for b in bs]),
              ptr(gsum), B, thw, ptr(mean), ptr(g), ptr(out), _arr(ctypes.c_int, lazy),
              _arr(ctypes.c_void_p, [ptr(i[0]) for i in bn_info]), _arr(ctypes.c_void_p, [ptr(i[1]) for i in bn_info]),
-             _arr(ctypes.c_int, [int(i[2]) for i in bn_info]), stream())
+             _arr(ctypes.c_int, [int(i[2]) for i in bn_info]), gsum_pass, stream())
         ctx.save_for_backward(*zs, *ws, g, mean)
         ctx.nseg, ctx.widths, ctx.thw = nseg, widths, thw
         ctx.bs = bs  # parameter handles only (their gradient buffers may be written in place)
@@ -1685,7 +1742,19 @@ def gate_concat(branches, fc_weights, fc_biases, gsums=None):
                 for b in branches]
     if gsums is None or any(s is None for s in gsums):
         gsums = [b.float().sum(dim=(1, 2, 3)) for b in branches]
-    gsum = gsums[0] if len(gsums) == 1 else torch.cat(gsums, dim=1)
+    deferred = [bool(getattr(s, "_milnce_gsum_deferred", False)) for s in gsums]
+    if all(deferred) and all(_is_lazy(b) for b in branches):
+        # every branch's sums in one pass inside the gate forward (gsum_pass)
+        gsum = _zeros_f32((branches[0].shape[0], sum(int(b.shape[-1]) for b in branches)), branches[0].device)
+        gsum._milnce_gsum_deferred = True
+    else:
+        for s, b, d in zip(gsums, branches, deferred):
+            if d:  # a deferred branch next to non-deferred ones: its own gsum-only pass now
+                y, ss, ld = b._milnce_bn
+                C = int(b.shape[-1])
+                call("milnce_bn_relu_apply", ptr(y), ld, None, C, ptr(ss), C, b.shape[0],
+                     b.numel() // (b.shape[0] * C), ptr(s), stream())
+        gsum = gsums[0] if len(gsums) == 1 else torch.cat(gsums, dim=1)
     return _GateConcat.apply(len(branches), gsum.contiguous(), *branches, *fc_weights, *fc_biases)
 
 
@@ -1778,7 +1847,7 @@ class _GatedPool(torch.autograd.Function):
         g = torch.empty((B, C), dtype=F32, device=dev)
         call("milnce_gate_fwd", 1, _arr(ctypes.c_int, [C]), _arr(ctypes.c_void_p, [0]), _arr(ctypes.c_void_p, [ptr(w)]),
              _arr(ctypes.c_void_p, [ptr(bias)]), ptr(gsum), B, T * H * W, ptr(mean), ptr(g), None, None, None, None,
-             None, stream())
+             None, 0, stream())
         pads = aten.tf_same_pad(kernel, stride)
         To = _pool_out(T, kernel[0], stride[0], *pads[0])
         Ho = _pool_out(H, kernel[1], stride[1], *pads[1])

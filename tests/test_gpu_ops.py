@@ -1147,3 +1147,53 @@ def test_step_weight_prepack_matches_per_call_pack():
         h._PACKER.entries.clear()
         h._PACKER.descs = None
 
+
+
+@pytest.mark.parametrize("B,T,HW,cin,cout", [(4, 8, 50, 192, 192), (4, 8, 25, 128, 128), (4, 4, 13, 96, 208),
+                                             (8, 2, 7, 384, 384), (3, 5, 9, 24, 40), (2, 16, 10, 64, 64)])
+@pytest.mark.parametrize("bn", [64, 128, 192])
+def test_temporal_box_wgrad(B, T, HW, cin, cout, bn):
+    """csrc/conv_twgrad.hip (3,1,1) weight gradient (boxes of frames x flattened positions with a
+    3-frame halo, 64/128/192-wide output tiles, partial boxes / channel chunks / output tiles) vs the
+    fp32 F.conv3d weight gradient of the same bf16 operands; slab + accumulate paths."""
+    h = hip()
+    torch.manual_seed(B * 131 + T * 7 + cin + cout + bn)
+    x = torch.randn(B, T, HW, HW, cin, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(B, T, HW, HW, cout, device=DEV).to(torch.bfloat16)
+    plan = h.conv_plan(x.shape, (cout, cin, 3, 1, 1), (1, 1, 1), (1, 0, 0))
+    ref = torch.nn.grad.conv3d_weight(x.permute(0, 4, 1, 2, 3).float(), (cout, cin, 3, 1, 1),
+                                      dy.permute(0, 4, 1, 2, 3).float(), padding=(1, 0, 0))
+    out = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
+    h._twgrad(dy, x, plan, bn, out, 0)
+    assert rel_err(out, ref) < 1e-4, rel_err(out, ref)
+    h._twgrad(dy, x, plan, bn, out, 1, occ=2)  # accumulate, another split count
+    assert rel_err(out, 2 * ref) < 1e-4
+
+
+def _inception_block_run(h, batch_gsum):
+    from mil_nce_howto100m_amd.models.s3dg import InceptionBlock
+    old = h._BATCH_GSUM
+    h._BATCH_GSUM = batch_gsum
+    try:
+        torch.manual_seed(23)
+        blk = InceptionBlock(192, 64, 96, 128, 16, 32, 32).to(DEV).train()
+        x = torch.randn(4, 4, 13, 13, 192, device=DEV).to(torch.bfloat16).requires_grad_(True)
+        out = blk(x)
+        g = torch.randn(out.shape, device=DEV).to(torch.bfloat16)
+        out.backward(g)
+        grads = [p.grad.detach().clone() for p in blk.parameters()]
+        return out.detach().float(), x.grad.detach().float(), grads
+    finally:
+        h._BATCH_GSUM = old
+
+
+def test_batched_block_gating_sums():
+    """The four branches' SelfGating sums taken in one pass over the block inside the gate forward
+    (csrc/gate.hip gate_gsum_kernel) vs one gsum-only pass per branch: the same block output and
+    gradients (the sums differ only in fp32 atomic order)."""
+    h = hip()
+    oa, xa, ga = _inception_block_run(h, True)
+    ob, xb, gb = _inception_block_run(h, False)
+    assert rel_err(oa, ob) < 1e-3 and rel_err(xa, xb) < 1e-2
+    for u, v in zip(ga, gb):
+        assert rel_err(u, v) < 1e-2

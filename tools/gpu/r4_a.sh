@@ -4,9 +4,11 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 D=gpurun_out/${1:-r4a}
 mkdir -p $D
-timeout -k 10 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_ops.py -x -v -m gpu -k "dp or two_ranks or softdtw_euclidean or stem or pool" --timeout 240 --timeout-method thread > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_dp.py tests/test_gpu_ops.py -x -v -m gpu -k "dp or two_ranks or softdtw_euclidean or stem or pool or temporal_box_wgrad or batched_block or lazy_gate or gated_pool" --timeout 240 --timeout-method thread > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
 tail -3 $D/pytest.log
 bash tools/gpu/box_trace.sh ${1:-r4a}/trace
+timeout -k 10 300 python tools/halo_bench.py > $D/halo_bench.txt 2>&1 || { tail -20 $D/halo_bench.txt; exit 1; }
+grep -v amdgpu.ids $D/halo_bench.txt
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $D/bench.log 2>&1 || { tail -30 $D/bench.log; exit 1; }
 tail -1 $D/bench.log | cut -c1-400
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $D/prof -o run --output-format csv -- python bench.py --steps 3 --warmup 2 > $D/prof.log 2>&1 || { tail -20 $D/prof.log; exit 1; }

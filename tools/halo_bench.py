@@ -11,7 +11,9 @@ from mil_nce_howto100m_amd.ops import hip_ops as h  # noqa: E402
 SHAPES = [(256, 8, 50, 50, 64, 192, (1, 3, 3)), (256, 8, 50, 50, 192, 192, (3, 1, 1)),
           (256, 8, 25, 25, 128, 192, (1, 3, 3)), (256, 8, 25, 25, 96, 128, (1, 3, 3)),
           (256, 8, 25, 25, 192, 192, (3, 1, 1)), (256, 4, 13, 13, 160, 320, (1, 3, 3)),
-          (256, 4, 13, 13, 320, 320, (3, 1, 1)), (256, 2, 7, 7, 192, 384, (1, 3, 3))]
+          (256, 4, 13, 13, 320, 320, (3, 1, 1)), (256, 2, 7, 7, 192, 384, (1, 3, 3)),
+          (256, 8, 25, 25, 128, 128, (3, 1, 1)), (256, 4, 13, 13, 288, 288, (3, 1, 1)),
+          (256, 2, 7, 7, 384, 384, (3, 1, 1))]
 
 
 def timeit(fn, iters=10):
@@ -40,4 +42,9 @@ for B, T, H, W, Cin, Cout, k in SHAPES:
     for cc in ((64,) if k[0] == 1 else (128, 64)):
         t = timeit(lambda: h._halo_wgrad(dy, x, plan, cc, out, 0))
         res.append(f"halo cc{cc} {t:.3f} ms {fl / t / 1e9:.0f} TF/s")
+    if k == (3, 1, 1):  # temporal box wgrad (csrc/conv_twgrad.hip), output tile x workgroups per CU
+        for bn in h._tw_tiles(Cout):
+            for occ in (1, 2):
+                t = timeit(lambda: h._twgrad(dy, x, plan, bn, out, 0, occ))
+                res.append(f"tw{bn}/o{occ} {t:.3f} ms {fl / t / 1e9:.0f} TF/s")
     print(f"{(B, T, H, W, Cin)}->{Cout} k{k}: " + " | ".join(res), flush=True)
