@@ -56,8 +56,9 @@ __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int n
 
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
-    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
-    float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */) {
+    const float* __restrict__ beta, float* rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
+    float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */,
+    float* yshift) {
   const int c = blockIdx.x * FIN_CH + threadIdx.x % FIN_CH;
   if (training && blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
   double s, q;
@@ -71,7 +72,14 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(
     mean = (float)m;
     var = (float)v;
     const double unbiased = count > 1.0 ? v * count / (count - 1.0) : v;
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+    // yshift: the per-channel shift the conv epilogue subtracted before rounding (the statistics
+    // and `mean` are those of the stored, shifted values, which is what apply / backward read);
+    // the running mean gets the true mean. yshift may be rmean itself; a separate buffer (a fused
+    // group's concatenated shifts) is advanced to the new running mean for the next step.
+    const float sh = yshift != nullptr ? yshift[c] : 0.f;
+    const float rm = (1.f - momentum) * rmean[c] + momentum * (mean + sh);
+    rmean[c] = rm;
+    if (yshift != nullptr && yshift != rmean) yshift[c] = rm;
     rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
   } else {
     mean = rmean[c];
@@ -291,10 +299,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
 // ---------------------------------------------------------------------------------------
 MILNCE_API int milnce_bn_finalize(const float* part, int nparts, int Npad, int C, double count, const float* gamma,
                                   const float* beta, float* rmean, float* rvar, long long* nbt, float momentum,
-                                  float eps, int training, float* out, hipStream_t stream) {
+                                  float eps, int training, float* out, float* yshift, hipStream_t stream) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream, part,
                      nparts, Npad, C,
-                     count, gamma, beta, rmean, rvar, nbt, momentum, eps, training, out);
+                     count, gamma, beta, rmean, rvar, nbt, momentum, eps, training, out, training ? yshift : nullptr);
   return (int)hipGetLastError();
 }
 

@@ -34,6 +34,8 @@ def flags(mode: str):
     f = ["--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-I" + HERE, "-Wno-unused-result"]
     f += {"debug": ["-O1", "-g"], "check": ["-O3", "-DMILNCE_KCHECK"],
           "trace": ["-O3", "-DBOX_TRACE=1"]}.get(mode, ["-O3"])
+    if mode.startswith("def_"):  # A/B libraries: def_NAME=VALUE[,NAME=VALUE] (python csrc/build.py --define ...)
+        f += ["-D" + d for d in mode[4:].split(",")]
     return f
 
 
@@ -87,9 +89,13 @@ if __name__ == "__main__":
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--check", action="store_true", help="build with the KASSERT kernel checks")
     ap.add_argument("--trace", action="store_true", help="box conv phase timestamps (tools/box_trace.py)")
+    ap.add_argument("--define", default="", help="NAME=VALUE[,...]: an A/B library libmilnce_hip_def_....so")
     a = ap.parse_args()
     try:
-        build(a.jobs, mode="check" if a.check else ("trace" if a.trace else ("debug" if a.debug else "release")))
+        if a.define:
+            build(a.jobs, mode="def_" + a.define)
+        else:
+            build(a.jobs, mode="check" if a.check else ("trace" if a.trace else ("debug" if a.debug else "release")))
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

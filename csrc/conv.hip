@@ -156,12 +156,20 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
   }
   float st_s[TN][4], st_q[TN][4];
   float e_s[8], e_q[8];  // EPI 2: partials of this thread's fixed 8-channel chunk (tid % (BN/8))
+  // EPI 1: per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
+  // rounding, so the stored pre-BN values keep their precision when |mean| >> std
+  float shv[TN][4];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { st_s[j][r] = 0.f; st_q[j][r] = 0.f; }
+    for (int r = 0; r < 4; ++r) {
+      st_s[j][r] = 0.f;
+      st_q[j][r] = 0.f;
+      const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4 + r;
+      shv[j][r] = (EPI == 1 && p.bn_ss != nullptr && n < p.Cout) ? p.bn_ss[n] : 0.f;
+    }
 
   for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
     const int m0 = m_tile * BM;
@@ -255,8 +263,10 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_kernel(ConvParams p) {
       const bool rv = (m0 + row) < p.M;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 v = acc[j][i];
+        f32x4 v = acc[j][i];
         if constexpr (EPI == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] -= shv[j][r];
           if (rv) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
@@ -610,12 +620,26 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ring_barrier();  // every wave done reading the ring before the epilogue reuses it
 
+    // EPI 1: per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
+    // rounding, so the stored pre-BN values keep their precision when |mean| >> std
+    float shv[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4 + r;
+        shv[j][r] = (EPI == 1 && p.bn_ss != nullptr && n < p.Cout) ? p.bn_ss[n] : 0.f;
+      }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wr * WM + i * 16 + (lane & 15);
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const f32x4 v = acc[j][i];
+        f32x4 v = acc[j][i];
+        if constexpr (EPI == 1) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] -= shv[j][r];
+        }
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
         o.y = pack2bf(v[2], v[3]);
@@ -1604,6 +1628,7 @@ struct StemFwdParams {
   const bf16_t* w;   // packed [64][Kpad] bf16
   bf16_t* y;         // [M, 64]
   float* stats;      // [gridDim][2][64]
+  const float* shift;  // [64] subtracted before the bf16 rounding (the BN's running mean) or null
   int B, T, H, To, Ho, Kpad;
   int nitems;
   long long x_bytes;
@@ -1713,11 +1738,15 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
   const char* Wb = (const char*)Ws;
   const char* Xb = (const char*)smem;
 
-  float s1[2][4], s2[2][4];
+  float s1[2][4], s2[2][4], shv[2][4];
 #pragma unroll
   for (int nf = 0; nf < 2; ++nf)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s1[nf][r] = 0.f; s2[nf][r] = 0.f; }
+    for (int r = 0; r < 4; ++r) {
+      s1[nf][r] = 0.f;
+      s2[nf][r] = 0.f;
+      shv[nf][r] = p.shift != nullptr ? p.shift[nh * 32 + nf * 16 + lg * 4 + r] : 0.f;
+    }
 
   int it = blockIdx.x;
   if (it < p.nitems) {
@@ -1761,8 +1790,8 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
         for (int nf = 0; nf < 2; ++nf) {
           const f32x4 v = acc[nf][j];
           uint2 o;
-          o.x = pack2bf(v[0], v[1]);
-          o.y = pack2bf(v[2], v[3]);
+          o.x = pack2bf(v[0] - shv[nf][0], v[1] - shv[nf][1]);
+          o.y = pack2bf(v[2] - shv[nf][2], v[3] - shv[nf][3]);
           *(uint2*)(p.y + (m0 + pos) * 64 + nh * 32 + nf * 16 + lg * 4) = o;
           const float q0 = __uint_as_float(o.x << 16), q1 = __uint_as_float(o.x & 0xffff0000u);
           const float q2 = __uint_as_float(o.y << 16), q3 = __uint_as_float(o.y & 0xffff0000u);
@@ -2041,6 +2070,10 @@ static int conv_fwd_impl(const void* x, int x_u8, const void* w, void* y, float*
   return (int)hipErrorInvalidValue;
 }
 
+// stats set, bn_y null (BN forward statistics, epilogue mode 1): bn_ss, when set, is a per-channel
+// shift [Cout] (the BN's running mean) subtracted from the outputs before their bf16 rounding; the
+// statistics are those of the shifted values and milnce_bn_finalize adds the shift back.
+// bn_y set: mode 2 (dgrad with the producer BN's backward partials), bn_ss = its [4][C] constants.
 MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, float* stats, const void* bn_y,
                                const float* bn_ss, int bn_ld,
                                int B, int T, int H, int W, int Cin, int Cout,
@@ -2057,7 +2090,8 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 // x_ld: x's row stride in elements (x may be a channel slice of a concatenated conv output).
 // Box-tiled variants only (impl 14 / 15); anything else returns V4_UNSUPPORTED.
 MILNCE_API int milnce_conv_fwd_pro(const void* x, int x_ld, const void* w, void* y, float* stats,
-                                   const float* pro_ss, void* pro_z, int B, int T, int H, int W, int Cin, int Cout,
+                                   const float* y_shift, const float* pro_ss, void* pro_z, int B, int T, int H,
+                                   int W, int Cin, int Cout,
                                    int KT, int KH, int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy,
                                    int bn, int grid_m, int impl, hipStream_t stream) {
   if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
@@ -2065,7 +2099,7 @@ MILNCE_API int milnce_conv_fwd_pro(const void* x, int x_ld, const void* w, void*
   pro.ss = pro_ss;
   pro.z = pro_z;
   pro.xld = x_ld;
-  return conv_fwd_impl(x, 0, w, y, stats, nullptr, nullptr, 0, B, T, H, W, Cin, Cout, KT, KH, KW, 1, 1, 1, pt, ph,
+  return conv_fwd_impl(x, 0, w, y, stats, nullptr, y_shift, 0, B, T, H, W, Cin, Cout, KT, KH, KW, 1, 1, 1, pt, ph,
                        pw, Kpad, Npad, ldy, bn, 64, grid_m, 0, impl, pro, stream);
 }
 
@@ -2314,9 +2348,10 @@ MILNCE_API int milnce_stem_wgrad_pool(const void* pdy, const void* parg, const v
 // returns the number of partial rows written (> 0), STEM_UNSUPPORTED (-1) for geometries it does
 // not cover (the caller falls back to the generic implicit GEMM), or -1000 - hipError on a launch error.
 MILNCE_API int milnce_stem_fwd(const void* x2, int x_u8, const void* wpacked, int Kpad, void* y, float* stats,
-                               long long stats_floats, int B, int T, int H, int W2, hipStream_t stream) {
+                               long long stats_floats, const float* shift, int B, int T, int H, int W2,
+                               hipStream_t stream) {
   StemFwdParams p;
-  p.x = (const bf16_t*)x2; p.w = (const bf16_t*)wpacked; p.y = (bf16_t*)y; p.stats = stats;
+  p.x = (const bf16_t*)x2; p.w = (const bf16_t*)wpacked; p.y = (bf16_t*)y; p.stats = stats; p.shift = shift;
   p.B = B; p.T = T; p.H = H; p.Kpad = Kpad;
   p.To = (T + 2 - 3) / 2 + 1;
   p.Ho = (H + 6 - 7) / 2 + 1;

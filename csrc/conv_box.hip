@@ -35,6 +35,7 @@
 
 #include <algorithm>
 #include <type_traits>
+#include <utility>
 
 static constexpr int BX_BM = 256;        // output rows per tile: 4 waves along M x 64 rows
 static constexpr int BX_BK = 64;         // channels per box / K stage
@@ -57,6 +58,12 @@ static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per threa
 // event e, so recording costs a compare and a select and no memory traffic until the kernel end).
 #ifndef BOX_TRACE
 #define BOX_TRACE 0
+#endif
+// EPI 2 epilogue rows prefetched into L2 during the last block (y_prefetch). Off: the A/B
+// (gpurun_out r4ypf) measured 4351 / 4355 pairs/s without it against 4323 / 4335 with it (the
+// EPI 2 variants spill more and the (1,3,3) dgrad of conv_2c went 2.24 -> 2.55 ms)
+#ifndef BOX_YPF
+#define BOX_YPF 0
 #endif
 
 struct BoxGeo {
@@ -99,6 +106,46 @@ __device__ __forceinline__ void bx_wait_bs(uint32_t n) {
 }
 __device__ __forceinline__ void bx_wait_c(int n) { bx_wait_bs<0, 63>((uint32_t)n); }
 
+// Epilogue staging LDS accesses as inline asm: the compiler treats every LDS access it can see
+// after an LDS-DMA as possibly aliasing it and puts a vmcnt(0) in front (no alias scopes on the
+// one dynamic LDS buffer), which would drain the next tile's weight stages, box loads and y
+// prefetches at every staging write and read. The staging rows live in the box region, which no
+// DMA targets, so the only ordering they need is lgkmcnt (waited explicitly) and the barriers.
+typedef unsigned int bx_u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int bx_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint32_t bx_lds_addr(const void* p) {
+  return (uint32_t)(size_t)(const __attribute__((address_space(3))) void*)p;
+}
+// (the byte offset is an immediate: unrolled accesses share one address VGPR, as compiled LDS
+// accesses do -- per-access addresses would be hoisted out of the tile loop as live registers)
+template <int OFF>
+__device__ __forceinline__ void bx_ds_write64(uint32_t a, uint2 v) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  const bx_u32x2 w = {v.x, v.y};
+  asm volatile("ds_write_b64 %0, %1 offset:%2" ::"v"(a), "v"(w), "n"(OFF));
+}
+__device__ __forceinline__ void bx_ds_write128(uint32_t a, uint4 v) {
+  const bx_u32x4 w = {v.x, v.y, v.z, v.w};
+  asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(w));
+}
+template <int OFF>
+__device__ __forceinline__ bx_u32x4 bx_ds_read128(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset");
+  bx_u32x4 r;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return r;
+}
+// compile-time loop: f(std::integral_constant<int, i>) for i in [0, N)
+template <typename F, int... I>
+__device__ __forceinline__ void bx_sfor_(F& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void bx_sfor(F&& f) {
+  bx_sfor_(f, std::make_integer_sequence<int, N>{});
+}
+__device__ __forceinline__ void bx_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // Exact vmcnt counts of the box kernel's weight-stage waits. At tap t of a channel block the wave
 // waits for stage t of the block; every vector-memory op it issued after that stage's DMA may still
 // be outstanding (vmcnt retires in issue order). Issue order per tap: wait, barrier, DMA of stage
@@ -108,36 +155,48 @@ __device__ __forceinline__ void bx_wait_c(int n) { bx_wait_bs<0, 63>((uint32_t)n
 // of the first tile (STG - 1 stages fired in the prologue), 1 = a later block of the same tile,
 // 2 = the first block of a later tile.
 struct BoxWaits {
-  int y[3][9];
+  int y[3][2][9];  // [case][last block of the tile][tap]
 };
+// TPF / PFI: the last block of a tile issues PFI y-prefetch DMAs (EPI 2) at tap TPF, after that
+// tap's weight DMA and box loads; a wait whose target was issued before them and that comes after
+// them counts them too.
 __host__ __device__ constexpr BoxWaits make_box_waits(int TAPS, int STG, int NDMA, int P0, int PT, int NPT,
-                                                      int EPI_IT, int NPRE, bool EPI2, int ZC) {
+                                                      int EPI_IT, int NPRE, bool EPI2, int ZC, int TPF = 0,
+                                                      int PFI = 0) {
   // P(u): box loads at tap u = P0 at tap 0, PT at taps 1 .. NPT-1 (P0 = PT when spread)
   BoxWaits w{};
   for (int c = 0; c < 3; ++c) {
-    for (int t = 0; t < TAPS; ++t) {
-      auto P = [&](int u) { return u == 0 ? P0 : (u < NPT ? PT : 0); };
-      const int g = t - (STG - 1);  // tap of this block that fired stage t (< 0: earlier)
-      const int epi_after_pre = (EPI2 ? 2 * EPI_IT - NPRE : 0) + 2 * EPI_IT;
-      const int epi_all = (EPI2 ? 2 * EPI_IT : 0) + NDMA + 2 * EPI_IT;
-      int y = 0;
-      if (c == 2 && t == STG - 1) {  // prefired in the previous tile's epilogue
-        y = epi_after_pre + ZC + P(0);
-        for (int h = 1; h < t; ++h) y += NDMA + P(h);
-      } else if (g >= 0) {
-        y = P(g);
-        for (int h = g + 1; h < t; ++h) y += NDMA + P(h);
-      } else if (c == 0) {  // fired in the prologue
-        y = (STG - 2 - t) * NDMA;
-        for (int h = 0; h < t; ++h) y += NDMA + P(h);
-      } else {  // fired at tap TAPS + g of the previous block
-        const int gp = TAPS + g;
-        y = P(gp);
-        for (int h = gp + 1; h < TAPS; ++h) y += NDMA + P(h);
-        y += (c == 2 ? epi_all : 0) + ZC;
-        for (int h = 0; h < t; ++h) y += (c == 2 && h == 0 ? 0 : NDMA) + P(h);
+    for (int last = 0; last < 2; ++last) {
+      for (int t = 0; t < TAPS; ++t) {
+        auto P = [&](int u) { return u == 0 ? P0 : (u < NPT ? PT : 0); };
+        const int g = t - (STG - 1);  // tap of this block that fired stage t (< 0: earlier)
+        const int epi_after_pre = (EPI2 ? 2 * EPI_IT - NPRE : 0) + 2 * EPI_IT;
+        const int epi_all = (EPI2 ? 2 * EPI_IT : 0) + NDMA + 2 * EPI_IT;
+        const bool pf_here = last && TPF < t;  // this block's prefetch lies before the wait
+        int y = 0;
+        if (c == 2 && t == STG - 1) {  // prefired in the previous tile's epilogue
+          y = epi_after_pre + ZC + P(0);
+          for (int h = 1; h < t; ++h) y += NDMA + P(h);
+          if (pf_here) y += PFI;
+        } else if (g >= 0) {
+          y = P(g);
+          for (int h = g + 1; h < t; ++h) y += NDMA + P(h);
+          if (pf_here && g <= TPF) y += PFI;
+        } else if (c == 0) {  // fired in the prologue
+          y = (STG - 2 - t) * NDMA;
+          for (int h = 0; h < t; ++h) y += NDMA + P(h);
+          if (pf_here) y += PFI;
+        } else {  // fired at tap TAPS + g of the previous block
+          const int gp = TAPS + g;
+          y = P(gp);
+          for (int h = gp + 1; h < TAPS; ++h) y += NDMA + P(h);
+          y += (c == 2 ? epi_all : 0) + ZC;
+          for (int h = 0; h < t; ++h) y += (c == 2 && h == 0 ? 0 : NDMA) + P(h);
+          if (c == 2 && gp <= TPF) y += PFI;  // the previous tile's last block prefetched after it
+          if (pf_here) y += PFI;
+        }
+        w.y[c][last][t] = y;
       }
-      w.y[c][t] = y;
     }
   }
   return w;
@@ -153,7 +212,8 @@ __host__ __device__ constexpr int box_stages(int bn, int ks) {
 __host__ __device__ constexpr int box_waits_max(const BoxWaits& w, int taps) {
   int m = 0;
   for (int c = 0; c < 3; ++c)
-    for (int t = 0; t < taps; ++t) m = w.y[c][t] > m ? w.y[c][t] : m;
+    for (int l = 0; l < 2; ++l)
+      for (int t = 0; t < taps; ++t) m = w.y[c][l][t] > m ? w.y[c][l][t] : m;
   return m;
 }
 
@@ -178,9 +238,11 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int RPP = NT / OCPR;               // rows per pass
   constexpr int EPI_IT = (128 + RPP - 1) / RPP;
   constexpr int NST = 2 * EPI_IT;              // epilogue stores (16 B) per wave per tile
+  constexpr int EPI_G = EPI == 2 ? 2 : 4;      // staged chunks read per LDS wait
   constexpr int ZC = PRO >= 2 ? NBX : 0;       // z stores per wave per written box
   constexpr int NBL = PRO == 3 ? 2 * NBX : NBX;  // box loads per wave (PRO 3: dz and y)
   static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
+  static_assert((NT / OCPR + (EPI_IT - 1) * RPP + 1) * LDE <= BX_ROWS * 80, "epilogue reads stay in the box");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BNR * BK;
   constexpr int STG = box_stages(BN, KS);      // weight ring stages
@@ -191,16 +253,24 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int LPP = PRO == 3 ? 2 : 1;        // loads per box piece (PRO 3: dz and y)
   constexpr int NPRE = EPI_IT < 4 ? EPI_IT : 4;  // EPI 2: y rows loaded before a half's barrier
   static_assert(STG - 1 <= TAPS && (KS != 133 || NBX <= TAPS), "wait tables");
-  constexpr BoxWaits kWaits = KS == 133 ? make_box_waits(TAPS, STG, NDMA, LPP, LPP, NBX, EPI_IT, NPRE, EPI == 2, ZC)
-                                        : make_box_waits(TAPS, STG, NDMA, NBX * LPP, 0, 1, EPI_IT, NPRE, EPI == 2, ZC);
+  // EPI 2: y-row prefetch of the tile's epilogue rows at tap TPF of its last block (y_prefetch)
+  constexpr int TPF = TAPS >= 4 ? TAPS - 4 : 0;
+  constexpr int PFI = (EPI == 2 && BOX_YPF) ? ((BM * ((BN * 2 + 127) / 128) / NWAVES) + 63) / 64 : 0;
+  constexpr BoxWaits kWaits = KS == 133 ? make_box_waits(TAPS, STG, NDMA, LPP, LPP, NBX, EPI_IT, NPRE, EPI == 2, ZC,
+                                                         TPF, PFI)
+                                        : make_box_waits(TAPS, STG, NDMA, NBX * LPP, 0, 1, EPI_IT, NPRE, EPI == 2, ZC,
+                                                         TPF, PFI);
   static_assert(box_waits_max(kWaits, TAPS) <= 63, "vmcnt range");
   static_assert(PRO != 3 || BN <= 128, "PRO 3 registers");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
   bf16_t* ring = box + BX_ROWS * 80;                             // [STG][BNR][BK]
-  float* ss_lds = (float*)(ring + STG * STAGE_ELEMS);            // EPI 2: [4][BN]
-  float* pro_lds = ss_lds + (EPI == 2 ? 4 * BN : 0);             // PRO 1/2: [2][Cin]; PRO 3: [7][Cin]
+  float* ss_lds = (float*)(ring + STG * STAGE_ELEMS);            // EPI 2: [4][BN]; EPI 1: shift [BN]
+  float* pro_lds = ss_lds + (EPI == 2 ? 4 * BN : EPI == 1 ? BN : 0);  // PRO 1/2: [2][Cin]; PRO 3: [7][Cin]
+  // EPI 2: 256 B that the epilogue's y-row L2 prefetch (LDS-DMA, one dword per lane) writes and
+  // nobody reads
+  char* pf_lds = (char*)(pro_lds + (PRO == 3 ? 7 * p.Cin : (PRO ? 2 * p.Cin : 0)));
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -238,6 +308,12 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
       const int q = t / BN, c = n0 + (t - q * BN);
       ss_lds[t] = c < p.Cout ? p.bn_ss[q * p.Cout + c] : 0.f;
     }
+  }
+  if constexpr (EPI == 1) {
+    // per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
+    // rounding of the staged rows, so the stored pre-BN values keep their precision when
+    // |mean| >> std
+    for (int t = tid; t < BN; t += NT) ss_lds[t] = (p.bn_ss != nullptr && n0 + t < p.Cout) ? p.bn_ss[n0 + t] : 0.f;
   }
   if constexpr (PRO == 1 || PRO == 2) {
     for (int t = tid; t < 2 * Cin; t += NT) pro_lds[t] = g.pro_ss[2 * Cin + t];  // scale [Cin], shift [Cin]
@@ -430,7 +506,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       const uint4 v = xr[k];
-      *(uint4*)(box + (xrow0 + 64 * k) * PITCH + xch * 8) = v;
+      bx_ds_write128(bx_lds_addr(box + (xrow0 + 64 * k) * PITCH + xch * 8), v);
       if constexpr (PRO >= 2) {
         bool own = n_tile == 0 && xo[k] != 0x80000000u && chv(cb);
         if constexpr (KS == 133) {
@@ -471,6 +547,38 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         const bool v = t < p.T && ti.p0 + j < g.HW;  // rows past T * P idle
         rb[i] = t < p.T ? lr : 0;
         yo[i] = v ? (uint32_t)(((long long)t * g.HW + ti.p0 + j) * p.ldy * 2) : 0x80000000u;
+      }
+    }
+  };
+
+  // EPI 2: pull the tile's producer rows bn_y[row][n0 .. n0 + BN) into L2 during the last block's
+  // taps, so the epilogue's y loads (one chain per thread) hit L2 instead of paying HBM latency
+  // twice per tile (tools/box_trace.py: ~1/3 of the (3,1,1) dgrad's tile time). One dword per lane
+  // and 128-B line, written to pf_lds and never read; issued after the tap's weight DMA, so only
+  // stages fired >= 2 taps later can wait for them.
+  auto y_prefetch = [&](const TileInfo& tt) {
+    if constexpr (EPI == 2) {
+      constexpr int LPR = (BN * 2 + 127) / 128;          // 128-B lines per row
+      constexpr int LPW = BM * LPR / NWAVES;             // lines per wave
+      constexpr int PF_INST = (LPW + 63) / 64;
+      static_assert(!BOX_YPF || PF_INST == PFI, "prefetch count in the wait tables");
+      // rows relative to the tile's first output row (133: rows m0 + lr; 311: (t * HW + p0 + j))
+      const long long row0 = KS == 133 ? (long long)tt.m0 : (long long)tt.b * p.T * g.HW + tt.p0;
+      const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bn_y + row0 * p.bn_ld), (short)0, 0x7FFFFFF0,
+                                                         0x00020000);
+#pragma unroll
+      for (int k = 0; k < PF_INST; ++k) {
+        const int L = wave * LPW + min(k * 64 + lane, LPW - 1);
+        const int lr = L / LPR, piece = L - lr * LPR;
+        int rel;  // row relative to row0 (out-of-tile rows clamp to the tile's last valid row)
+        if constexpr (KS == 133) {
+          rel = min(lr, p.M - 1 - tt.m0);
+        } else {
+          const int t0 = (int)fdiv((uint32_t)lr, g.fP), t = min(t0, p.T - 1);
+          rel = t * g.HW + min(lr - t0 * g.P, g.HW - 1 - tt.p0);
+        }
+        const uint32_t off = (uint32_t)((rel * p.bn_ld + min(n0 + piece * 64, p.Cout - 8)) * 2);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(prs, (lds_ptr_t)pf_lds, 4, off, 0, 0, 0);
       }
     }
   };
@@ -533,9 +641,16 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         // after its DMA -- later stages, box loads, the previous tile's epilogue stores and z
         // stores -- drain only when a stage fired after them is waited for
         const bool carried = cb == 0 && !first_tile;
-        if (cb > 0) bx_wait_c(kWaits.y[1][t]);
-        else if (first_tile) bx_wait_c(kWaits.y[0][t]);
-        else bx_wait_c(kWaits.y[2][t]);
+        // (the last-block tables differ only after the y prefetch: t > TPF, EPI 2)
+        if (PFI > 0 && t > TPF && last_cb) {
+          if (cb > 0) bx_wait_c(kWaits.y[1][1][t]);
+          else if (first_tile) bx_wait_c(kWaits.y[0][1][t]);
+          else bx_wait_c(kWaits.y[2][1][t]);
+        } else {
+          if (cb > 0) bx_wait_c(kWaits.y[1][0][t]);
+          else if (first_tile) bx_wait_c(kWaits.y[0][0][t]);
+          else bx_wait_c(kWaits.y[2][0][t]);
+        }
         tev();  // W: weight stage landed (this wave's share)
         ring_barrier();
         tev();  // B: every wave at the ring barrier
@@ -558,6 +673,9 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           if (t < NBX) box_load(xrs, last_cb ? 0 : cb + 1, t, t + 1);
         } else {
           if (t == 0) box_load(xrs, last_cb ? 0 : cb + 1, 0, NBX);
+        }
+        if constexpr (PFI > 0) {
+          if (last_cb && t == TPF) y_prefetch(ti);
         }
         // ---- MFMAs of stage s: A = weights (ring), B = box rows shifted by the tap ----
         const bf16_t* bsh = ring + (gs % STG) * STAGE_ELEMS;
@@ -638,21 +756,26 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         for (int it = 0; it < NPRE; ++it) ypre[it] = yload(it);
       }
       if ((wr >> 1) == half) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = (wr & 1) * WM + i * MF + (lane & (MF - 1));  // row within the half
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-#pragma unroll
-            for (int gq = 0; gq < (MF == 16 ? 1 : 4); ++gq) {
-              const int col = wc * WN + j * MF + (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4);
+        // row (wr & 1) * WM + i * MF + (lane & (MF - 1)) of the half, column wc * WN + j * MF + the
+        // lane's 4-column group (+ gq * 8 for 32x32 fragments)
+        const uint32_t sbase = bx_lds_addr(box + ((wr & 1) * WM + (lane & (MF - 1))) * LDE + wc * WN +
+                                           (MF == 16 ? (lane >> 4) * 4 : (lane >> 5) * 4));
+        bx_sfor<TN>([&](auto J) {
+          bx_sfor<(MF == 16 ? 1 : 4)>([&](auto Q) {
+            constexpr int j = decltype(J)::value, gq = decltype(Q)::value;
+            float4 sh = {0.f, 0.f, 0.f, 0.f};
+            if constexpr (EPI == 1)  // EPI 1 shift of these 4 columns
+              sh = *(const float4*)(ss_lds + wc * WN + j * MF +
+                                    (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4));
+            bx_sfor<TM>([&](auto I) {
+              constexpr int i = decltype(I)::value;
               uint2 o;
-              o.x = pack2bf(acc[j][i][gq * 4 + 0], acc[j][i][gq * 4 + 1]);
-              o.y = pack2bf(acc[j][i][gq * 4 + 2], acc[j][i][gq * 4 + 3]);
-              *(uint2*)(box + row * LDE + col) = o;
-            }
-          }
-        }
+              o.x = pack2bf(acc[j][i][gq * 4 + 0] - sh.x, acc[j][i][gq * 4 + 1] - sh.y);
+              o.y = pack2bf(acc[j][i][gq * 4 + 2] - sh.z, acc[j][i][gq * 4 + 3] - sh.w);
+              bx_ds_write64<(i * MF * LDE + j * MF + gq * 8) * 2>(sbase, o);
+            });
+          });
+        });
       }
       lds_barrier();
       tev();  // H1: the half's rows staged
@@ -666,12 +789,26 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
           for (int it = NPRE; it < EPI_IT; ++it) ypre[it] = yload(it);
         }
+        // the thread's staged chunks read EPI_G at a time, one wait per group (the other half's
+        // waves still hold their accumulators here, so not all EPI_IT at once)
+        // (rows past the half -- it * RPP + tid / OCPR >= 128 -- are read but not stored; they stay
+        // inside the box region)
+        bx_u32x4 dvs[EPI_IT];
+        const uint32_t rbase = bx_lds_addr(box + (tid / OCPR) * LDE + cc * 8);
 #pragma unroll
         for (int it = 0; it < EPI_IT; ++it) {
+          if (it % EPI_G == 0) {
+            bx_sfor<EPI_IT>([&](auto U) {
+              constexpr int u = decltype(U)::value;
+              if (u >= it && u < it + EPI_G) dvs[u] = bx_ds_read128<u * RPP * LDE * 2>(rbase);
+            });
+            bx_lgkm0();
+          }
           const int row = tid / OCPR + it * RPP;  // row within the half
           const int lr = half * 128 + row;
           const bool act = (tid < RPP * OCPR) & (row < 128);
-          const uint4 dv = *(const uint4*)(box + min(row, 127) * LDE + cc * 8);
+          const bx_u32x4 dw = dvs[it];
+          const uint4 dv = {dw.x, dw.y, dw.z, dw.w};
           uint32_t yo;
           long long grow;  // global output row
           if constexpr (KS == 133) {
@@ -820,7 +957,7 @@ bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
 template <int BN, int KS, int EPI, int PRO, int MF>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
   const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)box_stages(BN, KS) * ((BN + 63) / 64 * 64) * BX_BK * 2 +
-                     (EPI == 2 ? 16 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
+                     (EPI == 2 ? 16 * BN + 256 : EPI == 1 ? 4 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
   if (lds > 160 * 1024) return V4_UNSUPPORTED;
   static bool attr_set = false;
   if (!attr_set) {

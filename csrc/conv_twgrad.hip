@@ -82,7 +82,11 @@ struct TwParams {
   FastDiv fnbs, fntb;
 };
 
-template <int BN>
+// REG = false: LDS-DMA ring of TW_NSTG stages (two boxes in flight). REG = true: register-staged
+// boxes (NSUB + 2 16-B chunks per thread and box) in a 3-box register ring written into 2 LDS
+// slots: three boxes (~100 KiB per CU) in flight instead of two, for ~1.5x the latency cover at
+// the same LDS footprint of the DMA ring's two stages.
+template <int BN, bool REG>
 __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
   using G = TwGeom<BN>;
   constexpr int NBLK = BN / 16, CBLK = TW_CC / 16;  // 16-row n blocks, 16-channel c blocks
@@ -191,6 +195,95 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
   };
 
+  auto compute = [&](int slot_i) {
+    const lds_char* dimg = lds + slot_i * G::STAGE_BYTES;
+    const lds_char* ximg = dimg + G::D_BYTES;
+    bf16x8 af0[NBW], bf0[KBW], af1[NBW], bf1[KBW];
+    load(dimg, ximg, 0, af0, bf0);
+    load(dimg, ximg, 1, af1, bf1);
+    __builtin_amdgcn_s_setprio(1);
+    mma(af0, bf0);
+    mma(af1, bf1);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  if constexpr (REG) {
+    constexpr int NR = G::NSUB + 2;
+    const int rrow = tid >> 3, rch = tid & 7;
+    // box -> this thread's NSUB dY chunks (row rrow of each sub-image) and 2 halo chunks (rows rrow,
+    // rrow + 64); every box issues all NR loads (past box_end / the halo: out of range, zeros), so
+    // the vmcnt wait before a box's LDS write is the same count on every path
+    auto rload = [&](int box, uint4 (&R)[NR]) {
+      const bool live = box < box_end;
+      const int bx = live ? box : box_begin;
+      const uint32_t q = fdiv((uint32_t)bx, p.fnbs);
+      const int sb = bx - (int)q * p.nbs;
+      const uint32_t b = fdiv(q, p.fntb);
+      const int tb = (int)(q - b * p.ntb);
+      const int t0 = tb * p.bt, s0 = sb << p.lbs;
+      const auto drs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.dy + (long long)b * clip_d), (short)0,
+                                                         (int)(live ? dlim : 0u), 0x00020000);
+      const auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.x + (long long)b * clip_x), (short)0,
+                                                         (int)(live ? xlim : 0u), 0x00020000);
+      {
+        const int t = t0 + (rrow >> p.lbs), s = s0 + (rrow & ((1 << p.lbs) - 1));
+        const bool vr = (t < p.T) & (s < p.HW);
+#pragma unroll
+        for (int k = 0; k < G::NSUB; ++k) {
+          const int n = n0 + k * 64 + rch * 8;
+          const uint32_t off = (vr & (n < p.Cout)) ? (uint32_t)((((long long)t * p.HW + s) * p.ldd + n) * 2)
+                                                   : 0x80000000u;
+          R[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = rrow + 64 * j;
+        const int t = t0 - 1 + (r >> p.lbs), s = s0 + (r & ((1 << p.lbs) - 1));
+        const int c = c0 + rch * 8;
+        const bool v = (r < (p.bt + 2) << p.lbs) & ((unsigned)t < (unsigned)p.T) & (s < p.HW) & (c < p.Cin);
+        const uint32_t off = v ? (uint32_t)((((long long)t * p.HW + s) * p.Cin + c) * 2) : 0x80000000u;
+        R[G::NSUB + j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+      }
+    };
+    auto rstore = [&](const uint4 (&R)[NR], int slot_i) {
+      char* sd = smem + slot_i * G::STAGE_BYTES;
+      char* sx = sd + G::D_BYTES;
+#pragma unroll
+      for (int k = 0; k < G::NSUB; ++k)
+        *(uint4*)(sd + k * G::SUB_BYTES + rrow * 128 + tw_chunk(rrow, rch) * 16) = R[k];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int r = rrow + 64 * j;
+        *(uint4*)(sx + r * 128 + tw_chunk(r, rch) * 16) = R[G::NSUB + j];
+      }
+    };
+    uint4 R0[NR], R1[NR], R2[NR];
+    rload(box_begin, R0);
+    rload(box_begin + 1, R1);
+    rload(box_begin + 2, R2);
+    rstore(R0, 0);
+    rload(box_begin + 3, R0);
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // box j lives in register set j % 3 and LDS slot (j - box_begin) % 2. Every step issues its NR
+    // loads, also past box_end (out of range: no traffic): the compiler's vmcnt before a set's LDS
+    // write counts the loads issued after that set on every path into it, and a path that skipped
+    // the later steps' loads made it wait for the set loaded one step earlier instead of three
+    auto step = [&](int box, uint4 (&Rn)[NR]) {
+      const int i = box - box_begin;
+      if (box < box_end) {
+        compute(i & 1);
+        if (box + 1 < box_end) rstore(Rn, (i + 1) & 1);  // slot of box - 1: every wave finished it
+      }
+      rload(box + 4, Rn);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    for (int box = box_begin; box < box_end; box += 3) {
+      step(box, R1);
+      step(box + 1, R2);
+      step(box + 2, R0);
+    }
+  } else {
   // prologue: boxes 0 .. NSTG-2 in flight
 #pragma unroll
   for (int s = 0; s < TW_NSTG - 1; ++s) issue(box_begin + s, s);
@@ -200,17 +293,10 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
     tw_wait<(TW_NSTG - 2) * G::PER_BOX>();  // this box landed (this wave's pieces); two behind it in flight
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave's pieces; slot i-1 free
     issue(box + TW_NSTG - 1, (i + TW_NSTG - 1) % TW_NSTG);
-    const lds_char* dimg = lds + stage * G::STAGE_BYTES;
-    const lds_char* ximg = dimg + G::D_BYTES;
-    bf16x8 af0[NBW], bf0[KBW], af1[NBW], bf1[KBW];
-    load(dimg, ximg, 0, af0, bf0);
-    load(dimg, ximg, 1, af1, bf1);
-    __builtin_amdgcn_s_setprio(1);
-    mma(af0, bf0);
-    mma(af1, bf1);
-    __builtin_amdgcn_s_setprio(0);
+    compute(stage);
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (dummy) stages
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing (dummy) stages / loads
 
   // C[n][k]: row n = 4 * (lane >> 4) + r of the n block, col = lane & 15 of the c block
   float* out = p.slab + (long long)split * p.Npad * p.Kdim;
@@ -250,16 +336,18 @@ bool tw_box(int T, int HW, int& bt, int& lbs) {
   return ok;
 }
 
-template <int BN>
+template <int BN, bool REG>
 int launch_tw(TwParams& p, hipStream_t stream) {
   using G = TwGeom<BN>;
+  const int lds = REG ? 2 * G::STAGE_BYTES : G::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)twgrad_kernel<BN>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                G::LDS));
+    HIP_RET(hipFuncSetAttribute((const void*)twgrad_kernel<BN, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                lds));
     attr_set = true;
   }
-  hipLaunchKernelGGL((twgrad_kernel<BN>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT), G::LDS, stream, p);
+  hipLaunchKernelGGL((twgrad_kernel<BN, REG>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT), lds, stream,
+                     p);
   return (int)hipGetLastError();
 }
 
@@ -287,9 +375,11 @@ MILNCE_API int milnce_twgrad_plan(int B, int T, int H, int W, int Cin, int Cout,
 
 // dW of a (3,1,1) / stride 1 / padding (1,0,0) conv: the split slab is written to `slab`; with dw
 // != null it is also reduced (accumulated when accumulate != 0) into dw [Cout][Cin_param][3][1][1].
+// reg != 0: the register-staged variant (REG = true).
 MILNCE_API int milnce_twgrad(const void* dy, int ldd, const void* x, float* slab, float* dw, int accumulate, int B,
-                             int T, int H, int W, int Cin, int Cin_param, int Cout, int bn, int splits,
+                             int T, int H, int W, int Cin, int Cin_param, int Cout, int bn, int splits, int reg,
                              hipStream_t stream) {
+  if (!(bn == 64 || bn == 128 || bn == 192)) return (int)hipErrorInvalidValue;
   TwParams p;
   p.dy = (const bf16_t*)dy;
   p.x = (const bf16_t*)x;
@@ -313,10 +403,15 @@ MILNCE_API int milnce_twgrad(const void* dy, int ldd, const void* x, float* slab
   // per-clip byte offsets are 32-bit buffer offsets
   if ((long long)T * p.HW * (ldd > Cin ? ldd : Cin) * 2 > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
   int rc;
-  if (bn == 64) rc = launch_tw<64>(p, stream);
-  else if (bn == 128) rc = launch_tw<128>(p, stream);
-  else if (bn == 192) rc = launch_tw<192>(p, stream);
-  else return (int)hipErrorInvalidValue;
+  if (reg) {
+    if (bn == 64) rc = launch_tw<64, true>(p, stream);
+    else if (bn == 128) rc = launch_tw<128, true>(p, stream);
+    else rc = launch_tw<192, true>(p, stream);
+  } else {
+    if (bn == 64) rc = launch_tw<64, false>(p, stream);
+    else if (bn == 128) rc = launch_tw<128, false>(p, stream);
+    else rc = launch_tw<192, false>(p, stream);
+  }
   if (rc) return rc;
   if (dw == nullptr) return 0;
   return launch_wgrad_reduce(slab, dw, splits, p.Npad, p.Kdim, Cout, Cin, Cin_param, 3, accumulate, stream);

@@ -284,32 +284,45 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     ring_barrier();  // every wave done reading the ring before the epilogue reuses it
 
+    // EPI 1: per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
+    // rounding, so the stored pre-BN values keep their precision when |mean| >> std
+    auto shift4 = [&](int col, float (&sh)[4]) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + col + r;
+        sh[r] = (EPI == 1 && p.bn_ss != nullptr && n < p.Cout) ? p.bn_ss[n] : 0.f;
+      }
+    };
     if constexpr (MF == 16) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wr * WM + i * 16 + (lane & 15);
+      for (int j = 0; j < TN; ++j) {
+        const int col = wc * WN + j * 16 + (lane >> 4) * 4;
+        float sh[4];
+        shift4(col, sh);
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int i = 0; i < TM; ++i) {
+          const int row = wr * WM + i * 16 + (lane & 15);
           const f32x4 v = acc[j][i];
           uint2 o;
-          o.x = pack2bf(v[0], v[1]);
-          o.y = pack2bf(v[2], v[3]);
-          const int col = wc * WN + j * 16 + (lane >> 4) * 4;
+          o.x = pack2bf(v[0] - sh[0], v[1] - sh[1]);
+          o.y = pack2bf(v[2] - sh[2], v[3] - sh[3]);
           *(uint2*)(Es + row * LDE + col) = o;
         }
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wr * WM + i * 32 + (lane & 31);
+      for (int j = 0; j < TN; ++j) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int g = 0; g < 4; ++g) {
+          const int col = wc * WN + j * 32 + g * 8 + (lane >> 5) * 4;
+          float sh[4];
+          shift4(col, sh);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
+          for (int i = 0; i < TM; ++i) {
+            const int row = wr * WM + i * 32 + (lane & 31);
             uint2 o;
-            o.x = pack2bf(acc[j][i][4 * g + 0], acc[j][i][4 * g + 1]);
-            o.y = pack2bf(acc[j][i][4 * g + 2], acc[j][i][4 * g + 3]);
-            const int col = wc * WN + j * 32 + g * 8 + (lane >> 5) * 4;
+            o.x = pack2bf(acc[j][i][4 * g + 0] - sh[0], acc[j][i][4 * g + 1] - sh[1]);
+            o.y = pack2bf(acc[j][i][4 * g + 2] - sh[2], acc[j][i][4 * g + 3] - sh[3]);
             *(uint2*)(Es + row * LDE + col) = o;
           }
         }

@@ -22,7 +22,7 @@ P, I, F, D, L = c_void_p, c_int, c_float, c_double, c_longlong
 
 SIGNATURES: Dict[str, list] = {
     "milnce_conv_fwd": [P, I, P, P, P, P, P, I] + [I] * 6 + [I] * 9 + [I] * 8 + [P],
-    "milnce_conv_fwd_pro": [P, I, P, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 6 + [P],
+    "milnce_conv_fwd_pro": [P, I, P, P, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 6 + [P],
     "milnce_conv_dgrad_bnbwd": [P, P, P, P, P, P, I, P, P, P, P] + [I] * 6 + [I] * 3 + [I] * 3 + [I] * 5 + [P],
     "milnce_conv_wgrad": [P, I, P, I, P, P] + [I] * 7 + [I] * 9 + [I] * 8 + [P],
     "milnce_pack_weight": [P, P] + [I] * 9 + [P],
@@ -30,7 +30,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_halo_wgrad": [P, I, P, P, P, I] + [I] * 13 + [P],
     "milnce_wgrad_reduce": [P, P] + [I] * 8 + [P],
     "milnce_pack_weights_multi": [P, I, I, P],
-    "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P],
+    "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
     "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, I, I, P],
     "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P],
@@ -48,7 +48,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_set_pool_s1_maxthr": [I],
     "milnce_stem_wgrad": [P, P, I, P, L, P, I, I, I, I, I, P],
     "milnce_stem_wgrad_pool": [P, P, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
-    "milnce_stem_fwd": [P, I, P, I, P, P, L, I, I, I, I, P],
+    "milnce_stem_fwd": [P, I, P, I, P, P, L, P, I, I, I, I, P],
     "milnce_maxpool_bwd_gate": [P, P, P] + [I] * 21 + [P, P, I, P],
     "milnce_bn_relu_gate_maxpool_fwd": [P, P, P, P, P] + [I] * 21 + [P],
     "milnce_maxpool_bwd_gated": [P, P, P] + [I] * 21 + [P, I, P, P, I, P, P, P],
@@ -76,7 +76,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_dtw_path": [P, I, I, I, P, P, P],
     "milnce_box_set_trace": [P],
     "milnce_twgrad_plan": [I] * 8 + [P, P],
-    "milnce_twgrad": [P, I, P, P, P, I] + [I] * 9 + [P],
+    "milnce_twgrad": [P, I, P, P, P, I] + [I] * 10 + [P],
 }
 
 # entry points that return something other than an int status

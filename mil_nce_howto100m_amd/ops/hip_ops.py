@@ -498,14 +498,19 @@ def _tune_local(launch, impls, default: Optional[int]) -> int:
 
 
 def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: Optional[torch.Tensor],
-                     pro=None):
+                     pro=None, shift: Optional[torch.Tensor] = None):
     """Raw conv output y (bf16) with the BN-statistics epilogue when ``stats`` is given.
+
+    ``shift`` (fp32 [Cout], with ``stats`` only): subtracted per channel before the bf16 rounding
+    (``_bn_shift``); the statistics are those of the shifted values.
 
     ``pro = (z_out or None)``: x is a "pro" placeholder (``_pro_z``) standing for
     relu(y_prod * scale + shift) of its producer BN. A box-tiled variant applies that while
     staging its input and writes z to ``z_out`` (the wgrad operand); any other variant gets
     z materialised into ``z_out`` (or a scratch buffer) first."""
     y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=x.device)
+    if stats is None:
+        shift = None
     if pro is not None:
         z_out = pro[0]
         yp, ssp, ldp = x._milnce_bn
@@ -515,13 +520,14 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
 
         def launch_pro(impl, grid):
             if impl in _BOX_IMPLS and fusable:
-                call("milnce_conv_fwd_pro", ptr(yp), ldp, ptr(wp), ptr(y), ptr(stats), ptr(ssp), ptr(z_out),
+                call("milnce_conv_fwd_pro", ptr(yp), ldp, ptr(wp), ptr(y), ptr(stats), ptr(shift), ptr(ssp),
+                     ptr(z_out),
                      plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
                      plan.Cout, plan.bn, grid, impl, stream())
             else:  # the variant needs z in memory: its timing includes the BN-apply pass
                 call("milnce_bn_relu_apply", ptr(yp), ldp, ptr(zbuf), plan.Cin, ptr(ssp), plan.Cin, plan.B, thw_in,
                      None, stream())
-                call("milnce_conv_fwd", ptr(zbuf), 0, ptr(wp), ptr(y), ptr(stats), None, None, 0,
+                call("milnce_conv_fwd", ptr(zbuf), 0, ptr(wp), ptr(y), ptr(stats), None, ptr(shift), 0,
                      plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.s, *plan.p,
                      plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
 
@@ -539,8 +545,8 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     pt, ph, pw = plan.p
 
     def launch(impl, grid):
-        call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None, None, 0,
-             plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
+        call("milnce_conv_fwd", ptr(x), int(x.dtype == torch.uint8), ptr(wp), ptr(y), ptr(stats), None,
+             ptr(shift), 0, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, st, sh, sw, pt, ph, pw,
              plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
 
     rows = stats.numel() // (2 * plan.Npad) if stats is not None else None
@@ -953,9 +959,10 @@ def _tw_tiles(cout: int) -> Tuple[int, ...]:
     return tuple(bn for bn in (192, 128, 64) if _ceil(cout, bn) * bn - cout < 64)
 
 
-def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accumulate: int, occ: int = 1):
-    """Temporal box wgrad; with ``target`` None only the split slab is filled and
-    (slab, splits, Npad, Kpad) of the pending reduction is returned."""
+def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accumulate: int, occ: int = 1,
+            reg: int = 1):
+    """Temporal box wgrad (reg: register-staged boxes, else the LDS-DMA ring); with ``target`` None
+    only the split slab is filled and (slab, splits, Npad, Kpad) of the pending reduction is returned."""
     key = (id(plan), bn, occ)
     geo = _TW_SPLITS.get(key)
     if geo is None:
@@ -967,7 +974,7 @@ def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accu
         geo = _TW_SPLITS[key] = (int(floats.value), int(splits.value))
     slab = torch.empty((geo[0],), dtype=F32, device=dy.device)
     call("milnce_twgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target) if target is not None else None,
-         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, bn, geo[1], stream())
+         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, bn, geo[1], int(reg), stream())
     return slab, geo[1], _ceil(plan.Cout, bn) * bn, 3 * plan.Cin
 
 
@@ -1026,8 +1033,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     def launch_with(tn, impl, occ, tk, target, accumulate):
         """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
         (slab, splits, Npad, Kpad) returned for the caller's reduction."""
-        if impl >= 1000:  # temporal box wgrad, N tile impl - 1000
-            return _twgrad(dy, x, plan, impl - 1000, target, accumulate, occ)
+        if impl >= 1000:  # temporal box wgrad: N tile impl % 1000, register-staged from 2000
+            return _twgrad(dy, x, plan, impl % 1000, target, accumulate, occ, int(impl >= 2000))
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
             return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, tk, occ)
@@ -1054,7 +1061,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 if plan.k == (3, 1, 1) and plan.Cin % 128 == 0:  # temporal boxes also take 128-channel chunks
                     cands += [(64, 228, occ, 0) for occ in _HALO_OCCS]
             if _twgrad_ok(plan, x):
-                cands += [(bn, 1000 + bn, occ, 0) for bn in _tw_tiles(plan.Cout) for occ in _TW_OCCS]
+                cands += [(bn, base + bn, occ, 0) for base in (1000, 2000) for bn in _tw_tiles(plan.Cout)
+                          for occ in _TW_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}
             default = (plan.w_tn, _DEFAULT_IMPL, 4, plan.w_tk)
@@ -1078,6 +1086,33 @@ def _bn_nparts(M: int) -> int:
     return int(max(1, min(2048, max(min(1024, _ceil(M, 64)), _ceil(M, 2048)))))
 
 
+# Pre-BN storage shift (MILNCE_BN_SHIFT, reference s3dg.py:107-111 trains BN on fp32 conv outputs):
+# in training, the conv epilogue stores y - running_mean (per channel) in bf16 instead of y, so a
+# channel whose mean is large against its spread keeps its precision in the rounding (trained
+# S3D-G layers have |mean| >> std). The statistics, the finalize's mean and everything reading y
+# (BN apply, lazy z, BN backward, the fused partial epilogues) live in the shifted frame, which is
+# exact: BN is invariant to a per-channel constant. bn_finalize adds the shift back for the running
+# mean. Eval stores y unshifted (its BN folds the running statistics).
+_BN_SHIFT = os.environ.get("MILNCE_BN_SHIFT", "1") == "1"
+
+
+def _bn_shift(rmeans, training: bool) -> Optional[torch.Tensor]:
+    """The epilogue shift for conv outputs feeding the BNs with running means ``rmeans`` (in
+    output channel order): the running mean itself for one BN, else a persistent concatenated
+    buffer kept on the first running mean, which bn_finalize advances to the new running means
+    (so no concatenation launch per step; a stale value is only a different, equally exact shift)."""
+    if not (training and _BN_SHIFT) or any(r is None or r.dtype != F32 or not r.is_contiguous() for r in rmeans):
+        return None
+    if len(rmeans) == 1:
+        return rmeans[0]
+    ctot = sum(int(r.numel()) for r in rmeans)
+    buf = getattr(rmeans[0], "_milnce_group_shift", None)
+    if buf is None or buf.numel() != ctot or buf.device != rmeans[0].device:
+        buf = torch.cat([r.detach() for r in rmeans])
+        rmeans[0]._milnce_group_shift = buf
+    return buf
+
+
 def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,
                    wo_override=0, pro=None):
     """conv (statistics epilogue) + BN finalize: returns (plan, raw conv output y, ss)."""
@@ -1085,13 +1120,14 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     dev = x.device
     wp = _pack(weight, plan, 0)
     nparts = plan.grid_m
+    shift = _bn_shift([rmean], training)
     y = None
     if _STEM_FWD and _is_paired_stem(plan) and x.dtype in (BF16, torch.uint8):
         # halo-tiled stem kernel (csrc/conv.hip stem_fwd_kernel); its statistics rows are per workgroup
         y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout), dtype=BF16, device=dev)
         stats = torch.empty((256 * 128,), dtype=F32, device=dev)
         rc = lib().milnce_stem_fwd(ptr(x), int(x.dtype == torch.uint8), ptr(wp), plan.Kpad, ptr(y), ptr(stats),
-                                   stats.numel(), plan.B, plan.T, plan.H, plan.W, stream())
+                                   stats.numel(), ptr(shift), plan.B, plan.T, plan.H, plan.W, stream())
         if rc > 0:
             nparts = rc
         elif rc == _STEM_UNSUPPORTED:
@@ -1101,13 +1137,13 @@ def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, mo
     if y is None:
         stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
                  if training else None)
-        y = conv_forward_raw(x, wp, plan, stats, pro)
+        y = conv_forward_raw(x, wp, plan, stats, pro, shift=shift)
         nparts = plan.grid_m  # as tuned
     C = plan.Cout
     ss = torch.empty((4 * C,), dtype=F32, device=dev)
     call("milnce_bn_finalize", ptr(stats), nparts, plan.Npad, C, float(plan.M), ptr(gamma), ptr(beta),
          ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(momentum), float(eps), int(training),
-         ptr(ss), stream())
+         ptr(ss), ptr(shift), stream())
     return plan, y, ss
 
 
@@ -1436,7 +1472,8 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
     wp = _pack(wcat, plan, 0)
     stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
              if training else None)
-    y = conv_forward_raw(x, wp, plan, stats)
+    shift = _bn_shift([b[2] for b in bns], training)
+    y = conv_forward_raw(x, wp, plan, stats, shift=shift)
     thw = plan.To * plan.Ho * plan.Wo
     zs, sss, gsum = [], [], None
     off = 0
@@ -1446,7 +1483,8 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
         st = stats[off:] if training else None
         call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
              ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
-             float(hyper[i][1]), int(training), ptr(ss), stream())
+             float(hyper[i][1]), int(training), ptr(ss), ptr(shift[off:off + c] if shift is not None else None),
+             stream())
         g = _zeros_f32((plan.B, c), dev) if (i == 0 and want_gsum0) else None
         ysl = y2[:, off:off + c]
         zshape = (plan.B, plan.To, plan.Ho, plan.Wo, c)

@@ -181,8 +181,11 @@ def test_inception_head_prologue_fusion():
             b.zero_grad()
             out = b(xi)
             out.backward(g)
-            res[fuse] = (out.detach().float(), xi.grad.float(), {n: p.grad.clone() for n, p in b.named_parameters()})
-        (o0, x0, g0), (o1, x1, g1) = res[False], res[True]
+            res[fuse] = (out.detach().float(), xi.grad.float(), {n: p.grad.clone() for n, p in b.named_parameters()},
+                         {n: t.clone() for n, t in b.named_buffers()})
+        (o0, x0, g0, b0), (o1, x1, g1, b1) = res[False], res[True]
+        print("out", _rel(o1, o0), "dx", _rel(x1, x0), "params", max(_rel(g1[n], g0[n]) for n in g0))
+        print("buffers", {n: (b0[n].float() - b1[n].float()).abs().max().item() for n in b0})
         assert _rel(o1, o0) < 2e-3 and _rel(x1, x0) < 5e-3
         for n in g0:
             assert _rel(g1[n], g0[n]) < 1e-2, n

@@ -260,6 +260,59 @@ def test_conv_bn_relu_train(cin, cout, k, p, gsum):
     assert int(bn.num_batches_tracked) == int(bn_ref.num_batches_tracked) == 1
 
 
+@pytest.mark.parametrize("group", [False, True])
+def test_bn_shifted_storage_large_mean(group, monkeypatch):
+    """Pre-BN outputs whose channel means dwarf their spread (trained layers): storing them in bf16
+    shifted by the running mean (MILNCE_BN_SHIFT) keeps BN's output, gradients and running statistics
+    at fp32 accuracy; unshifted storage loses most of the spread to the rounding."""
+    torch.manual_seed(11)
+    h = hip()
+    B, T, H, W, cin = 2, 4, 8, 8, 64
+    k, p = ((1, 1, 1), (0, 0, 0)) if group else ((1, 3, 3), (0, 0, 0))  # (no padding: uniform channel means)
+    widths = (96, 48) if group else (96,)
+    x = (3.0 + 0.5 * torch.randn(B, T, H, W, cin, device=DEV)).to(torch.bfloat16)
+    ws = [(0.02 + 0.01 * torch.randn(c, cin, *k, device=DEV)).to(torch.bfloat16).float() for c in widths]
+    xr = x.float()
+    ys = [F.conv3d(xr.permute(0, 4, 1, 2, 3), w, padding=p) for w in ws]
+    assert float(ys[0].mean()) > 20 * float(ys[0].std(dim=(0, 2, 3, 4)).mean())
+
+    def run(shift):
+        monkeypatch.setattr(h, "_BN_SHIFT", shift)
+        bns = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+        with torch.no_grad():
+            for bn, y in zip(bns, ys):
+                bn.running_mean.copy_(y.mean(dim=(0, 2, 3, 4)) + 0.05 * torch.randn_like(bn.running_mean))
+                bn.weight.uniform_(0.5, 1.5)
+        refs = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+        for r, bn in zip(refs, bns):
+            r.load_state_dict(bn.state_dict())
+        wp = [w.clone().requires_grad_(True) for w in ws]
+        xh = x.clone().requires_grad_(True)
+        if group:
+            zs = list(h.conv1x1_group_bn_relu(xh, wp, bns, True))[:len(widths)]
+        else:
+            zs = [h.conv_bn_relu(xh, wp[0], bns[0], (1, 1, 1), p, True)]
+        zs = [h._materialize(z) if h._is_lazy(z) else z for z in zs]
+        xf = xr.clone().requires_grad_(True)
+        wf = [w.clone().requires_grad_(True) for w in ws]
+        zrs = [aten.conv_bn_relu(xf, w, r, (1, 1, 1), p, True) for w, r in zip(wf, refs)]
+        dzs = [torch.randn_like(zr) for zr in zrs]
+        torch.autograd.backward(zs, [d.to(torch.bfloat16) for d in dzs])
+        torch.autograd.backward(zrs, dzs)
+        errs = {"out": max(rel_err(z, zr) for z, zr in zip(zs, zrs)), "dx": rel_err(xh.grad, xf.grad),
+                "dw": max(rel_err(a.grad, b.grad) for a, b in zip(wp, wf)),
+                "dgamma": max(rel_err(a.weight.grad, b.weight.grad) for a, b in zip(bns, refs))}
+        for bn, r in zip(bns, refs):  # the running mean gets the true (unshifted) batch mean
+            assert torch.allclose(bn.running_mean, r.running_mean, rtol=1e-3, atol=1e-3)
+            assert torch.allclose(bn.running_var, r.running_var, rtol=5e-2, atol=1e-3)
+        return errs
+
+    shifted, plain = run(True), run(False)
+    print("shifted", shifted, "plain", plain)
+    assert shifted["out"] < 2e-2 and shifted["dx"] < 3e-2 and shifted["dw"] < 3e-2 and shifted["dgamma"] < 3e-2
+    assert shifted["out"] < plain["out"] / 4
+
+
 def test_conv_bn_relu_eval_mode_backward():
     """Running-statistics BN (eval mode) is a fixed affine map: no batch-mean correction terms."""
     torch.manual_seed(6)
@@ -891,7 +944,7 @@ def test_stem_fwd_halo_kernel(B, T, S):
     wp = h._pack(w2, plan, 0)
     y = torch.empty((plan.B, plan.To, plan.Ho, plan.Wo, 64), dtype=torch.bfloat16, device=DEV)
     stats = torch.empty((256 * 128,), device=DEV)
-    n = lib().milnce_stem_fwd(ptr(x2), 0, ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), plan.B, plan.T,
+    n = lib().milnce_stem_fwd(ptr(x2), 0, ptr(wp), plan.Kpad, ptr(y), ptr(stats), stats.numel(), None, plan.B, plan.T,
                               plan.H, plan.W, stream())
     assert n > 0
     xr = x2.float().permute(0, 4, 1, 2, 3)
@@ -1152,7 +1205,8 @@ def test_step_weight_prepack_matches_per_call_pack():
 @pytest.mark.parametrize("B,T,HW,cin,cout", [(4, 8, 50, 192, 192), (4, 8, 25, 128, 128), (4, 4, 13, 96, 208),
                                              (8, 2, 7, 384, 384), (3, 5, 9, 24, 40), (2, 16, 10, 64, 64)])
 @pytest.mark.parametrize("bn", [64, 128, 192])
-def test_temporal_box_wgrad(B, T, HW, cin, cout, bn):
+@pytest.mark.parametrize("reg", [0, 1])
+def test_temporal_box_wgrad(B, T, HW, cin, cout, bn, reg):
     """csrc/conv_twgrad.hip (3,1,1) weight gradient (boxes of frames x flattened positions with a
     3-frame halo, 64/128/192-wide output tiles, partial boxes / channel chunks / output tiles) vs the
     fp32 F.conv3d weight gradient of the same bf16 operands; slab + accumulate paths."""
@@ -1164,9 +1218,9 @@ def test_temporal_box_wgrad(B, T, HW, cin, cout, bn):
     ref = torch.nn.grad.conv3d_weight(x.permute(0, 4, 1, 2, 3).float(), (cout, cin, 3, 1, 1),
                                       dy.permute(0, 4, 1, 2, 3).float(), padding=(1, 0, 0))
     out = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
-    h._twgrad(dy, x, plan, bn, out, 0)
+    h._twgrad(dy, x, plan, bn, out, 0, reg=reg)
     assert rel_err(out, ref) < 1e-4, rel_err(out, ref)
-    h._twgrad(dy, x, plan, bn, out, 1, occ=2)  # accumulate, another split count
+    h._twgrad(dy, x, plan, bn, out, 1, occ=2, reg=reg)  # accumulate, another split count
     assert rel_err(out, 2 * ref) < 1e-4
 
 

@@ -43,8 +43,9 @@ for B, T, H, W, Cin, Cout, k in SHAPES:
         t = timeit(lambda: h._halo_wgrad(dy, x, plan, cc, out, 0))
         res.append(f"halo cc{cc} {t:.3f} ms {fl / t / 1e9:.0f} TF/s")
     if k == (3, 1, 1):  # temporal box wgrad (csrc/conv_twgrad.hip), output tile x workgroups per CU
-        for bn in h._tw_tiles(Cout):
-            for occ in (1, 2):
-                t = timeit(lambda: h._twgrad(dy, x, plan, bn, out, 0, occ))
-                res.append(f"tw{bn}/o{occ} {t:.3f} ms {fl / t / 1e9:.0f} TF/s")
+        for reg in (0, 1):
+            for bn in h._tw_tiles(Cout):
+                for occ in (1, 2):
+                    t = timeit(lambda: h._twgrad(dy, x, plan, bn, out, 0, occ, reg))
+                    res.append(f"tw{'r' if reg else ''}{bn}/o{occ} {t:.3f} ms {fl / t / 1e9:.0f} TF/s")
     print(f"{(B, T, H, W, Cin)}->{Cout} k{k}: " + " | ".join(res), flush=True)

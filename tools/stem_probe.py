@@ -33,7 +33,7 @@ def main():
     st2 = torch.empty((256 * 128,), device="cuda")
     for _ in range(o.reps):
         h.conv_forward_raw(x2, wp, plan, stats)  # generic implicit GEMM
-        lib().milnce_stem_fwd(ptr(x2), 0, ptr(wp), plan.Kpad, ptr(y), ptr(st2), st2.numel(), plan.B, plan.T, plan.H,
+        lib().milnce_stem_fwd(ptr(x2), 0, ptr(wp), plan.Kpad, ptr(y), ptr(st2), st2.numel(), None, plan.B, plan.T, plan.H,
                               plan.W, stream())  # halo kernel
         h.conv_wgrad(dy, x2, plan)
     torch.cuda.synchronize()
