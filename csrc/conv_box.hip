@@ -59,6 +59,10 @@ static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per threa
 #ifndef BOX_TRACE
 #define BOX_TRACE 0
 #endif
+// Fragment double-buffering across the K steps of a tap (see the tap loop); 0 for A/B libraries
+#ifndef BOX_PIPE
+#define BOX_PIPE 1
+#endif
 // EPI 2 epilogue rows prefetched into L2 during the last block (y_prefetch). Off: the A/B
 // (gpurun_out r4ypf) measured 4351 / 4355 pairs/s without it against 4323 / 4335 with it (the
 // EPI 2 variants spill more and the (1,3,3) dgrad of conv_2c went 2.24 -> 2.55 ms)
@@ -692,22 +696,38 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           const int ch = MF == 16 ? ks * 4 + (lane >> 4) : ks * 2 + (lane >> 5);
           return *(const bf16x8*)(bsh + row * BK + swz<BK>(row, ch) * 8);
         };
+        // fragments double-buffered across the K steps (BOX_PIPE): step ks + 1's LDS reads are in
+        // flight while step ks's MFMAs issue, instead of every step waiting out the LDS latency
+        // before its MFMAs (the register sets alternate, so the reads need not wait for the MFMAs
+        // that still read the previous set)
+        // (only where a second fragment set fits the VGPR budget: 32x32 tiles, narrow 16x16 ones;
+        // not the 192-wide (3,1,1) variants, which then spill ~25 VGPRs)
+        constexpr bool PIPE = BOX_PIPE && (TM + TN) * 4 <= 24 && !(KS == 311 && BN == 192);
+        bf16x8 xf[PIPE ? 2 : 1][TM], wf[PIPE ? 2 : 1][TN];
+        auto frags = [&](int ks, int b) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i) xf[b][i] = xfrag(ks, i);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) wf[b][j] = wfrag(ks, j);
+        };
+        if constexpr (PIPE) frags(0, 0);
 #pragma unroll
         for (int ks = 0; ks < KSTEPS; ++ks) {
-          bf16x8 xf[TM], wf[TN];
-#pragma unroll
-          for (int i = 0; i < TM; ++i) xf[i] = xfrag(ks, i);
-#pragma unroll
-          for (int j = 0; j < TN; ++j) wf[j] = wfrag(ks, j);
+          const int b = PIPE ? (ks & 1) : 0;
+          if constexpr (PIPE) {
+            if (ks + 1 < KSTEPS) frags(ks + 1, b ^ 1);
+          } else {
+            frags(ks, 0);
+          }
           __builtin_amdgcn_s_setprio(1);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int i = 0; i < TM; ++i)
               if constexpr (MF == 16)
-                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[b][j], xf[b][i], acc[j][i], 0, 0, 0);
               else
-                acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[j], xf[i], acc[j][i], 0, 0, 0);
+                acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[b][j], xf[b][i], acc[j][i], 0, 0, 0);
           __builtin_amdgcn_s_setprio(0);
         }
         ++gs;

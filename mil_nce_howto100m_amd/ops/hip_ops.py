@@ -1106,11 +1106,14 @@ def _bn_shift(rmeans, training: bool) -> Optional[torch.Tensor]:
     if len(rmeans) == 1:
         return rmeans[0]
     ctot = sum(int(r.numel()) for r in rmeans)
-    buf = getattr(rmeans[0], "_milnce_group_shift", None)
-    if buf is None or buf.numel() != ctot or buf.device != rmeans[0].device:
-        buf = torch.cat([r.detach() for r in rmeans])
-        rmeans[0]._milnce_group_shift = buf
-    return buf
+    cached = getattr(rmeans[0], "_milnce_group_shift", None)
+    # rebuilt when a running mean was modified from Python (load_state_dict, copy_: the version
+    # counters move; the finalize kernel's own updates do not, and it advances the buffer itself)
+    vers = tuple(r._version for r in rmeans)
+    if cached is None or cached[1] != vers or cached[0].numel() != ctot or cached[0].device != rmeans[0].device:
+        cached = (torch.cat([r.detach() for r in rmeans]), vers)
+        rmeans[0]._milnce_group_shift = cached
+    return cached[0]
 
 
 def _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps, training,

@@ -174,6 +174,12 @@ def test_inception_head_prologue_fusion():
             b = copy.deepcopy(blk)
             xi = x.clone().requires_grad_(True)
             b(xi).sum().backward()  # tune
+            # the same running statistics in both arms (the pre-BN storage shift is the running
+            # mean, and the tuning pass ran different kernels, i.e. summation orders, per arm)
+            if fuse:
+                b.load_state_dict(bufs, strict=False)
+            else:
+                bufs = {n: t.clone() for n, t in b.named_buffers()}
             for cin, cout in ((96, 128), (16, 32)):  # the spatial convs reading z1a / z2a: box-tiled
                 plan = h.conv_plan(tuple(shape) + (cin,), (cout, cin, 1, 3, 3), (1, 1, 1), (0, 1, 1))
                 plan.impl = 15
@@ -181,11 +187,8 @@ def test_inception_head_prologue_fusion():
             b.zero_grad()
             out = b(xi)
             out.backward(g)
-            res[fuse] = (out.detach().float(), xi.grad.float(), {n: p.grad.clone() for n, p in b.named_parameters()},
-                         {n: t.clone() for n, t in b.named_buffers()})
-        (o0, x0, g0, b0), (o1, x1, g1, b1) = res[False], res[True]
-        print("out", _rel(o1, o0), "dx", _rel(x1, x0), "params", max(_rel(g1[n], g0[n]) for n in g0))
-        print("buffers", {n: (b0[n].float() - b1[n].float()).abs().max().item() for n in b0})
+            res[fuse] = (out.detach().float(), xi.grad.float(), {n: p.grad.clone() for n, p in b.named_parameters()})
+        (o0, x0, g0), (o1, x1, g1) = res[False], res[True]
         assert _rel(o1, o0) < 2e-3 and _rel(x1, x0) < 5e-3
         for n in g0:
             assert _rel(g1[n], g0[n]) < 1e-2, n

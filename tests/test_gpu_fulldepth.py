@@ -105,7 +105,8 @@ def test_full_depth_blocks_teacher_forced():
     assert worst["out"] < 0.02
     for key in ("dx", "flat", "param"):
         assert worst[key] <= 1.25 * worst_b[key] + 0.01, (key, worst[key], worst_b[key])
-    assert worst["dx"] < 0.15 and worst["flat"] < 0.15
+    # measured worst 0.092 / 0.091 (profiles/r4_fulldepth.md)
+    assert worst["dx"] < 0.11 and worst["flat"] < 0.11
 
 
 def test_full_depth_end_to_end_vs_fp32():

@@ -4,6 +4,8 @@ Inputs are generated in bf16 (the kernels' storage type) and the reference runs 
 same (upcast) values, so the tolerance covers accumulation order and the bf16 rounding of the
 outputs only. Run on an MI355X: ``pytest -m gpu``.
 """
+import copy
+
 import pytest
 import torch
 import torch.nn as nn
@@ -885,10 +887,14 @@ def test_fused_bn_backward_partials_match_unfused():
     convs = [nn.Conv3d(c0, c1, (1, 3, 3), 1, (0, 1, 1), bias=False).to(DEV),
              nn.Conv3d(c1, c2, (3, 1, 1), 1, (1, 0, 0), bias=False).to(DEV)]
     bns = [nn.BatchNorm3d(c1).to(DEV), nn.BatchNorm3d(c2).to(DEV)]
+    # both runs from the same running statistics: they are the pre-BN storage shift, and this
+    # small chain's gradients move ~6 % with any bf16 rounding change (both bf16 paths are ~6.5 %
+    # from fp32 here, shift on or off: tools/debug/shift_chain.py)
+    bns_plain = copy.deepcopy(bns)
     fused = _stack_grads(h, x, convs, bns)
     old = h.set_bn_bwd_fusion(False)
     try:
-        plain = _stack_grads(h, x, convs, bns)
+        plain = _stack_grads(h, x, convs, bns_plain)
     finally:
         h.set_bn_bwd_fusion(old)
     for a, b in zip(fused, plain):

@@ -12,9 +12,13 @@ conv outputs' channel means dwarf their spread in many layers (printed as |mean|
 """
 import argparse
 import copy
+import os
+import sys
 import time
 
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 BLOCKS = ["mixed_3b", "mixed_3c", "mixed_4b", "mixed_4c", "mixed_4d", "mixed_4e", "mixed_4f", "mixed_5b", "mixed_5c"]
 
