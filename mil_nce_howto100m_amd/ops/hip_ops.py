@@ -89,6 +89,17 @@ def _ceil(a: int, b: int) -> int:
     return (a + b - 1) // b
 
 
+# MILNCE_TUNE_LOG=path: append one line per wgrad tuning decision (layer shape -> kernel), for
+# mapping a step trace's kernels to layers (tools/gpu scripts)
+_TUNE_LOG = os.environ.get("MILNCE_TUNE_LOG", "")
+
+
+def _tune_log(line: str) -> None:
+    if _TUNE_LOG:
+        with open(_TUNE_LOG, "a") as f:
+            f.write(line + "\n")
+
+
 def _plan_sig(plan) -> str:
     """Problem identity of a conv plan for rank-consistent tuning (tune_sync)."""
     return (f"|B{plan.B}T{plan.T}H{plan.H}W{plan.W}|{plan.Cin}>{plan.Cout}|k{plan.k}s{plan.s}p{plan.p}"
@@ -1069,6 +1080,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             best = _tune(lambda c: launch_with(*inv[c], scratch, 0), tuple(code.values()),
                          default=code.get(default), sig=f"wgrad{_plan_sig(plan)}|{sorted(cands)}")
             tn, impl, occ, tk = inv[best]
+            _tune_log(f"wgrad{_plan_sig(plan)} -> tn {tn} impl {impl} occ {occ} tk {tk}")
             plan.w_tn, plan.w_impl, plan.w_occ = tn, impl, occ
             if impl < 100:
                 plan.w_tk = tk
