@@ -230,11 +230,20 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
         for (int k = 0; k < 8; ++k) raw[k] = f[k];
       }
       if constexpr (BN) {
+        // = the stored z (rounded in pairs: one v_cvt_pk_bf16_f32 per two channels, same bits)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f)));  // = the stored z
+        for (int k = 0; k < 8; k += 2) {
+          const uint32_t z2 = pack2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f), fmaxf(f[k + 1] * sc[k + 1] + sh[k + 1], 0.f));
+          f[k] = __uint_as_float(z2 << 16);
+          f[k + 1] = __uint_as_float(z2 & 0xffff0000u);
+        }
         if constexpr (GATE) {  // SelfGating output z * gate[b, c], as gate_scale would store it
 #pragma unroll
-          for (int k = 0; k < 8; ++k) f[k] = bf2f(f2bf(f[k] * gv[k]));
+          for (int k = 0; k < 8; k += 2) {
+            const uint32_t g2 = pack2bf(f[k] * gv[k], f[k + 1] * gv[k + 1]);
+            f[k] = __uint_as_float(g2 << 16);
+            f[k + 1] = __uint_as_float(g2 & 0xffff0000u);
+          }
         }
       }
 #pragma unroll
