@@ -80,6 +80,11 @@ struct TwParams {
   int n_slices, c_chunks, splits;
   int Npad, Kdim;
   FastDiv fnbs, fntb;
+  // REG only, optional: x is the raw conv output of a BN layer and the operand is
+  // z = relu(x * scale + shift) (xss = that BN's [mean, invstd, scale, shift][Cin]), applied to the
+  // staged halo chunks as the forward's box prologue does (same roundings; padding rows stay zero),
+  // so the forward need not write z for this wgrad
+  const float* xss;
 };
 
 // REG = false: LDS-DMA ring of TW_NSTG stages (two boxes in flight). REG = true: register-staged
@@ -208,8 +213,16 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
   };
 
   if constexpr (REG) {
-    constexpr int NR = G::NSUB + 2;
+    constexpr int NR = G::NSUB + 3;  // NSUB dY chunks, 2 halo chunks, the halo chunks' validity (.x)
     const int rrow = tid >> 3, rch = tid & 7;
+    // this thread's 8 input channels (the chunk rch of the tile's channel block): BN-ReLU constants
+    float xsc[8], xsh[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = min(c0 + rch * 8 + k, p.Cin - 1);
+      xsc[k] = p.xss != nullptr ? p.xss[2 * p.Cin + c] : 0.f;
+      xsh[k] = p.xss != nullptr ? p.xss[3 * p.Cin + c] : 0.f;
+    }
     // box -> this thread's NSUB dY chunks (row rrow of each sub-image) and 2 halo chunks (rows rrow,
     // rrow + 64); every box issues all NR loads (past box_end / the halo: out of range, zeros), so
     // the vmcnt wait before a box's LDS write is the same count on every path
@@ -236,6 +249,7 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
           R[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(drs, off, 0, 0));
         }
       }
+      uint32_t valid = 0;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int r = rrow + 64 * j;
@@ -244,7 +258,9 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
         const bool v = (r < (p.bt + 2) << p.lbs) & ((unsigned)t < (unsigned)p.T) & (s < p.HW) & (c < p.Cin);
         const uint32_t off = v ? (uint32_t)((((long long)t * p.HW + s) * p.Cin + c) * 2) : 0x80000000u;
         R[G::NSUB + j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
+        valid |= (uint32_t)v << j;
       }
+      R[G::NSUB + 2] = make_uint4(valid, 0u, 0u, 0u);
     };
     auto rstore = [&](const uint4 (&R)[NR], int slot_i) {
       char* sd = smem + slot_i * G::STAGE_BYTES;
@@ -255,7 +271,15 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int r = rrow + 64 * j;
-        *(uint4*)(sx + r * 128 + tw_chunk(r, rch) * 16) = R[G::NSUB + j];
+        uint4 xv = R[G::NSUB + j];
+        if (p.xss != nullptr) {  // z = relu(x * scale + shift) of the real rows; padding stays zero
+          float f[8];
+          unpack8(xv, f);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) f[k] = fmaxf(f[k] * xsc[k] + xsh[k], 0.f);
+          xv = ((R[G::NSUB + 2].x >> j) & 1u) ? pack8(f) : make_uint4(0u, 0u, 0u, 0u);
+        }
+        *(uint4*)(sx + r * 128 + tw_chunk(r, rch) * 16) = xv;
       }
     };
     uint4 R0[NR], R1[NR], R2[NR];
@@ -376,13 +400,16 @@ MILNCE_API int milnce_twgrad_plan(int B, int T, int H, int W, int Cin, int Cout,
 // dW of a (3,1,1) / stride 1 / padding (1,0,0) conv: the split slab is written to `slab`; with dw
 // != null it is also reduced (accumulated when accumulate != 0) into dw [Cout][Cin_param][3][1][1].
 // reg != 0: the register-staged variant (REG = true).
+// xss (register-staged kernel only, else null): x is a BN layer's raw conv output and the operand
+// its relu(x * scale + shift), xss = [mean, invstd, scale, shift][Cin] (see TwParams::xss)
 MILNCE_API int milnce_twgrad(const void* dy, int ldd, const void* x, float* slab, float* dw, int accumulate, int B,
                              int T, int H, int W, int Cin, int Cin_param, int Cout, int bn, int splits, int reg,
-                             hipStream_t stream) {
-  if (!(bn == 64 || bn == 128 || bn == 192)) return (int)hipErrorInvalidValue;
+                             const float* xss, hipStream_t stream) {
+  if (!(bn == 64 || bn == 128 || bn == 192) || (xss != nullptr && !reg)) return (int)hipErrorInvalidValue;
   TwParams p;
   p.dy = (const bf16_t*)dy;
   p.x = (const bf16_t*)x;
+  p.xss = xss;
   p.slab = slab;
   p.B = B; p.T = T; p.HW = H * W; p.Cin = Cin; p.Cout = Cout; p.ldd = ldd;
   if (Cin % 8 || ldd % 8 || splits < 1) return (int)hipErrorInvalidValue;

@@ -76,7 +76,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_dtw_path": [P, I, I, I, P, P, P],
     "milnce_box_set_trace": [P],
     "milnce_twgrad_plan": [I] * 8 + [P, P],
-    "milnce_twgrad": [P, I, P, P, P, I] + [I] * 10 + [P],
+    "milnce_twgrad": [P, I, P, P, P, I] + [I] * 10 + [P, P],
 }
 
 # entry points that return something other than an int status

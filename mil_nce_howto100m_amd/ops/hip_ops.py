@@ -956,6 +956,11 @@ def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: Optional[torch.Tensor], 
 # their 3-frame halo staged once through a counted 3-deep LDS-DMA ring. In the wgrad tuner next to
 # the im2col / halo kernels (impl codes 1000 + N tile); MILNCE_TWGRAD=0 leaves it out.
 _TWGRAD = os.environ.get("MILNCE_TWGRAD", "1") != "0"
+# A temporal conv whose input is a BN-ReLU placeholder ("pro") and whose tuned wgrad is the
+# register-staged box wgrad: that wgrad applies the producer's BN-ReLU to its staged x rows itself,
+# so the forward's box kernel runs PRO 1 (applies it, writes no z): the input-sized z write of the
+# forward is gone (conv_2c's temporal conv: 2 GB per step). MILNCE_TW_PRO=0 keeps writing z.
+_TW_PRO = os.environ.get("MILNCE_TW_PRO", "1") != "0"
 _TW_OCCS = (1, 2)
 _TW_SPLITS: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
 
@@ -971,9 +976,11 @@ def _tw_tiles(cout: int) -> Tuple[int, ...]:
 
 
 def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accumulate: int, occ: int = 1,
-            reg: int = 1):
+            reg: int = 1, xss: Optional[torch.Tensor] = None):
     """Temporal box wgrad (reg: register-staged boxes, else the LDS-DMA ring); with ``target`` None
-    only the split slab is filled and (slab, splits, Npad, Kpad) of the pending reduction is returned."""
+    only the split slab is filled and (slab, splits, Npad, Kpad) of the pending reduction is returned.
+    ``xss`` (register-staged only): x is a BN layer's raw output and the operand relu(x * scale +
+    shift) with that layer's constants (see _TW_PRO)."""
     key = (id(plan), bn, occ)
     geo = _TW_SPLITS.get(key)
     if geo is None:
@@ -985,7 +992,8 @@ def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accu
         geo = _TW_SPLITS[key] = (int(floats.value), int(splits.value))
     slab = torch.empty((geo[0],), dtype=F32, device=dy.device)
     call("milnce_twgrad", ptr(dy), plan.Cout, ptr(x), ptr(slab), ptr(target) if target is not None else None,
-         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, bn, geo[1], int(reg), stream())
+         accumulate, plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cin_p, plan.Cout, bn, geo[1], int(reg), ptr(xss),
+         stream())
     return slab, geo[1], _ceil(plan.Cout, bn) * bn, 3 * plan.Cin
 
 
@@ -1032,6 +1040,13 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     acc = int(out is not None)
     dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
+    xss = None
+    if _is_pro(x):  # x stands for relu(y * scale + shift) of its producer BN (_TW_PRO)
+        yp, ssp, ldp = x._milnce_bn
+        if plan.w_impl >= 2000 and ldp == plan.Cin:  # the register-staged temporal wgrad applies it
+            x, xss = yp, ssp
+        else:
+            x = _materialize(x)
     if _STEM_WGRAD and _is_paired_stem(plan) and x.dtype in (BF16, torch.uint8):
         slab = torch.empty((256 * 64 * 672,), dtype=F32, device=dy.device)
         rc = lib().milnce_stem_wgrad(ptr(dy), ptr(x), int(x.dtype == torch.uint8), ptr(slab), slab.numel(), ptr(dw),
@@ -1045,7 +1060,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
         (slab, splits, Npad, Kpad) returned for the caller's reduction."""
         if impl >= 1000:  # temporal box wgrad: N tile impl % 1000, register-staged from 2000
-            return _twgrad(dy, x, plan, impl % 1000, target, accumulate, occ, int(impl >= 2000))
+            return _twgrad(dy, x, plan, impl % 1000, target, accumulate, occ, int(impl >= 2000),
+                           xss if impl >= 2000 else None)
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
             return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
         npad, kpad, splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, tk, occ)
@@ -1275,9 +1291,15 @@ class _ConvBNReLU(torch.autograd.Function):
         pro, x_saved = None, x
         if _is_pro(x):
             # x stands for its producer's relu(y * scale + shift): this conv's kernel applies it
-            # and writes z (the wgrad operand) when one is needed
-            x_saved = torch.empty(x.shape, dtype=BF16, device=x.device) if need_z else None
-            pro = (x_saved,)
+            # and writes z (the wgrad operand) when one is needed -- not when the tuned wgrad
+            # applies it itself (_TW_PRO: x stays the placeholder)
+            plan0 = conv_plan(x.shape, weight.shape, stride, padding, wo_override)
+            if need_z and _TW_PRO and plan0.w_impl >= 2000 and x._milnce_bn[2] == plan0.Cin:
+                pro = (None,)
+                ctx.x_pro = x._milnce_bn
+            else:
+                x_saved = torch.empty(x.shape, dtype=BF16, device=x.device) if need_z else None
+                pro = (x_saved,)
         plan, y, ss = _conv_bn_stats(x, weight, gamma, beta, rmean, rvar, nbt, stride, padding, momentum, eps,
                                      training, wo_override, pro)
         C = plan.Cout
@@ -1307,6 +1329,9 @@ class _ConvBNReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz, *unused):
         x, weight, y, ss, gamma = ctx.saved_tensors
+        x_pro = getattr(ctx, "x_pro", None)
+        if x_pro is not None and not _is_pro(x):  # (the saved placeholder without its tags)
+            x = _pro_z(x.shape, x.device, x_pro)
         dx, dw, dgamma, dbeta = _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma)
         return dx, dw, dgamma, dbeta, None, None, None, None, None, None, None, None, None, None, None, None
 

@@ -1230,6 +1230,60 @@ def test_temporal_box_wgrad(B, T, HW, cin, cout, bn, reg):
     assert rel_err(out, 2 * ref) < 1e-4
 
 
+@pytest.mark.parametrize("B,T,HW,cin,cout", [(4, 8, 13, 192, 192), (3, 5, 9, 24, 40)])
+@pytest.mark.parametrize("bn", [64, 192])
+def test_temporal_box_wgrad_bn_relu_operand(B, T, HW, cin, cout, bn):
+    """The register-staged temporal wgrad applying its input's BN-ReLU itself (xss: the producer's
+    [mean, invstd, scale, shift], padding rows kept zero) is bitwise the same kernel on the
+    materialised z = relu(y * scale + shift) (bn_relu_apply)."""
+    from mil_nce_howto100m_amd.ops._lib import call, ptr, stream
+    h = hip()
+    torch.manual_seed(B + T + cin + cout + bn)
+    y = torch.randn(B, T, HW, HW, cin, device=DEV).to(torch.bfloat16)
+    ss = torch.stack([torch.randn(cin), torch.rand(cin) + 0.5, torch.rand(cin) + 0.5, torch.randn(cin) * 0.5])
+    ss = ss.to(DEV).reshape(-1).contiguous()
+    z = torch.empty_like(y)
+    call("milnce_bn_relu_apply", ptr(y), cin, ptr(z), cin, ptr(ss), cin, B, T * HW * HW, None, stream())
+    dy = torch.randn(B, T, HW, HW, cout, device=DEV).to(torch.bfloat16)
+    plan = h.conv_plan(y.shape, (cout, cin, 3, 1, 1), (1, 1, 1), (1, 0, 0))
+    a = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
+    b = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
+    h._twgrad(dy, z, plan, bn, a, 0, reg=1)
+    h._twgrad(dy, y, plan, bn, b, 0, reg=1, xss=ss)
+    assert torch.equal(a, b)
+
+
+def test_temporal_conv_without_forward_z_write(monkeypatch):
+    """A separable unit whose temporal conv's tuned wgrad is the register-staged box wgrad: with
+    _TW_PRO the forward kernel writes no z and the wgrad applies the spatial BN-ReLU itself;
+    outputs and every gradient are bitwise those of the z-writing path."""
+    import copy
+    from mil_nce_howto100m_amd.models.s3dg import STConv3D
+    h = hip()
+    torch.manual_seed(29)
+    shape, cin, cmid = (4, 8, 13, 13), 64, 128
+    unit = STConv3D(cin, cmid, [3, 3, 3], padding=1, separable=True).to(DEV).train()
+    x = torch.randn(*shape, cin, device=DEV).to(torch.bfloat16)
+    g = torch.randn(*shape, cmid, device=DEV).to(torch.bfloat16)
+    plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, 3, 1, 1), (1, 1, 1), (1, 0, 0))
+    res = {}
+    for tw_pro in (False, True):
+        monkeypatch.setattr(h, "_TW_PRO", tw_pro)
+        u = copy.deepcopy(unit)
+        xi = x.clone().requires_grad_(True)
+        u(xi).backward(g)  # tunes
+        plan.w_impl, plan.w_tn, plan.w_occ = 2128, 128, 1  # the register-staged box wgrad, N tile 128
+        xi.grad = None
+        u.zero_grad()
+        out = u(xi)
+        out.backward(g)
+        res[tw_pro] = (out.detach(), xi.grad.clone(), {n: p.grad.clone() for n, p in u.named_parameters()})
+    (o0, x0, g0), (o1, x1, g1) = res[False], res[True]
+    assert torch.equal(o0, o1) and torch.equal(x0, x1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
+
+
 def _inception_block_run(h, batch_gsum):
     from mil_nce_howto100m_amd.models.s3dg import InceptionBlock
     old = h._BATCH_GSUM
