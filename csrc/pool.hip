@@ -268,6 +268,120 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
   }
 }
 
+// Pair forward for the 1x3x3 / (1,2,2) windows without leading padding (maxpool_2a / 3a): a thread
+// owns two horizontally adjacent output cells (one 8-channel chunk) and reads the 3 x 5 input patch
+// under them once, each cell feeding the one or two windows that contain it: 7.5 loads and BN /
+// gate transforms per output instead of 9 (the BN forward is VALU-bound on the per-tap transform).
+// Cells are visited in (h, w) order, so each window still sees its taps in scan order and the first
+// maximum wins. Without leading padding every window starts with a real cell and a trailing zero
+// pad never beats it, so the arg-max is a real cell and yr is the raw value there. (A 2x2-quad
+// version needed 4 windows of state and ran slower: occupancy and compare-mask pressure.)
+template <bool BN = false, bool GATE = false>
+__global__ __launch_bounds__(256) void maxpool_fwd_pair(PoolParams p, PoolDivs d, const bf16_t* __restrict__ x,
+                                                        bf16_t* __restrict__ y, uint8_t* __restrict__ arg,
+                                                        uint32_t npair_chunks, int Wq,
+                                                        const float* __restrict__ ss = nullptr,
+                                                        const float* __restrict__ gate = nullptr,
+                                                        bf16_t* __restrict__ yr = nullptr) {
+  constexpr bool YR = BN && !GATE;
+  const FastDiv fWq = d.fmw;  // Wq, set by the launcher
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npair_chunks; i += gridDim.x * blockDim.x) {
+    const uint32_t r = fdiv(i, d.fcpr);
+    const int c0 = (int)(i - r * d.fcpr.d) * 8;
+    const uint32_t q = fdiv(r, fWq);
+    const int wq = (int)(r - q * Wq);
+    const uint32_t q2 = fdiv(q, d.fHo);
+    const int ho = (int)(q - q2 * p.Ho);
+    const uint32_t b = fdiv(q2, d.fTo);
+    const int to = (int)(q2 - b * p.To);
+    const bf16_t* xb = x + ((size_t)b * p.T + to) * p.H * p.W * p.C + c0;
+    const int h0 = 2 * ho, w0 = 4 * wq;
+    uint4 v[3][5];
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < 5; ++cc) {
+        const bool in = (h0 + rr < p.H) & (w0 + cc < p.W);
+        v[rr][cc] = *(const uint4*)(xb + (in ? ((size_t)(h0 + rr) * p.W + w0 + cc) * p.C : 0));
+      }
+    float sc[8], sh[8], gv[8];
+    if constexpr (BN) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        sc[k] = ss[2 * p.C + c0 + k];
+        sh[k] = ss[3 * p.C + c0 + k];
+        if constexpr (GATE) gv[k] = gate[(size_t)b * p.C + c0 + k];
+      }
+    }
+    float best[2][8], braw[YR ? 2 : 1][8];
+    uint32_t bi[2][8];
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        best[o][k] = -INFINITY;
+        bi[o][k] = 0u;
+        if constexpr (YR) braw[o][k] = 0.f;
+      }
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr)
+#pragma unroll
+      for (int cc = 0; cc < 5; ++cc) {
+        const bool in = (h0 + rr < p.H) & (w0 + cc < p.W);
+        const bool cand = in | (p.zero_pad & (h0 + rr < p.Hp) & (w0 + cc < p.Wp));
+        float f[8], raw[8];
+        unpack8(v[rr][cc], f);
+        if constexpr (YR) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) raw[k] = f[k];
+        }
+        if constexpr (BN) {  // = the stored z (rounded in pairs)
+#pragma unroll
+          for (int k = 0; k < 8; k += 2) {
+            const uint32_t z2 = pack2bf(fmaxf(f[k] * sc[k] + sh[k], 0.f), fmaxf(f[k + 1] * sc[k + 1] + sh[k + 1], 0.f));
+            f[k] = __uint_as_float(z2 << 16);
+            f[k + 1] = __uint_as_float(z2 & 0xffff0000u);
+          }
+          if constexpr (GATE) {  // SelfGating output z * gate[b, c], as gate_scale would store it
+#pragma unroll
+            for (int k = 0; k < 8; k += 2) {
+              const uint32_t g2 = pack2bf(f[k] * gv[k], f[k + 1] * gv[k + 1]);
+              f[k] = __uint_as_float(g2 << 16);
+              f[k + 1] = __uint_as_float(g2 & 0xffff0000u);
+            }
+          }
+        }
+        const float pad = cand ? 0.f : -INFINITY;
+#pragma unroll
+        for (int o = 0; o < 2; ++o) {
+          const int dw = cc - 2 * o;
+          if (dw < 0 || dw > 2) continue;  // compile time after unrolling
+          const uint32_t tap = (uint32_t)(rr * 3 + dw);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const float val = in ? f[k] : pad;
+            const bool gt = val > best[o][k];
+            best[o][k] = gt ? val : best[o][k];
+            bi[o][k] = gt ? tap : bi[o][k];
+            if constexpr (YR) braw[o][k] = gt ? raw[k] : braw[o][k];
+          }
+        }
+      }
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int wo = 2 * wq + o;
+      if (wo >= p.Wo) continue;
+      const size_t oo = ((((size_t)b * p.To + to) * p.Ho + ho) * p.Wo + wo) * p.C + c0;
+      *(uint4*)(y + oo) = pack8(best[o]);
+      *(uint2*)(arg + oo) = make_uint2(bi[o][0] | (bi[o][1] << 8) | (bi[o][2] << 16) | (bi[o][3] << 24),
+                                       bi[o][4] | (bi[o][5] << 8) | (bi[o][6] << 16) | (bi[o][7] << 24));
+      if constexpr (YR) {
+        if (yr != nullptr) *(uint4*)(yr + oo) = pack8(braw[o]);
+      }
+    }
+  }
+}
+
 // BN-backward partial sums of the pool input's producer (dx is that layer's dz), accumulated
 // per thread for its fixed channel chunk and reduced over the block's row groups in LDS:
 // part[blockIdx][2][C] (mask = y*scale + shift > 0, xhat = (y - mean) * invstd).
@@ -1158,6 +1272,24 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
                              const float* bn_ss = nullptr, const float* gate = nullptr, void* yr = nullptr) {
   if (n >= (1ll << 31)) return false;
   const PoolDivs d = make_divs(p);
+  // 1x3x3 / (1,2,2) windows without leading padding: the pair forward (maxpool_fwd_pair)
+  if (p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 && p.To == p.T &&
+      p.ph == 0 && p.pw == 0 && g_pool_quad) {
+    const int Wq = (p.Wo + 1) / 2;
+    const long long np = n / p.Wo * Wq;  // n = B*To*Ho*Wo*cpr
+    PoolDivs dq = d;
+    dq.fmw = make_fastdiv(Wq);
+    const long long g = (np + 255) / 256;
+    const int grid = (int)(g > 65536 ? 65536 : g);
+#define XPF(bn_, gt_)                                                                                           \
+    hipLaunchKernelGGL((maxpool_fwd_pair<bn_, gt_>), dim3(grid), dim3(256), 0, s, p, dq, (const bf16_t*)x,      \
+                       (bf16_t*)y, (uint8_t*)arg, (uint32_t)np, Wq, bn_ss, gate, (bf16_t*)yr);
+    if (bn_ss == nullptr) { XPF(false, false) }
+    else if (gate != nullptr) { XPF(true, true) }
+    else { XPF(true, false) }
+#undef XPF
+    return true;
+  }
   if (bn_ss != nullptr) {
     long long g = (n + 255) / 256;
     const int grid = (int)(g > 65536 ? 65536 : g);
