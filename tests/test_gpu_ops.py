@@ -1170,6 +1170,49 @@ def test_pool_block_gather_bitwise(shape, kernel, stride):
     assert rel_err(grads[1], xr.grad) < 1e-2
 
 
+@pytest.mark.parametrize("shape", [(2, 4, 100, 100, 64), (2, 8, 25, 25, 32), (2, 5, 11, 12, 24)])
+@pytest.mark.parametrize("mode", ["plain", "bn", "gate"])
+def test_pool_pair_forward_bitwise(shape, mode):
+    """The output-pair forward of the TF-SAME 1x3x3/(1,2,2) pool (csrc/pool.hip maxpool_fwd_pair:
+    even and odd planes, ties) is bitwise the per-output kernel: pooled values, arg-max bytes and
+    (BN mode) the raw input at the arg-max; plain mode also against the ATen TF-SAME pool."""
+    from mil_nce_howto100m_amd.ops._lib import lib, ptr, stream
+    torch.manual_seed(17)
+    h = hip()
+    B, T, H, W, C = shape
+    x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
+    x[:, :, :4, :4, :8] = 0.5  # ties
+    ss = torch.stack([torch.zeros(C), torch.ones(C), torch.rand(C) + 0.5, torch.rand(C) - 0.5]).to(DEV).reshape(-1)
+    gate = torch.rand(B, C, device=DEV)
+    (ph0, ph1), (pw0, pw1) = aten.tf_same_pad((3, 3), (2, 2))
+    Ho, Wo = h._pool_out(H, 3, 2, ph0, ph1), h._pool_out(W, 3, 2, pw0, pw1)
+    geo = [B, T, H, W, C, T, Ho, Wo, 1, 3, 3, 1, 2, 2, 0, 0, ph0, ph1, pw0, pw1, 1]
+    res = {}
+    for on in (1, 0):
+        lib().milnce_pool_set_quad(on)
+        try:
+            y = torch.empty((B, T, Ho, Wo, C), dtype=torch.bfloat16, device=DEV)
+            arg = torch.empty(y.shape, dtype=torch.uint8, device=DEV)
+            yr = torch.empty_like(y)
+            if mode == "plain":
+                rc = lib().milnce_maxpool_fwd(ptr(x), ptr(y), ptr(arg), *geo, stream())
+            elif mode == "bn":
+                rc = lib().milnce_bn_relu_maxpool_fwd(ptr(x), ptr(ss), ptr(y), ptr(arg), *geo, ptr(yr), stream())
+            else:
+                rc = lib().milnce_bn_relu_gate_maxpool_fwd(ptr(x), ptr(ss), ptr(gate), ptr(y), ptr(arg), *geo,
+                                                           stream())
+            assert rc == 0
+            torch.cuda.synchronize()
+            res[on] = (y, arg, yr)
+        finally:
+            lib().milnce_pool_set_quad(1)
+    assert torch.equal(res[1][0], res[0][0]) and torch.equal(res[1][1], res[0][1])
+    if mode == "bn":
+        assert torch.equal(res[1][2], res[0][2])
+    if mode == "plain":
+        assert torch.equal(res[1][0].float(), aten.maxpool_tf_same(x.float(), (1, 3, 3), (1, 2, 2)))
+
+
 def test_step_weight_prepack_matches_per_call_pack():
     """The one-launch step pre-pack (hip_ops._WeightPacker) is bitwise identical to the per-conv
     pack for forward and dgrad layouts, and only kicks in from the second step."""
