@@ -13,6 +13,7 @@ struct PoolParams {
   int kt, kh, kw, st, sh, sw, pt, ph, pw;  // front padding
   int Tp, Hp, Wp;                          // padded extents (input + front + back padding)
   int zero_pad;                            // 1: padded cells are zeros (candidates); 0: -inf (ignored)
+  int s1_codes;                            // stride-1 plane sweeps: 1 = workgroup-order codes (S1Geo)
 };
 
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(PoolParams p, const bf16_t* __restrict__ x,
@@ -911,10 +912,20 @@ __global__ __launch_bounds__(256) void maxpool_s1_bwd_slide(PoolParams p, PoolDi
 // with out-of-range offsets for idle lanes (branch-free, so counted vmcnt waits keep the
 // prefetches in flight across the LDS-only barriers), and the workgroup owns complete
 // (clip, channel) planes, so plane sums need no atomics. Requires T*H*G <= 512.
+//
+// The arg-max codes of the sweeps are stored in workgroup order (only the sweep backward reads
+// them): per clip [chunk][W][T*H][gc][8] bytes (gc = the chunk's channel groups), i.e. a column of
+// a workgroup is one contiguous run in thread order and a wave's 8-B code stores / loads cover
+// whole 128-B lines. In the activation layout each (row, group) is 8 B of a 128-B line that the
+// clip's other workgroups fill at other times: the forward's L2 -> HBM write requests were mostly
+// partial lines (tools/gpu/pool_pmc.sh). The layout depends on G, which s1_groups derives from the
+// shape alone (and the workgroup-size cap, which must not change between forward and backward).
 struct S1Geo {
   int rows, G, nchunk, b, chunk, r, g, t, h;
   bool active;
   uint32_t e0;  // element offset (in the clip) of this thread's column 0, or out of range
+  uint32_t a0;   // byte offset (in the clip's codes) of this thread's column-0 code, or out of range
+  uint32_t acs;  // code bytes per column of this chunk
 };
 
 __device__ __forceinline__ S1Geo s1_geo(const PoolParams& p, int G, int nchunk) {
@@ -932,6 +943,14 @@ __device__ __forceinline__ S1Geo s1_geo(const PoolParams& p, int G, int nchunk) 
   s.t = s.r / p.H;
   s.h = s.r - s.t * p.H;
   s.e0 = s.active ? (uint32_t)(s.r * p.W * p.C + cg * 8) : 0x40000000u;
+  const int gc = min(G, (p.C >> 3) - s.chunk * G);  // groups of this chunk (the last may be partial)
+  if (p.s1_codes) {
+    s.a0 = s.active ? (uint32_t)(s.chunk * G * p.W * s.rows * 8 + (s.r * gc + s.g) * 8) : 0x40000000u;
+    s.acs = (uint32_t)(s.rows * gc * 8);
+  } else {  // activation layout (A/B runs)
+    s.a0 = s.e0;
+    s.acs = (uint32_t)p.C;
+  }
   return s;
 }
 
@@ -977,7 +996,9 @@ __device__ __forceinline__ void max3(const float* a, bool va, const float* b, bo
 
 constexpr int S1_PF = 8;  // forward sweep: register ring of input columns (6 loads in flight)
 
-template <int WT>  // WT = W when specialised (the sweep is then fully unrolled), 0 = runtime W
+// WT = W when specialised (the sweep is then fully unrolled), 0 = runtime W. (Two output columns
+// per step, sharing the h / t stages' barriers, ran 5-40 % slower: tools/pool_bench.py, r4.)
+template <int WT>
 __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, int nchunk, const bf16_t* __restrict__ x,
                                                           bf16_t* __restrict__ y, uint8_t* __restrict__ arg) {
   extern __shared__ uint4 s1_lds[];  // m1 [rows+1][G], m2 [rows+1][G] (bf16 x 8); row `rows`: idle lanes
@@ -997,6 +1018,7 @@ __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, i
   const int ihm = vhm ? me - G : me, ihp = vhp ? me + G : me;
   const int itm = vtm ? me - p.H * G : me, itp = vtp ? me + p.H * G : me;
   auto col = [&](int w) { return (w >= 0 && w < p.W) ? (s.e0 + (uint32_t)w * ecol) : oob; };
+  auto acol = [&](int w) { return (w >= 0 && w < p.W) ? (s.a0 + (uint32_t)w * s.acs) : oob; };
   // register ring of input columns, slot = column % S1_PF (column -1 reads as zeros): the loop is
   // unrolled by the ring size so a pending load is never copied between registers (a copy would
   // make the compiler wait for it), i.e. S1_PF - 2 columns stay in flight across the barriers
@@ -1029,15 +1051,14 @@ __global__ __launch_bounds__(512) void maxpool_s1_fwd_sep(PoolParams p, int G, i
       unpack8(m2s[itm], fa);
       unpack8(m2s[itp], fc);
       max3(fa, vtm, m2, true, fc, vtp, o, ct);
-      const uint32_t off = col(s.active ? w : -1);
-      bst16(yr, off * 2, pack8(o));
+      bst16(yr, col(s.active ? w : -1) * 2, pack8(o));
       uint32_t cb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) cb[k] = cw[k] | (ch[k] << 2) | (ct[k] << 4);
       uint2 a;
       a.x = cb[0] | (cb[1] << 8) | (cb[2] << 16) | (cb[3] << 24);
       a.y = cb[4] | (cb[5] << 8) | (cb[6] << 16) | (cb[7] << 24);
-      bst8(ar, off, a);
+      bst8(ar, acol(w), a);
     }
   }
 }
@@ -1080,6 +1101,7 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
   const int ihm = vhm ? me - G : me, ihp = vhp ? me + G : me;
   const int itm = vtm ? me - p.H * G : me, itp = vtp ? me + p.H * G : me;
   auto col = [&](int w) { return (w >= 0 && w < p.W) ? (s.e0 + (uint32_t)w * ecol) : oob; };
+  auto acol = [&](int w) { return (w >= 0 && w < p.W) ? (s.a0 + (uint32_t)w * s.acs) : oob; };
   auto code = [](const uint2& a, int k, int sh) {
     return ((((k < 4 ? a.x : a.y) >> (8 * (k & 3))) >> sh) & 3u);
   };
@@ -1089,13 +1111,13 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
 #pragma unroll
   for (int k = 0; k < 8; ++k) { sacc[k] = 0.f; dA[k] = 0.f; dB[k] = 0.f; }
   uint4 gcur = bld16(dyr, col(0) * 2);
-  uint2 acur = bld8(agr, col(0));
+  uint2 acur = bld8(agr, acol(0));
   for (int wo = 0; wo <= W; ++wo) {
     // emit operands of column wo-1 first, then the next column's gradient and codes
     const uint32_t ep = col(wo - 1);
     const uint4 ein = bld16(inr, ep * 2), xin = bld16(xr, ep * 2);
     const uint4 gnext = bld16(dyr, col(wo + 1) * 2);
-    const uint2 anext = bld8(agr, col(wo + 1));
+    const uint2 anext = bld8(agr, acol(wo + 1));
     float dC[8];  // dm1 of column wo
     uint2 cC = acur;
     if (wo < W) {
@@ -1291,11 +1313,12 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
     return true;
   }
   if (bn_ss != nullptr) {
+    if (is_s1_333(p) && s1_use_lds(p)) return false;  // its backward reads sweep-layout codes (S1Geo)
     long long g = (n + 255) / 256;
     const int grid = (int)(g > 65536 ? 65536 : g);
 #define X(a, b, c, e, f, h)                                                                                      \
     if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                            \
-      if (gate != nullptr)                                                                                       \
+      if (gate != nullptr)                                                                                           \
         hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, true>), dim3(grid), dim3(256), 0, s, p, d,     \
                            (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);               \
       else                                                                                                       \
@@ -1347,6 +1370,9 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
                              const float* gate_g = nullptr, const float* gate_dm = nullptr, float inv_thw = 0.f,
                              const float* coef = nullptr) {
   if (n >= (1ll << 31)) return false;
+  // codes in the sweep layout (the plane-sweep forward wrote them) are read by the sweep backward
+  // only, which has no BN-partials / gate / apply epilogues
+  if (is_s1_333(p) && s1_use_lds(p) && (bn_y != nullptr || gate_g != nullptr || coef != nullptr)) return false;
   const PoolDivs d = make_divs(p);
   if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
     const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
@@ -1412,6 +1438,12 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   return false;
 }
 
+static int g_s1_codes = 1;  // milnce_set_pool_s1_codes: code layout of the plane sweeps (S1Geo)
+MILNCE_API int milnce_set_pool_s1_codes(int on) {
+  const int old = g_s1_codes;
+  g_s1_codes = on != 0;
+  return old;
+}
 static PoolParams make_pool(int T, int H, int W, int C, int To, int Ho, int Wo, int kt, int kh, int kw, int st,
                             int sh, int sw, int pt0, int pt1, int ph0, int ph1, int pw0, int pw1, int zero_pad) {
   PoolParams p;
@@ -1420,6 +1452,7 @@ static PoolParams make_pool(int T, int H, int W, int C, int To, int Ho, int Wo, 
   p.pt = pt0; p.ph = ph0; p.pw = pw0;
   p.Tp = T + pt0 + pt1; p.Hp = H + ph0 + ph1; p.Wp = W + pw0 + pw1;
   p.zero_pad = zero_pad;
+  p.s1_codes = g_s1_codes;
   return p;
 }
 
@@ -1466,6 +1499,7 @@ MILNCE_API int milnce_maxpool_bwd(const void* dy, const void* arg, void* dx, int
   const long long n = (long long)B * T * H * W * (C / 8);
   if (pool_bwd_special(p, dy, arg, dx, n, bn_y, bn_ld, bn_ss, part, nparts, stream)) return (int)hipGetLastError();
   if (dx == nullptr) return (int)hipErrorInvalidValue;  // partials-only passes: specialised shapes
+  if (is_s1_333(p) && s1_use_lds(p)) return (int)hipErrorInvalidValue;  // sweep-layout codes (S1Geo)
   if (bn_y != nullptr && (256 % (C / 8) != 0 || bn_ld != C)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(nparts), dim3(256), 0, stream, p, (const bf16_t*)dy,
                      (const uint8_t*)arg, (bf16_t*)dx, n, (const bf16_t*)bn_y, bn_ss, part);

@@ -46,6 +46,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_maxpool_s1_bwd_fused": [P, P, P, P, P, P] + [I] * 5 + [P],
     "milnce_set_pool_s1_impl": [I],
     "milnce_set_pool_s1_maxthr": [I],
+    "milnce_set_pool_s1_codes": [I],
     "milnce_stem_wgrad": [P, P, I, P, L, P, I, I, I, I, I, P],
     "milnce_stem_wgrad_pool": [P, P, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
     "milnce_stem_fwd": [P, I, P, I, P, P, L, P, I, I, I, I, P],

@@ -1871,7 +1871,10 @@ class _MaxPool(torch.autograd.Function):
         ctx.geo = geo
         xb = getattr(x, "_milnce_bn", None)
         special = (tuple(kernel), tuple(stride)) in _POOL_SPECIAL  # csrc/pool.hip MILNCE_POOL_SHAPES
-        ctx.x_bn = xb if (xb is not None and (special or (256 % (C // 8) == 0 and xb[2] == C))) else None
+        # (the stride-1 plane sweep's codes are read by its own backward only, which takes no BN
+        # partials: csrc/pool.hip S1Geo)
+        s1 = tuple(kernel) == (3, 3, 3) and tuple(stride) == (1, 1, 1) and not tf_same
+        ctx.x_bn = xb if (xb is not None and not s1 and (special or (256 % (C // 8) == 0 and xb[2] == C))) else None
         # a SelfGating output: the backward also returns the gate's reduction sum dx * x
         ctx.x_gate = bool(getattr(x, "_milnce_gate", False)) and special and tf_same and ctx.x_bn is None
         if ctx.x_gate:

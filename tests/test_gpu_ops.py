@@ -414,9 +414,12 @@ def test_maxpool_tf_same_even_plane(shape):
     assert torch.equal(y.float(), yr)
 
 
-@pytest.mark.parametrize("shape", [(2, 16, 25, 9, 16), (3, 4, 13, 13, 56), (2, 2, 7, 7, 832), (1, 3, 1, 5, 8)])
+@pytest.mark.parametrize("shape", [(2, 16, 25, 9, 16), (3, 4, 13, 13, 56), (2, 2, 7, 7, 832), (1, 3, 1, 5, 8),
+                                   (256, 2, 3, 3, 56), (256, 8, 25, 25, 40)])
 def test_maxpool_s1_lds_shapes(shape):
-    """LDS plane-sweep stride-1 pool: > 256 plane rows (1 group), partial channel chunks, W=5/H=1."""
+    """LDS plane-sweep stride-1 pool: > 256 plane rows (1 group), W=5/H=1, and (batch 256: 2-group
+    workgroups over 7 / 5 channel groups) a partial last channel chunk, whose arg-max codes take a
+    narrower run of the sweep's workgroup-order code layout."""
     torch.manual_seed(12)
     h = hip()
     x = torch.randn(*shape, device=DEV).to(torch.bfloat16)

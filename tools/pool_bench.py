@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""Time the Inception branch-3 stride-1 max pool (forward and backward) at the flagship shapes
-(bs 256, 16x200x200 input) for both implementations: LDS plane sweep vs global sliding window.
+"""Time the Inception branch-3 stride-1 max pool at the flagship shapes (bs 256, 16x200x200 input):
+forward, plain backward and the fused backward of the model (+ the 1x1 head's dX, + the gate
+reduction sum dx * x), for both arg-code layouts of the LDS plane sweep (csrc/pool.hip S1Geo:
+workgroup order vs activation layout) and, with --slide, the global sliding-window kernels. The
+pooled values and the gradients must agree between variants (bitwise: same arg-max, same sums).
 
-    python tools/pool_bench.py
+    python tools/pool_bench.py [--slide] [--only I[,J..]]   (shape indices)
 """
 import os
 import sys
@@ -11,8 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from mil_nce_howto100m_amd.ops import hip_ops as h  # noqa: E402
-from mil_nce_howto100m_amd.ops._lib import lib  # noqa: E402
+from mil_nce_howto100m_amd.ops._lib import lib, ptr, stream  # noqa: E402
 
 SHAPES = [(256, 8, 25, 25, 192), (256, 8, 25, 25, 256), (256, 4, 13, 13, 480), (256, 4, 13, 13, 512),
           (256, 4, 13, 13, 528), (256, 2, 7, 7, 832)]
@@ -32,22 +34,44 @@ def timeit(fn, reps=20):
 
 def main():
     L = lib()
-    print(f"{'shape':32s} {'impl':6s} {'fwd us':>8s} {'bwd us':>8s} {'GB/s fwd':>9s} {'GB/s bwd':>9s}")
-    for shp in SHAPES:
+    variants = [(1, 1, "wgord"), (1, 0, "actlay")] + ([(0, 1, "slide")] if "--slide" in sys.argv else [])
+    print(f"{'shape':28s} {'impl':6s} {'fwd us':>8s} {'bwd us':>8s} {'fused us':>8s} {'GB/s fwd':>9s} "
+          f"{'GB/s bwd':>9s} {'GB/s fus':>9s}")
+    shapes = SHAPES
+    if "--only" in sys.argv:
+        shapes = [SHAPES[int(i)] for i in sys.argv[sys.argv.index("--only") + 1].split(",")]
+    for shp in shapes:
+        B, T, H, W, C = shp
         x = torch.randn(*shp, device="cuda").to(torch.bfloat16)
         dy = torch.randn(*shp, device="cuda").to(torch.bfloat16)
+        acc = torch.randn(*shp, device="cuda").to(torch.bfloat16)
+        y, dx = torch.empty_like(x), torch.empty_like(x)
+        arg = torch.empty(shp, dtype=torch.uint8, device="cuda")
+        gs = torch.zeros(B, C, device="cuda")
+        geo = [B, T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0]
         nb = x.numel() * 2
-        for impl, name in ((1, "lds"), (0, "slide")):
+        ref = None
+        for impl, codes, name in variants:
             L.milnce_set_pool_s1_impl(impl)
-            xr = x.clone().requires_grad_(True)
-            f = lambda: h.maxpool3d(xr, (3, 3, 3), (1, 1, 1), False)  # noqa: E731
-            tf = timeit(f)
-            y = f()
-            tb = timeit(lambda: torch.autograd.grad(y, xr, dy, retain_graph=True))
-            # fwd: read x, write y + arg; bwd: read dy + arg, write dx
-            print(f"{str(shp):32s} {name:6s} {tf * 1e3:8.1f} {tb * 1e3:8.1f} {2.5 * nb / tf / 1e6:9.0f} "
-                  f"{2.5 * nb / tb / 1e6:9.0f}")
+            L.milnce_set_pool_s1_codes(codes)
+            fwd = lambda: L.milnce_maxpool_fwd(ptr(x), ptr(y), ptr(arg), *geo, stream())  # noqa: E731
+            bwd = lambda: L.milnce_maxpool_bwd(ptr(dy), ptr(arg), ptr(dx), *geo, None, 0, None, None, 2048,  # noqa: E731
+                                              stream())
+            fus = lambda: L.milnce_maxpool_s1_bwd_fused(ptr(dy), ptr(arg), ptr(acc), ptr(x), ptr(gs), ptr(dx),  # noqa: E731
+                                                       B, T, H, W, C, stream())
+            tf = timeit(fwd)
+            tb = timeit(bwd)
+            out = (y.clone(), dx.clone())
+            tu = timeit(fus) if impl == 1 else float("nan")
+            if ref is None:
+                ref = out
+            else:
+                assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]), (shp, name)
+            # fwd: read x, write y + arg; bwd: read dy + arg, write dx; fused: + acc_in, x
+            print(f"{str(shp):28s} {name:6s} {tf * 1e3:8.1f} {tb * 1e3:8.1f} {tu * 1e3:8.1f} "
+                  f"{2.5 * nb / tf / 1e6:9.0f} {2.5 * nb / tb / 1e6:9.0f} {4.5 * nb / tu / 1e6:9.0f}", flush=True)
     L.milnce_set_pool_s1_impl(1)
+    L.milnce_set_pool_s1_codes(1)
 
 
 if __name__ == "__main__":
