@@ -432,7 +432,10 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   bf16_t* ring = (bf16_t*)smem;  // stage s: A [BM][BK] then B [BN][BK]
   bf16_t* Es = (bf16_t*)smem;    // epilogue staging [BM][LDE] (after the ring drained)
   float* ssl = (float*)(smem + EPI_BYTES);  // [4][BN] producer-BN constants (EPI 2), per tile
-  (void)SSL_BYTES;
+  // EPI 1 shift of the block's (fixed) N tile, behind everything else: written once, read by every
+  // tile's epilogue from LDS (loaded per tile from global memory it cost a full vmcnt drain there)
+  constexpr int SHL_OFF = RING_BYTES > EPI_BYTES + SSL_BYTES ? RING_BYTES : EPI_BYTES + SSL_BYTES;
+  float* shl = (float*)(smem + SHL_OFF);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -460,6 +463,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
   float e_s[8], e_q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
+  if constexpr (EPI == 1) {  // published by the first tile's barriers
+    for (int t = tid; t < BN; t += NT) shl[t] = (p.bn_ss != nullptr && n0 + t < p.Cout) ? p.bn_ss[n0 + t] : 0.f;
+  }
 
   for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
     const int m0 = m_tile * BM;
@@ -622,14 +628,10 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
 
     // EPI 1: per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
     // rounding, so the stored pre-BN values keep their precision when |mean| >> std
-    float shv[TN][4];
+    float4 shv[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wc * WN + j * 16 + (lane >> 4) * 4 + r;
-        shv[j][r] = (EPI == 1 && p.bn_ss != nullptr && n < p.Cout) ? p.bn_ss[n] : 0.f;
-      }
+      shv[j] = EPI == 1 ? *(const float4*)(shl + wc * WN + j * 16 + (lane >> 4) * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int row = wr * WM + i * 16 + (lane & 15);
@@ -637,8 +639,10 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
       for (int j = 0; j < TN; ++j) {
         f32x4 v = acc[j][i];
         if constexpr (EPI == 1) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] -= shv[j][r];
+          v[0] -= shv[j].x;
+          v[1] -= shv[j].y;
+          v[2] -= shv[j].z;
+          v[3] -= shv[j].w;
         }
         uint2 o;
         o.x = pack2bf(v[0], v[1]);
@@ -1622,6 +1626,11 @@ __global__ __launch_bounds__(64 * NKQ, 1) void stem_wgrad_kernel(StemWgradParams
 // bf16 stores of 4 channels per lane and BN partial statistics of the stored values, kept in
 // registers across items and reduced once: stats[block][2][64].
 constexpr int STF_LDW = 688;  // padded LDS row of the weight: 86 16-B chunks, conflict-free b128 groups
+// Diagnostic ablations (A/B libraries only: python csrc/build.py --define STEM_ABLATE=N; results
+// are garbage): bit 0 no output stores, bit 1 no halo loads, bit 2 no MFMAs
+#ifndef STEM_ABLATE
+#define STEM_ABLATE 0
+#endif
 
 struct StemFwdParams {
   const bf16_t* x;   // [B, T, H, W2, 8]
@@ -1693,6 +1702,7 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
     hgeo[i] = f < HALO ? (tt | (hh << 2) | (wp << 8)) : -1;
   }
   auto load = [&](int it) {
+    if constexpr ((STEM_ABLATE & 2) != 0) return;
     const int hg = it % hg_per, q = it / hg_per;
     const int to = q % p.To, b = q / p.To;
     const int t0 = 2 * to - 1, h0 = 2 * hg * HR - 3;
@@ -1747,6 +1757,9 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
       s2[nf][r] = 0.f;
       shv[nf][r] = p.shift != nullptr ? p.shift[nh * 32 + nf * 16 + lg * 4 + r] : 0.f;
     }
+  // the shift loads are conditional: left pending into the item loop, the compiler's waits merge
+  // them with the loop's paths and drained every epilogue's output stores (vmcnt(0) per fragment)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 
   int it = blockIdx.x;
   if (it < p.nitems) {
@@ -1774,7 +1787,7 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
       for (int j = 0; j < PFW; ++j) bf[j] = *(const bf16x8*)(Xb + bbase[j] + boff);
 #pragma unroll
       for (int j = 0; j < PFW; ++j)
-        if (j < npf)
+        if (j < npf && !(STEM_ABLATE & 4))
 #pragma unroll
           for (int nf = 0; nf < 2; ++nf)
             acc[nf][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nf], bf[j], acc[nf][j], 0, 0, 0);
@@ -1792,7 +1805,7 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
           uint2 o;
           o.x = pack2bf(v[0] - shv[nf][0], v[1] - shv[nf][1]);
           o.y = pack2bf(v[2] - shv[nf][2], v[3] - shv[nf][3]);
-          *(uint2*)(p.y + (m0 + pos) * 64 + nh * 32 + nf * 16 + lg * 4) = o;
+          if (!(STEM_ABLATE & 1)) *(uint2*)(p.y + (m0 + pos) * 64 + nh * 32 + nf * 16 + lg * 4) = o;
           const float q0 = __uint_as_float(o.x << 16), q1 = __uint_as_float(o.x & 0xffff0000u);
           const float q2 = __uint_as_float(o.y << 16), q3 = __uint_as_float(o.y & 0xffff0000u);
           s1[nf][0] += q0; s1[nf][1] += q1; s1[nf][2] += q2; s1[nf][3] += q3;
@@ -1953,7 +1966,7 @@ static int launch_fwd_v3(ConvParams& p, hipStream_t stream) {
   constexpr int BM = 64 * NWM;
   constexpr size_t ring = (size_t)STAGES * (BM + BN) * BK * 2;
   constexpr size_t epi = (size_t)BM * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
-  const size_t lds_v3 = ring > epi ? ring : epi;
+  const size_t lds_v3 = (ring > epi ? ring : epi) + (EPI == 1 ? 4 * BN : 0);  // + the EPI 1 shift (shl)
   static bool attr_set = false;
   if (!attr_set) {
     HIP_RET(hipFuncSetAttribute((const void*)conv_fwd_v3_kernel<BN, BK, STAGES, EPI, NWM>,

@@ -23,6 +23,8 @@
 // its dY rows / halo are fetched into that XCD's L2 once.
 #include "common.h"
 
+#include <type_traits>
+
 struct HaloWgParams {
   const bf16_t* dy;  // [B, T, H, W, ldd]
   const bf16_t* x;   // [B, T, H, W, Cin]
@@ -97,7 +99,13 @@ __global__ __launch_bounds__(512, 1) void halo_wgrad_kernel(HaloWgParams p) {
   constexpr int KBW = TAPS * (CBLK / WK);  // k-blocks per wave: j -> (tap j % TAPS, cb wk + WK * (j / TAPS))
   static_assert(NBLK % WN == 0 && CBLK % WK == 0, "wave tiling");
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // two stages and the position table as SEPARATE static arrays: a fragment read of one stage then
+  // provably does not alias the LDS-DMA filling the other, so the compiler does not drain that DMA
+  // (s_waitcnt vmcnt(0)) in front of the read -- with one dynamic buffer it did, at every box, and
+  // the next box's load never overlapped this box's MFMAs
+  __shared__ __attribute__((aligned(16))) char st0[G::STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char st1[G::STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char tabmem[G::TAB_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -124,8 +132,8 @@ __global__ __launch_bounds__(512, 1) void halo_wgrad_kernel(HaloWgParams p) {
 #pragma unroll
     for (int j = 0; j < KBW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  auto issue = [&](int box, int stage) {
-    char* sd = smem + stage * G::STAGE_BYTES;
+  auto issue = [&](int box, auto SC) {
+    char* sd = decltype(SC)::value ? st1 : st0;
     char* sx = sd + G::D_BYTES;
     uint32_t q0 = fdiv((uint32_t)box, p.fnbw);
     const int bw = box - q0 * p.nbw;
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(512, 1) void halo_wgrad_kernel(HaloWgParams p) {
   // row-relative address are zero, so a lane XORs its own chunk/half bits on top)
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   __attribute__((address_space(3))) u32x4* tab =
-      (__attribute__((address_space(3))) u32x4*)((__attribute__((address_space(3))) char*)smem + 2 * G::STAGE_BYTES);
+      (__attribute__((address_space(3))) u32x4*)((__attribute__((address_space(3))) char*)tabmem);
   if (tid < G::PMAX) {
     const int pos = tid;
     const uint32_t tq = fdiv((uint32_t)pos, p.fBHBW);
@@ -209,14 +217,18 @@ __global__ __launch_bounds__(512, 1) void halo_wgrad_kernel(HaloWgParams p) {
     lane_a[i] = (uint32_t)(lp * DROWB) +
                 ((uint32_t)((((wn * NBW + i) * 2 + (pp >> 1)) << 4) | ((pp & 1) << 3)) ^ Swz<G::DCPR>::x(lp));
   typedef __attribute__((address_space(3))) char lds_char;
-  lds_char* lds = (lds_char*)smem;
-  if (box_begin < box_end) issue(box_begin, 0);
-  for (int box = box_begin; box < box_end; ++box) {
-    const int stage = (box - box_begin) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (box_begin < box_end) issue(box_begin, S0{});
+  // boxes in pairs, stage 0 then stage 1 (compile-time stages: see st0 / st1)
+  auto body = [&](int box, auto SC) {
+    constexpr int stage = decltype(SC)::value;
+    // (the builtin, not inline asm: the compiler's wait tracking sees it, so the stage DMAs before
+    // it count as complete and only the one issued below stays pending)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     halo_barrier();  // this box's images landed (every wave waited) and the other stage is free
-    if (box + 1 < box_end) issue(box + 1, stage ^ 1);
-    lds_char* dimg = lds + stage * G::STAGE_BYTES;
+    if (box + 1 < box_end) issue(box + 1, std::integral_constant<int, stage ^ 1>{});
+    lds_char* dimg = (lds_char*)(stage ? st1 : st0);
     lds_char* ximg = dimg + G::D_BYTES;
     auto load = [&](int ks, bf16x8 (&af)[NBW], bf16x8 (&bfr)[KBW]) {
       lds_char* dks = dimg + ks * 32 * DROWB;
@@ -257,6 +269,10 @@ __global__ __launch_bounds__(512, 1) void halo_wgrad_kernel(HaloWgParams p) {
       if (ks + 2 < nks) load(ks + 2, af0, bf0);
       mma(af1, bf1);
     }
+  };
+  for (int box = box_begin; box < box_end; box += 2) {
+    body(box, S0{});
+    if (box + 1 < box_end) body(box + 1, S1{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // C[n][k]: row (n) = 4*(lane>>4) + r, col (k) = lane & 15
@@ -318,15 +334,9 @@ Box choose_box(int T, int H, int W, int KT, int KH, int KW, int hpmax) {
 template <int KT, int KH, int KW, int BN, int CC, int HWD>
 int launch_halo_wgrad_t(HaloWgParams& p, hipStream_t stream) {
   using G = HaloWgGeom<BN, CC>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)halo_wgrad_kernel<KT, KH, KW, BN, CC, HWD>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  static_assert(2 * G::STAGE_BYTES + G::TAB_BYTES <= 160 * 1024, "static LDS");
   const int nblocks = p.n_slices * p.c_chunks * p.splits;
-  hipLaunchKernelGGL((halo_wgrad_kernel<KT, KH, KW, BN, CC, HWD>), dim3(nblocks), dim3(G::NT),
-                     2 * G::STAGE_BYTES + G::TAB_BYTES, stream, p);
+  hipLaunchKernelGGL((halo_wgrad_kernel<KT, KH, KW, BN, CC, HWD>), dim3(nblocks), dim3(G::NT), 0, stream, p);
   return (int)hipGetLastError();
 }
 

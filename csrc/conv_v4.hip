@@ -85,6 +85,12 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
   bf16_t* ring = (bf16_t*)smem;  // stage s: A [BM][BK] then B [BN][BK]
   bf16_t* Es = (bf16_t*)smem;    // epilogue staging [BM][LDE] (after the ring drained)
   float* ssl = (float*)(smem + BM * LDE * 2);  // [4][BN] producer-BN constants (EPI 2)
+  // EPI 1 shift of the block's (fixed) N tile behind the whole layout (launch_v4_t): written once,
+  // read from LDS by every tile's epilogue (per-tile global loads there cost vmcnt drains)
+  constexpr int V4_RING = STAGES * STAGE_ELEMS * 2, V4_EPI = BM * LDE * 2 + (EPI == 2 ? 16 * BN : 0);
+  constexpr int V4_RED = 16 * 128 * NWM * 4;
+  constexpr int SHL_OFF = V4_RING > V4_EPI ? (V4_RING > V4_RED ? V4_RING : V4_RED) : (V4_EPI > V4_RED ? V4_EPI : V4_RED);
+  float* shl = (float*)(smem + SHL_OFF);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -121,6 +127,9 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
   float e_s[8], e_q[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) { e_s[k] = 0.f; e_q[k] = 0.f; }
+  if constexpr (EPI == 1) {  // published by the first tile's barriers
+    for (int t = tid; t < BN; t += NT) shl[t] = (p.bn_ss != nullptr && n0 + t < p.Cout) ? p.bn_ss[n0 + t] : 0.f;
+  }
 
   for (int m_tile = m_slot; m_tile < p.num_m_tiles; m_tile += p.grid_m) {
     const int m0 = m_tile * BM;
@@ -287,11 +296,11 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v4_kernel(ConvParams p)
     // EPI 1: per-channel shift (bn_ss, when set: the BN's running mean) subtracted before the bf16
     // rounding, so the stored pre-BN values keep their precision when |mean| >> std
     auto shift4 = [&](int col, float (&sh)[4]) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + col + r;
-        sh[r] = (EPI == 1 && p.bn_ss != nullptr && n < p.Cout) ? p.bn_ss[n] : 0.f;
-      }
+      const float4 v = EPI == 1 ? *(const float4*)(shl + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sh[0] = v.x;
+      sh[1] = v.y;
+      sh[2] = v.z;
+      sh[3] = v.w;
     };
     if constexpr (MF == 16) {
 #pragma unroll
@@ -403,7 +412,7 @@ static int launch_v4_t(ConvParams& p, hipStream_t stream) {
   constexpr size_t ring = (size_t)STAGES * (BM + BN) * V4_BK * 2;
   constexpr size_t epi = (size_t)BM * (BN + 8) * 2 + (EPI == 2 ? 16 * BN : 0);
   constexpr size_t red = (size_t)16 * 128 * NWM * 4;
-  constexpr size_t lds = ring > epi ? (ring > red ? ring : red) : (epi > red ? epi : red);
+  constexpr size_t lds = (ring > epi ? (ring > red ? ring : red) : (epi > red ? epi : red)) + (EPI == 1 ? 4 * BN : 0);
   static_assert(lds <= 160 * 1024, "LDS");
   static bool attr_set = false;
   if (!attr_set) {
