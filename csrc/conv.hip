@@ -663,7 +663,43 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
     constexpr int OCPR = BN / 8;
     constexpr int RPP = NT / OCPR;  // rows per pass
     const int cc = tid % OCPR;
-    if (tid < RPP * OCPR) {
+    // EPI 2: the producer rows of every row this thread stores, loaded before the first store
+    // (unconditional, clamped addresses): one exposed latency per tile instead of a vmcnt(0)
+    // drain of the preceding stores at every row (conditional loads merge into the full wait)
+    constexpr int NIT = EPI == 2 ? (BM + RPP - 1) / RPP : 1;
+    uint4 yv[NIT];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = min(tid / OCPR + it * RPP, BM - 1);
+        const int m = min(m0 + row, p.M - 1), n = min(n0 + cc * 8, p.Cout - 8);
+        yv[it] = *(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n);
+      }
+    }
+    if (tid < RPP * OCPR && EPI == 2) {
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const int row = tid / OCPR + it * RPP;
+        const int m = m0 + row, n = n0 + cc * 8;
+        if (row >= BM) break;
+        const uint4 dv = *(const uint4*)(Es + row * LDE + cc * 8);
+        const bool ok = (m < p.M) & (n < p.Cout);
+        if (ok) *(uint4*)(p.y + (long long)m * p.ldy + n) = dv;
+        if (ok) {
+          float d8[8], y8[8];
+          unpack8(dv, d8);
+          unpack8(yv[it], y8);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int cl = cc * 8 + k;
+            const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
+            e_s[k] += gm;
+            e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
+          }
+        }
+      }
+    }
+    if (tid < RPP * OCPR && EPI != 2) {
 #pragma unroll 4
       for (int row = tid / OCPR; row < BM; row += RPP) {
         const int m = m0 + row, n = n0 + cc * 8;
@@ -680,20 +716,6 @@ __global__ __launch_bounds__(128 * NWM, 1) void conv_fwd_v3_kernel(ConvParams p)
             for (int k = 0; k < 8; ++k) {
               e_s[k] += d8[k];
               e_q[k] += d8[k] * d8[k];
-            }
-          }
-        }
-        if constexpr (EPI == 2) {
-          if (ok) {
-            float d8[8], y8[8];
-            unpack8(dv, d8);
-            unpack8(*(const uint4*)(p.bn_y + (long long)m * p.bn_ld + n), y8);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-              const int cl = cc * 8 + k;
-              const float gm = (y8[k] * ssl[2 * BN + cl] + ssl[3 * BN + cl] > 0.f) ? d8[k] : 0.f;
-              e_s[k] += gm;
-              e_q[k] += gm * (y8[k] - ssl[cl]) * ssl[BN + cl];
             }
           }
         }

@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 D=gpurun_out/${1:-halostep}
 mkdir -p $D
-timeout -k 10 600 python -u -m pytest tests/test_gpu_halo.py tests/test_gpu_ops.py -x -q -m gpu -k "halo or wgrad or stem or conv_bn or shifted" --timeout 240 --timeout-method thread > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_halo.py tests/test_gpu_ops.py -x -q -m gpu -k "halo or wgrad or stem or conv_bn or shifted or producer or dgrad or fused or v4 or v3" --timeout 240 --timeout-method thread > $D/pytest.log 2>&1 || { tail -60 $D/pytest.log; exit 1; }
 tail -1 $D/pytest.log
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $D/bench.log 2>&1 || { tail -30 $D/bench.log; exit 1; }
 tail -1 $D/bench.log | cut -c1-300
