@@ -1112,8 +1112,23 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
   constexpr int STAGE_ELEMS = R * (TN_ + TK_);
   static_assert(D_INST >= 1 && X_INST >= 1, "tile too small for the DMA mapping");
 
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* ring = (bf16_t*)smem;  // stage: dY [R][TN] then X [R][TK]
+  // one static array per ring stage (stage: dY [R][TN] then X [R][TK]): a step's fragment reads
+  // then provably miss the LDS-DMA filling the other stages, so the compiler does not drain that
+  // DMA (s_waitcnt vmcnt(0)) in front of them -- with one dynamic buffer it did at every step
+  __shared__ __attribute__((aligned(16))) bf16_t rd0[R * TN_];
+  __shared__ __attribute__((aligned(16))) bf16_t rx0[R * TK_];
+  __shared__ __attribute__((aligned(16))) bf16_t rd1[R * TN_];
+  __shared__ __attribute__((aligned(16))) bf16_t rx1[R * TK_];
+  __shared__ __attribute__((aligned(16))) bf16_t rd2[STAGES > 2 ? R * TN_ : 8];
+  __shared__ __attribute__((aligned(16))) bf16_t rx2[STAGES > 2 ? R * TK_ : 8];
+  auto stage_d = [&](auto SL) -> bf16_t* {
+    constexpr int sl = decltype(SL)::value;
+    return sl == 0 ? rd0 : (sl == 1 ? rd1 : rd2);
+  };
+  auto stage_x = [&](auto SL) -> bf16_t* {
+    constexpr int sl = decltype(SL)::value;
+    return sl == 0 ? rx0 : (sl == 1 ? rx1 : rx2);
+  };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1165,9 +1180,9 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
   const int nsteps = (m_end - m_begin + R - 1) / R;
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
 
-  auto issue = [&](int st) {
-    bf16_t* sd = ring + (st % STAGES) * STAGE_ELEMS;
-    bf16_t* sx = sd + R * TN_;
+  auto issue = [&](int st, auto SL) {
+    bf16_t* sd = stage_d(SL);
+    bf16_t* sx = stage_x(SL);
     const int mb = m_begin + st * R;
 #pragma unroll
     for (int i = 0; i < D_INST; ++i) {
@@ -1199,18 +1214,22 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
     }
   };
 
-  if (nsteps > 0) {
-#pragma unroll
-    for (int st = 0; st < STAGES - 1; ++st)
-      if (st < nsteps) issue(st);
-  }
-  for (int s = 0; s < nsteps; ++s) {
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  if (nsteps > 0) issue(0, S0{});
+  if (STAGES > 2 && nsteps > 1) issue(1, S1{});
+  // steps in groups of STAGES (step s uses stage s % STAGES, a compile-time index per body)
+  auto body = [&](int s, auto SL) {
+    constexpr int sl = decltype(SL)::value;
     const int ahead = min(nsteps - 1, s + STAGES - 2) - s;
-    wait_stages<NDMA, STAGES - 2>(ahead);
+    // (the builtin, not inline asm: the compiler's wait tracking sees it)
+    if (ahead <= 0) __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    else if (ahead == 1 || STAGES < 3) __builtin_amdgcn_s_waitcnt(vmcnt_imm(NDMA));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(STAGES > 2 ? 2 * NDMA : 0));
     ring_barrier();
-    if (s + STAGES - 1 < nsteps) issue(s + STAGES - 1);
-    const bf16_t* d = ring + (s % STAGES) * STAGE_ELEMS;
-    const bf16_t* x = d + R * TN_;
+    if (s + STAGES - 1 < nsteps) issue(s + STAGES - 1, std::integral_constant<int, (sl + STAGES - 1) % STAGES>{});
+    const bf16_t* d = stage_d(SL);
+    const bf16_t* x = stage_x(SL);
 #pragma unroll
     for (int ks = 0; ks < R / 32; ++ks) {
       bf16x8 af[TI], bfr[TJ];
@@ -1224,6 +1243,11 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+  for (int s = 0; s < nsteps; s += STAGES) {
+    body(s, S0{});
+    if (s + 1 < nsteps) body(s + 1, S1{});
+    if (STAGES > 2 && s + 2 < nsteps) body(s + 2, std::integral_constant<int, 2>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float* out = p.slab + (long long)split * p.Npad * p.Kpad;
@@ -2174,15 +2198,9 @@ static int launch_wgrad(WgradParams& p, hipStream_t stream) {
 
 template <int TN_, int TK_, int STAGES>
 static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
-  const size_t lds = (size_t)STAGES * WG_R * (TN_ + TK_) * 2;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_wgrad_v3_kernel<TN_, TK_, STAGES>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
-  }
+  static_assert((size_t)STAGES * WG_R * (TN_ + TK_) * 2 <= 160 * 1024, "static LDS ring");
   const int nblocks = p.n_tiles * p.k_tiles * p.splits;
-  hipLaunchKernelGGL((conv_wgrad_v3_kernel<TN_, TK_, STAGES>), dim3(nblocks), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_v3_kernel<TN_, TK_, STAGES>), dim3(nblocks), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
 

@@ -50,6 +50,11 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// s_waitcnt immediate for vmcnt(n) alone (gfx9 encoding: vmcnt bits [3:0] and [15:14], expcnt
+// [6:4] and lgkmcnt [11:8] at their maxima), for __builtin_amdgcn_s_waitcnt: unlike an inline-asm
+// wait, the compiler's own wait tracking sees it
+constexpr unsigned vmcnt_imm(int n) { return 0x0F70u | ((unsigned)n & 15u) | (((unsigned)n >> 4) << 14); }
+
 template <int NDMA, int MAXAHEAD>
 __device__ __forceinline__ void wait_stages(int ahead) {
   static_assert(MAXAHEAD <= 2, "ring depth");
