@@ -1844,19 +1844,29 @@ __global__ __launch_bounds__(128 * NPG, 1) void stem_fwd_kernel(StemFwdParams p)
 #pragma unroll
     for (int j = 0; j < PFW; ++j) {
       const int pos = (pf0 + j) * 16 + l16;
-      if (j < npf && pos < ROWS) {
+      if (j < npf && pos < ROWS) {  // (uniform over the lane pairs lg, lg ^ 1: same position)
+        uint2 o[2];
 #pragma unroll
         for (int nf = 0; nf < 2; ++nf) {
           const f32x4 v = acc[nf][j];
-          uint2 o;
-          o.x = pack2bf(v[0] - shv[nf][0], v[1] - shv[nf][1]);
-          o.y = pack2bf(v[2] - shv[nf][2], v[3] - shv[nf][3]);
-          if (!(STEM_ABLATE & 1)) *(uint2*)(p.y + (m0 + pos) * 64 + nh * 32 + nf * 16 + lg * 4) = o;
-          const float q0 = __uint_as_float(o.x << 16), q1 = __uint_as_float(o.x & 0xffff0000u);
-          const float q2 = __uint_as_float(o.y << 16), q3 = __uint_as_float(o.y & 0xffff0000u);
+          o[nf].x = pack2bf(v[0] - shv[nf][0], v[1] - shv[nf][1]);
+          o[nf].y = pack2bf(v[2] - shv[nf][2], v[3] - shv[nf][3]);
+          const float q0 = __uint_as_float(o[nf].x << 16), q1 = __uint_as_float(o[nf].x & 0xffff0000u);
+          const float q2 = __uint_as_float(o[nf].y << 16), q3 = __uint_as_float(o[nf].y & 0xffff0000u);
           s1[nf][0] += q0; s1[nf][1] += q1; s1[nf][2] += q2; s1[nf][3] += q3;
           s2[nf][0] += q0 * q0; s2[nf][1] += q1 * q1; s2[nf][2] += q2 * q2; s2[nf][3] += q3 * q3;
         }
+        // 16-B stores: lanes lg = 2a, 2a + 1 swap halves, so lane 2a holds channels 8a .. 8a + 7 of
+        // fragment 0 and lane 2a + 1 channels 16 + 8a .. of fragment 1; a wave's stores then cover
+        // 64 contiguous bytes per position (8-B stores left 32-B pieces of the 128-B rows)
+        const bool odd = lg & 1;
+        const uint2 snd = odd ? o[0] : o[1];
+        uint2 rcv;
+        rcv.x = (uint32_t)__shfl_xor((int)snd.x, 16, 64);
+        rcv.y = (uint32_t)__shfl_xor((int)snd.y, 16, 64);
+        const uint4 st = odd ? make_uint4(rcv.x, rcv.y, o[1].x, o[1].y) : make_uint4(o[0].x, o[0].y, rcv.x, rcv.y);
+        const int ch = nh * 32 + (odd ? 16 + (lg - 1) * 4 : lg * 4);
+        if (!(STEM_ABLATE & 1)) *(uint4*)(p.y + (m0 + pos) * 64 + ch) = st;
       }
     }
     lds_barrier();  // every wave done reading this item's halo (output stores stay in flight)
