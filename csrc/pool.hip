@@ -1290,6 +1290,19 @@ static bool is_s1_333(const PoolParams& p) {
 // milnce_pool_set_quad(0) turns the quad / block gathers off (A/B runs and the equality tests)
 static bool g_pool_quad = true;
 
+// Workgroups of the BN-apply pool backward (it writes no partial rows, so the grid is free;
+// MILNCE_POOL_APPLY_GRID). 2048 blocks at 5 resident per CU leave a 60 %-full second round, but
+// 1280 / 2560 measured the same end to end (same-box A/B, tools/gpu/env_ab.sh, r4)
+static int pool_apply_grid() {
+  static int g = -1;
+  if (g < 0) {
+    const char* e = getenv("MILNCE_POOL_APPLY_GRID");
+    g = e ? atoi(e) : 2048;
+    if (g < 1) g = 2048;
+  }
+  return g;
+}
+
 static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* arg, long long n, hipStream_t s,
                              const float* bn_ss = nullptr, const float* gate = nullptr, void* yr = nullptr) {
   if (n >= (1ll << 31)) return false;
@@ -1390,9 +1403,10 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
                        (const uint8_t*)arg, (bf16_t*)dx, (uint32_t)rows);
     return true;
   }
+  const int mode = coef != nullptr ? POOL_BWD_APPLY : (gate_g != nullptr ? POOL_BWD_GATED : POOL_BWD_PLAIN);
+  if (mode == POOL_BWD_APPLY && part == nullptr) nparts = pool_apply_grid();  // grid only: no partial rows
   const uint32_t npos = (uint32_t)(n / (p.C / 8));
   const uint32_t ppb = (npos + nparts - 1) / nparts;
-  const int mode = coef != nullptr ? POOL_BWD_APPLY : (gate_g != nullptr ? POOL_BWD_GATED : POOL_BWD_PLAIN);
   const bool blk133 = p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 &&
                       p.To == p.T && p.ph <= 1 && p.pw <= 1;
   const bool blk333 = p.kt == 3 && p.kh == 3 && p.kw == 3 && p.st == 2 && p.sh == 2 && p.sw == 2 && p.pt <= 1 &&
