@@ -150,6 +150,32 @@ __device__ __forceinline__ void bx_sfor(F&& f) {
 }
 __device__ __forceinline__ void bx_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// N (1 or 4) float4 reads at byte offsets OFF + 32 k and the wait for them, as ONE asm statement:
+// the values exist only after its lgkmcnt(0), so nothing that uses them can be scheduled before
+// the wait (a compiled LDS read here would be preceded by a vmcnt(0) drain, see above; a separate
+// read and wait could have their uses hoisted between the two). Early-clobber outputs: a result
+// landing early must not overwrite the address of a later read.
+template <int OFF, int N>
+__device__ __forceinline__ void bx_ds_read_f4_sync(uint32_t a, float4 (&out)[4]) {
+  static_assert((N == 1 || N == 4) && OFF >= 0 && OFF + 96 < 65536, "reads");
+  bx_u32x4 r0, r1, r2, r3;
+  if constexpr (N == 1) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=&v"(r0) : "v"(a), "n"(OFF));
+    r1 = r2 = r3 = r0;
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:%5\n\tds_read_b128 %1, %4 offset:%6\n\t"
+        "ds_read_b128 %2, %4 offset:%7\n\tds_read_b128 %3, %4 offset:%8\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+        : "v"(a), "n"(OFF), "n"(OFF + 32), "n"(OFF + 64), "n"(OFF + 96));
+  }
+  const bx_u32x4 rr[4] = {r0, r1, r2, r3};
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    out[k] = make_float4(__uint_as_float(rr[k].x), __uint_as_float(rr[k].y), __uint_as_float(rr[k].z),
+                         __uint_as_float(rr[k].w));
+}
+
 // Exact vmcnt counts of the box kernel's weight-stage waits. At tap t of a channel block the wave
 // waits for stage t of the block; every vector-memory op it issued after that stage's DMA may still
 // be outstanding (vmcnt retires in issue order). Issue order per tap: wait, barrier, DMA of stage
@@ -780,13 +806,16 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
         // lane's 4-column group (+ gq * 8 for 32x32 fragments)
         const uint32_t sbase = bx_lds_addr(box + ((wr & 1) * WM + (lane & (MF - 1))) * LDE + wc * WN +
                                            (MF == 16 ? (lane >> 4) * 4 : (lane >> 5) * 4));
+        // EPI 1 shift of the lane's 4-column groups of fragment column j (+ gq * 8 for 32x32), read by
+        // asm: a compiled LDS read here drained the next tile's weight DMA and box loads (vmcnt(0))
+        const uint32_t shbase = bx_lds_addr(ss_lds + wc * WN + (MF == 16 ? (lane >> 4) * 4 : (lane >> 5) * 4));
         bx_sfor<TN>([&](auto J) {
+          constexpr int jj = decltype(J)::value;
+          float4 sh4[4] = {};
+          if constexpr (EPI == 1) bx_ds_read_f4_sync<jj * MF * 4, MF == 16 ? 1 : 4>(shbase, sh4);
           bx_sfor<(MF == 16 ? 1 : 4)>([&](auto Q) {
             constexpr int j = decltype(J)::value, gq = decltype(Q)::value;
-            float4 sh = {0.f, 0.f, 0.f, 0.f};
-            if constexpr (EPI == 1)  // EPI 1 shift of these 4 columns
-              sh = *(const float4*)(ss_lds + wc * WN + j * MF +
-                                    (MF == 16 ? (lane >> 4) * 4 : gq * 8 + (lane >> 5) * 4));
+            const float4 sh = sh4[gq];
             bx_sfor<TM>([&](auto I) {
               constexpr int i = decltype(I)::value;
               uint2 o;
