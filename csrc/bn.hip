@@ -17,7 +17,10 @@
 // 1024 threads: each thread sums ~nparts/128 rows with two chains in flight, then a fixed-order
 // LDS tree reduces the 128 groups (deterministic).
 constexpr int FIN_CH = 8, FIN_RG = 128;
-constexpr int BN_U = 4;  // rows in flight per thread in the streaming apply kernels
+#ifndef MILNCE_BN_U
+#define MILNCE_BN_U 4
+#endif
+constexpr int BN_U = MILNCE_BN_U;  // rows in flight per thread in the streaming apply kernels
 
 __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int nparts, int stride, int c, bool ok,
                                            double& s1, double& s2) {

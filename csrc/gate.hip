@@ -104,7 +104,10 @@ __global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float
 // ramp / tail dominated the small Mixed_4 / Mixed_5 planes). Same per-element value as that kernel
 // (fp32 relu before any bf16 rounding). Grid (splits, B); every thread owns one 8-channel chunk of
 // the concat row and walks rows of clip b with BN_U loads in flight.
-constexpr int GS_U = 4;
+#ifndef MILNCE_GS_U
+#define MILNCE_GS_U 4
+#endif
+constexpr int GS_U = MILNCE_GS_U;
 __global__ __launch_bounds__(256) void gate_gsum_kernel(SegTable t, int Ctot, int thw, int rows_per_block,
                                                         float* __restrict__ gsum) {
   __shared__ float red[256 * 8];
@@ -209,7 +212,10 @@ __global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict
 // Grid (splits, B), each thread owns one fixed 8-channel chunk of the concat row, so when the
 // branches carry producer-BN info the BN-backward partial sums of every branch's last BN layer
 // (sum dz*mask, sum dz*mask*xhat) are produced here: part[b * splits + split][2][Ctot].
-constexpr int GATE_U = 4;  // rows in flight per thread in gate_bwd_apply_kernel
+#ifndef MILNCE_GATE_U
+#define MILNCE_GATE_U 4
+#endif
+constexpr int GATE_U = MILNCE_GATE_U;  // rows in flight per thread in gate_bwd_apply_kernel
 __global__ __launch_bounds__(256) void gate_bwd_apply_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ g,
                                                              const float* __restrict__ dmean, int Ctot, int thw,
