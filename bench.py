@@ -50,6 +50,8 @@ def main():
     ap.add_argument("--seq_len", type=int, default=8, help="clips per sequence for the soft-DTW losses")
     ap.add_argument("--grad_cache_chunks", type=int, default=-1,
                     help="GradCache micro-batches per GPU (config 5: 32f, 1024 clips/GPU)")
+    ap.add_argument("--save_plan", type=str, default="",
+                    help="write this run's kernel-plan decisions as a plan table (ops/tune_sync.py)")
     opts = ap.parse_args()
 
     if opts.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -179,6 +181,11 @@ def main():
             "peak_mem_gib": round(peak, 2),
         }
         out["plan_hash"] = hashes[0] if len(set(hashes)) == 1 else hashes
+        # where the kernel plan came from: the shipped plan table (ops/plans/gfx950.json, valid for
+        # these kernel sources) or first-use timing on this box
+        out["plan"] = tune_sync.table_info()
+        if opts.save_plan:
+            out["plan"]["saved"] = tune_sync.save_table(opts.save_plan)
         if comm is not None:
             out["comm"] = comm
         if cuda:

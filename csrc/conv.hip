@@ -2126,7 +2126,7 @@ static int conv_fwd_impl(const void* x, int x_u8, const void* w, void* y, float*
   p.fCin = make_fastdiv(Cin);
   p.fKW = make_fastdiv(KW); p.fKH = make_fastdiv(KH);
   p.x_total_bytes = (long long)B * p.x_bstride * (x_u8 ? 1 : 2);
-  if (impl == 14 || impl == 15)  // conv_box.hip
+  if (impl >= 14 && impl <= 17)  // conv_box.hip
     return x_u8 ? V4_UNSUPPORTED : launch_fwd_box(p, bn, impl, pro, stream);
   if (impl >= 8) return x_u8 ? V4_UNSUPPORTED : launch_fwd_v4(p, bn, impl, stream);  // conv_v4.hip
   if (!x_u8 && (bn == 96 || bn == 160 || bn == 192)) {
@@ -2169,13 +2169,13 @@ MILNCE_API int milnce_conv_fwd(const void* x, int x_u8, const void* w, void* y, 
 // = that layer's [4][Cin] mean / invstd / scale / shift) is applied while the box-tiled kernel
 // stages its input, and written to pro_z (dense; the consumer's wgrad operand; null: not needed).
 // x_ld: x's row stride in elements (x may be a channel slice of a concatenated conv output).
-// Box-tiled variants only (impl 14 / 15); anything else returns V4_UNSUPPORTED.
+// Box-tiled variants only (impl 14-17); anything else returns V4_UNSUPPORTED.
 MILNCE_API int milnce_conv_fwd_pro(const void* x, int x_ld, const void* w, void* y, float* stats,
                                    const float* y_shift, const float* pro_ss, void* pro_z, int B, int T, int H,
                                    int W, int Cin, int Cout,
                                    int KT, int KH, int KW, int pt, int ph, int pw, int Kpad, int Npad, int ldy,
                                    int bn, int grid_m, int impl, hipStream_t stream) {
-  if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
+  if (impl < 14 || impl > 17) return V4_UNSUPPORTED;
   BoxPro pro;
   pro.ss = pro_ss;
   pro.z = pro_z;
@@ -2194,7 +2194,7 @@ MILNCE_API int milnce_conv_dgrad_bnbwd(const void* dz, const void* wd, void* dx,
                                        const float* coef, void* dy_out, int B, int T, int H, int W, int C,
                                        int Cx, int KT, int KH, int KW, int pt, int ph, int pw, int Kpad, int Npad,
                                        int bn, int grid_m, int impl, hipStream_t stream) {
-  if (impl != 14 && impl != 15) return V4_UNSUPPORTED;
+  if (impl < 14 || impl > 17) return V4_UNSUPPORTED;
   BoxPro pro;
   pro.ss = ss;
   pro.z = dy_out;

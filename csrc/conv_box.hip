@@ -37,14 +37,25 @@
 #include <type_traits>
 #include <utility>
 
-static constexpr int BX_BM = 256;        // output rows per tile: 4 waves along M x 64 rows
+// Two workgroup shapes (template NW): 8 waves, one workgroup per CU (impls 14 / 15): 256-row tiles
+// (4 waves along M x 2 along N), a 448-row box; 4 waves, TWO workgroups per CU (impls 16 / 17,
+// <= 80 KiB of LDS each): 128-row tiles (2 x 2 waves), a 288-row (1,3,3) / 192-row (3,1,1) box,
+// so one workgroup's barrier waits, box / weight-stage waits and epilogue stores run while the
+// other one issues MFMAs on the same SIMDs (one wave of each per SIMD).
+template <int NW> struct BoxShape {
+  static constexpr int BM = NW * 32;  // output rows per tile: NW / 2 waves along M x 64 rows
+};
+static constexpr int BX_BM = 256;        // 8-wave tile rows
 static constexpr int BX_BK = 64;         // channels per box / K stage
 // bf16 per box row: 16x16x32 fragments (lane rows l & 15, chunks c + (l >> 4)) are conflict-free
 // at a 10-chunk pitch, 32x32x16 fragments (rows l & 31, one chunk per half-wave) at 9 chunks
 template <int MF> struct BoxPitch { static constexpr int v = 80; };
 template <> struct BoxPitch<32> { static constexpr int v = 72; };
-static constexpr int BX_ROWS = 448;      // box capacity (rows)
-static constexpr int BX_NBX = BX_ROWS * 8 / 512;  // box chunks (16 B) per thread: 7
+static constexpr int BX_ROWS = 448;      // box capacity (rows), 8 waves
+// box capacity by workgroup shape and conv: 4 waves, (1,3,3): 128 output rows span <= 288 box rows
+// up to W = 50 (conv_2c at 200^2); (3,1,1): (T + 2) * P <= 192 rows (T = 8: P = 16)
+__host__ __device__ constexpr int box_rows(int ks, int nw) { return nw == 8 ? BX_ROWS : ks == 133 ? 288 : 192; }
+__host__ __device__ constexpr int box_lds_limit(int nw) { return nw == 8 ? 160 * 1024 : 80 * 1024; }
 
 // Diagnostic ablations (debug libraries only, tools/gpu/box_ablate.sh; results are garbage):
 // bit 0 box loads read one fixed chunk (L1-hot), bit 1 no weight DMA, bit 2 no epilogue stores /
@@ -176,6 +187,32 @@ __device__ __forceinline__ void bx_ds_read_f4_sync(uint32_t a, float4 (&out)[4])
                          __uint_as_float(rr[k].w));
 }
 
+// N (1-4) 16-B reads at byte offsets OFF + k * STRIDE and their lgkmcnt(0), as ONE asm statement
+// (same reason as above: a use of a result can only follow the wait)
+template <int OFF, int STRIDE, int N>
+__device__ __forceinline__ void bx_ds_read128_sync(uint32_t a, bx_u32x4 (&out)[N]) {
+  static_assert(N >= 1 && N <= 4 && OFF >= 0 && OFF + (N - 1) * STRIDE < 65536, "reads");
+  if constexpr (N == 1) {
+    asm volatile("ds_read_b128 %0, %1 offset:%2\n\ts_waitcnt lgkmcnt(0)" : "=&v"(out[0]) : "v"(a), "n"(OFF));
+  } else if constexpr (N == 2) {
+    asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(out[0]), "=&v"(out[1])
+                 : "v"(a), "n"(OFF), "n"(OFF + STRIDE));
+  } else if constexpr (N == 3) {
+    asm volatile(
+        "ds_read_b128 %0, %3 offset:%4\n\tds_read_b128 %1, %3 offset:%5\n\tds_read_b128 %2, %3 offset:%6\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(out[0]), "=&v"(out[1]), "=&v"(out[2])
+        : "v"(a), "n"(OFF), "n"(OFF + STRIDE), "n"(OFF + 2 * STRIDE));
+  } else {
+    asm volatile(
+        "ds_read_b128 %0, %4 offset:%5\n\tds_read_b128 %1, %4 offset:%6\n\t"
+        "ds_read_b128 %2, %4 offset:%7\n\tds_read_b128 %3, %4 offset:%8\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(out[0]), "=&v"(out[1]), "=&v"(out[2]), "=&v"(out[3])
+        : "v"(a), "n"(OFF), "n"(OFF + STRIDE), "n"(OFF + 2 * STRIDE), "n"(OFF + 3 * STRIDE));
+  }
+}
+
 // Exact vmcnt counts of the box kernel's weight-stage waits. At tap t of a channel block the wave
 // waits for stage t of the block; every vector-memory op it issued after that stage's DMA may still
 // be outstanding (vmcnt retires in issue order). Issue order per tap: wait, barrier, DMA of stage
@@ -190,8 +227,10 @@ struct BoxWaits {
 // TPF / PFI: the last block of a tile issues PFI y-prefetch DMAs (EPI 2) at tap TPF, after that
 // tap's weight DMA and box loads; a wait whose target was issued before them and that comes after
 // them counts them too.
+// NH: epilogue passes per tile (each: EPI_IT y loads (EPI 2, NPRE of them before the pass's barrier)
+// and EPI_IT stores; the first pass fires the next tile's stage after its barrier)
 __host__ __device__ constexpr BoxWaits make_box_waits(int TAPS, int STG, int NDMA, int P0, int PT, int NPT,
-                                                      int EPI_IT, int NPRE, bool EPI2, int ZC, int TPF = 0,
+                                                      int EPI_IT, int NPRE, bool EPI2, int ZC, int NH, int TPF = 0,
                                                       int PFI = 0) {
   // P(u): box loads at tap u = P0 at tap 0, PT at taps 1 .. NPT-1 (P0 = PT when spread)
   BoxWaits w{};
@@ -200,8 +239,8 @@ __host__ __device__ constexpr BoxWaits make_box_waits(int TAPS, int STG, int NDM
       for (int t = 0; t < TAPS; ++t) {
         auto P = [&](int u) { return u == 0 ? P0 : (u < NPT ? PT : 0); };
         const int g = t - (STG - 1);  // tap of this block that fired stage t (< 0: earlier)
-        const int epi_after_pre = (EPI2 ? 2 * EPI_IT - NPRE : 0) + 2 * EPI_IT;
-        const int epi_all = (EPI2 ? 2 * EPI_IT : 0) + NDMA + 2 * EPI_IT;
+        const int epi_after_pre = (EPI2 ? NH * EPI_IT - NPRE : 0) + NH * EPI_IT;
+        const int epi_all = (EPI2 ? NH * EPI_IT : 0) + NDMA + NH * EPI_IT;
         const bool pf_here = last && TPF < t;  // this block's prefetch lies before the wait
         int y = 0;
         if (c == 2 && t == STG - 1) {  // prefired in the previous tile's epilogue
@@ -236,7 +275,9 @@ __host__ __device__ constexpr BoxWaits make_box_waits(int TAPS, int STG, int NDM
 // allows. A box load issued at tap t is waited for by tap t + stages at the latest.
 // (3,1,1) blocks have 3 taps: at most 4 stages, so a stage's DMA is always issued within the
 // previous block (the wait tables above assume it)
-__host__ __device__ constexpr int box_stages(int bn, int ks) {
+__host__ __device__ constexpr int box_stages(int bn, int ks, int nw = 8) {
+  if (nw == 4)  // within 80 KiB next to the 288 / 192-row box (stage rows rounded to 32)
+    return ks == 133 ? (bn <= 64 ? 3 : 2) : (bn <= 64 ? 4 : bn <= 128 ? 3 : 2);
   return bn <= 64 ? (ks == 133 ? 8 : 4) : bn <= 128 ? 4 : 3;
 }
 __host__ __device__ constexpr int box_waits_max(const BoxWaits& w, int taps) {
@@ -247,35 +288,40 @@ __host__ __device__ constexpr int box_waits_max(const BoxWaits& w, int taps) {
   return m;
 }
 
-template <int BN, int KS, int EPI, int PRO, int MF>
-__global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g) {
-  constexpr int BM = BX_BM, BK = BX_BK, PITCH = BoxPitch<MF>::v;
-  constexpr int NT = 512, NWAVES = 8;
+template <int BN, int KS, int EPI, int PRO, int MF, int NW>
+__global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(ConvParams p, BoxGeo g) {
+  constexpr int BM = BoxShape<NW>::BM, BK = BX_BK, PITCH = BoxPitch<MF>::v;
+  constexpr int NT = NW * 64, NWAVES = NW;
+  constexpr int BXR = box_rows(KS, NW);        // box rows
+  constexpr int RPB = NT / 8;                  // box rows per staging pass (8 chunks per row)
   constexpr int WM = 64, WN = BN / 2;
   constexpr int TM = WM / MF, TN = WN / MF;
   constexpr int KSTEPS = BK / (MF == 16 ? 32 : 16);
   constexpr int TAPS = KS == 133 ? 9 : 3;
   constexpr int CPR = BK / 8, RPI = 64 / CPR;  // B ring: 8 rows (1 KiB) per DMA instruction
-  // weight stage rows: BN rounded up to the 64 rows one DMA round of 8 waves covers (N tiles of
-  // 96 / 160 load 128 / 192 rows; the extra rows are never read)
-  constexpr int BNR = (BN + 63) / 64 * 64;
+  // weight stage rows: BN rounded up to the rows one DMA round of all waves covers (8 waves: N tiles
+  // of 96 / 160 load 128 / 192 rows; the extra rows are never read)
+  constexpr int BNR = (BN + RPI * NWAVES - 1) / (RPI * NWAVES) * (RPI * NWAVES);
   constexpr int B_INST = BNR / RPI / NWAVES;   // DMA pieces per wave per stage
   constexpr int NDMA = B_INST;
-  constexpr int NBX = BX_NBX;
-  // epilogue: column-owner pass over 128-row halves staged in the box region
+  constexpr int NBX = BXR * 8 / NT;            // box chunks (16 B) per thread (7 / 9 / 6)
+  static_assert(NBX * NT == BXR * 8, "box staging");
+  // epilogue: column-owner passes over EH-row pieces staged in the box region (128 rows, or 64
+  // where a 128-row piece of a wide tile does not fit the 4-wave box)
   constexpr int LDE = BN + 8;                  // staged row (elements)
+  constexpr int EH = 128 * LDE <= BXR * 80 ? 128 : 64;
+  constexpr int NH = BM / EH;                  // epilogue passes per tile
   constexpr int OCPR = BN / 8;                 // 16-B chunks per output row
   constexpr int RPP = NT / OCPR;               // rows per pass
-  constexpr int EPI_IT = (128 + RPP - 1) / RPP;
-  constexpr int NST = 2 * EPI_IT;              // epilogue stores (16 B) per wave per tile
+  constexpr int EPI_IT = (EH + RPP - 1) / RPP;
   constexpr int EPI_G = EPI == 2 ? 2 : 4;      // staged chunks read per LDS wait
   constexpr int ZC = PRO >= 2 ? NBX : 0;       // z stores per wave per written box
-  constexpr int NBL = PRO == 3 ? 2 * NBX : NBX;  // box loads per wave (PRO 3: dz and y)
-  static_assert(128 * LDE <= BX_ROWS * 80, "epilogue half fits the box region");
-  static_assert((NT / OCPR + (EPI_IT - 1) * RPP + 1) * LDE <= BX_ROWS * 80, "epilogue reads stay in the box");
+  static_assert(EH * LDE <= BXR * 80 && EH % WM == 0 && BM % EH == 0, "epilogue piece fits the box region");
   static_assert(WN % MF == 0, "wave tile");
   constexpr int STAGE_ELEMS = BNR * BK;
-  constexpr int STG = box_stages(BN, KS);      // weight ring stages
+  constexpr int STG = box_stages(BN, KS, NW);  // weight ring stages
+  // (rows past the piece are read but not stored: they stay inside the LDS allocation)
+  static_assert((NT / OCPR + (EPI_IT - 1) * RPP + 1) * LDE <= BXR * 80 + STG * STAGE_ELEMS, "epilogue reads in LDS");
   static_assert(B_INST * RPI * NWAVES == BNR, "DMA mapping");
   // box loads of one block: spread over the first taps of a (1,3,3) block (one x / y row chunk
   // per tap, so each has the ring's depth in taps to land and the loads do not arrive as one
@@ -287,15 +333,15 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   constexpr int TPF = TAPS >= 4 ? TAPS - 4 : 0;
   constexpr int PFI = (EPI == 2 && BOX_YPF) ? ((BM * ((BN * 2 + 127) / 128) / NWAVES) + 63) / 64 : 0;
   constexpr BoxWaits kWaits = KS == 133 ? make_box_waits(TAPS, STG, NDMA, LPP, LPP, NBX, EPI_IT, NPRE, EPI == 2, ZC,
-                                                         TPF, PFI)
+                                                         NH, TPF, PFI)
                                         : make_box_waits(TAPS, STG, NDMA, NBX * LPP, 0, 1, EPI_IT, NPRE, EPI == 2, ZC,
-                                                         TPF, PFI);
+                                                         NH, TPF, PFI);
   static_assert(box_waits_max(kWaits, TAPS) <= 63, "vmcnt range");
   static_assert(PRO != 3 || BN <= 128, "PRO 3 registers");
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* box = (bf16_t*)smem;                                   // [BX_ROWS][PITCH]
-  bf16_t* ring = box + BX_ROWS * 80;                             // [STG][BNR][BK]
+  bf16_t* box = (bf16_t*)smem;                                   // [BXR][PITCH]
+  bf16_t* ring = box + BXR * 80;                                 // [STG][BNR][BK]
   float* ss_lds = (float*)(ring + STG * STAGE_ELEMS);            // EPI 2: [4][BN]; EPI 1: shift [BN]
   float* pro_lds = ss_lds + (EPI == 2 ? 4 * BN : EPI == 1 ? BN : 0);  // PRO 1/2: [2][Cin]; PRO 3: [7][Cin]
   // EPI 2: 256 B that the epilogue's y-row L2 prefetch (LDS-DMA, one dword per lane) writes and
@@ -378,7 +424,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   };
 
   // ---- tile geometry ----
-  const int xch = tid & 7, xrow0 = tid >> 3;  // box staging: chunk, first row (rows xrow0 + 64 k)
+  const int xch = tid & 7, xrow0 = tid >> 3;  // box staging: chunk, first row (rows xrow0 + RPB k)
   struct TileInfo {
     long long xbase;     // byte offset of the tile's input base (rows of xld elements)
     long long zbase;     // byte offset of the same rows in the dense pro_z / pro_y
@@ -536,11 +582,11 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       const uint4 v = xr[k];
-      bx_ds_write128(bx_lds_addr(box + (xrow0 + 64 * k) * PITCH + xch * 8), v);
+      bx_ds_write128(bx_lds_addr(box + (xrow0 + RPB * k) * PITCH + xch * 8), v);
       if constexpr (PRO >= 2) {
         bool own = n_tile == 0 && xo[k] != 0x80000000u && chv(cb);
         if constexpr (KS == 133) {
-          const int j = xrow0 + 64 * k;
+          const int j = xrow0 + RPB * k;
           own = own && j >= g.W1 + 1 && j <= bt.elast - bt.e0 + g.W1 + 1;
         }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v),
@@ -634,7 +680,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
   auto xrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + ti.xbase), (short)0, (int)ti.xnrec,
                                                0x00020000);
 #pragma unroll
-  for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + 64 * k);
+  for (int k = 0; k < NBX; ++k) xo[k] = box_off(ti, xrow0 + RPB * k);
   auto zrs = zrsrc(ti, PRO >= 2);
   if constexpr (PRO == 3) yrs_box = yrsrc(ti, true);
   box_load(xrs, 0, 0, NBX);
@@ -692,7 +738,7 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
           auto nrs = __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)p.x + tn.xbase), (short)0,
                                                        (int)(has_next ? tn.xnrec : 0u), 0x00020000);
 #pragma unroll
-          for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + 64 * k);
+          for (int k = 0; k < NBX; ++k) xo[k] = box_off(tn, xrow0 + RPB * k);
           if constexpr (PRO == 3) yrs_box = yrsrc(tn, has_next);
           xrs = nrs;
           zrs = zrsrc(tn, PRO >= 2 && has_next);
@@ -778,14 +824,14 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
     // bf16 rows, then every thread owns one 8-channel column chunk and walks rows (16-B coalesced
     // stores, statistics carried in registers across tiles as in v4) ----
 #pragma unroll
-    for (int half = 0; half < ((BOX_ABLATE & 8) ? 0 : 2); ++half) {
+    for (int half = 0; half < ((BOX_ABLATE & 8) ? 0 : NH); ++half) {
       // EPI 2: the producer's raw outputs of this thread's rows, loaded before the staging writes
       // and the barrier so their latency overlaps them (one load chain, not one per row)
       // (at most 4 rows ahead: the other half's waves still hold their accumulators here)
       uint4 ypre[EPI_IT];
       auto yload = [&](int it) {
         const int cc = tid % OCPR;
-        const int lr = half * 128 + min(tid / OCPR + it * RPP, 127);
+        const int lr = half * EH + min(tid / OCPR + it * RPP, EH - 1);
         long long grow;
         if constexpr (KS == 133) {
           grow = min(ti.m0 + lr, p.M - 1);
@@ -801,10 +847,10 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
         for (int it = 0; it < NPRE; ++it) ypre[it] = yload(it);
       }
-      if ((wr >> 1) == half) {
-        // row (wr & 1) * WM + i * MF + (lane & (MF - 1)) of the half, column wc * WN + j * MF + the
+      if ((wr * WM) / EH == half) {
+        // row (wr * WM) % EH + i * MF + (lane & (MF - 1)) of the piece, column wc * WN + j * MF + the
         // lane's 4-column group (+ gq * 8 for 32x32 fragments)
-        const uint32_t sbase = bx_lds_addr(box + ((wr & 1) * WM + (lane & (MF - 1))) * LDE + wc * WN +
+        const uint32_t sbase = bx_lds_addr(box + ((wr * WM) % EH + (lane & (MF - 1))) * LDE + wc * WN +
                                            (MF == 16 ? (lane >> 4) * 4 : (lane >> 5) * 4));
         // EPI 1 shift of the lane's 4-column groups of fragment column j (+ gq * 8 for 32x32), read by
         // asm: a compiled LDS read here drained the next tile's weight DMA and box loads (vmcnt(0))
@@ -847,15 +893,22 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 #pragma unroll
         for (int it = 0; it < EPI_IT; ++it) {
           if (it % EPI_G == 0) {
-            bx_sfor<EPI_IT>([&](auto U) {
-              constexpr int u = decltype(U)::value;
-              if (u >= it && u < it + EPI_G) dvs[u] = bx_ds_read128<u * RPP * LDE * 2>(rbase);
+            // the group's reads and their wait in one asm statement (with a separate
+            // wait, uses of the results could be scheduled between the reads and the wait)
+            bx_sfor<(EPI_IT + EPI_G - 1) / EPI_G>([&](auto G) {
+              constexpr int u0 = decltype(G)::value * EPI_G;
+              constexpr int n = EPI_IT - u0 < EPI_G ? EPI_IT - u0 : EPI_G;
+              if (u0 == it) {
+                bx_u32x4 grp[n];
+                bx_ds_read128_sync<u0 * RPP * LDE * 2, RPP * LDE * 2, n>(rbase, grp);
+#pragma unroll
+                for (int v = 0; v < n; ++v) dvs[u0 + v] = grp[v];
+              }
             });
-            bx_lgkm0();
           }
           const int row = tid / OCPR + it * RPP;  // row within the half
-          const int lr = half * 128 + row;
-          const bool act = (tid < RPP * OCPR) & (row < 128);
+          const int lr = half * EH + row;
+          const bool act = (tid < RPP * OCPR) & (row < EH);
           const bx_u32x4 dw = dvs[it];
           const uint4 dv = {dw.x, dw.y, dw.z, dw.w};
           uint32_t yo;
@@ -948,7 +1001,8 @@ __global__ __launch_bounds__(512, 1) void conv_box_kernel(ConvParams p, BoxGeo g
 }
 
 // ------------------------------------------------------------------------------------------
-static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
+static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles, int nw) {
+  const int BM = nw * 32, BXR = box_rows(p.KT * 100 + p.KH * 10 + p.KW, nw);
   const int ks = p.KT * 100 + p.KH * 10 + p.KW;
   if (p.st != 1 || p.sh != 1 || p.sw != 1) return V4_UNSUPPORTED;
   if (p.To != p.T || p.Ho != p.H || p.Wo != p.W) return V4_UNSUPPORTED;
@@ -968,19 +1022,20 @@ static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
     g.fW1 = make_fastdiv(g.W1);
     g.P = g.tpc = 1;
     g.ftpc = g.fP = make_fastdiv(1);
-    // box rows of the widest tile: extended span of 256 output rows + one pad row and column on
+    // box rows of the widest tile: extended span of BM output rows + one pad row and column on
     // each side (bounded by the worst alignment: a tile starting at a plane's last column)
-    // e(m + 255) - e(m) = 255 + (row wraps) + (W + 2) (plane wraps): a row wrap skips the shared
-    // pad column, a plane wrap also the shared pad row
-    const long long span = 255 + (255 / p.W + 1) + (255 / g.HW + 1) * (long long)(p.W + 2) + 2 * g.W1 + 3;
-    if (span > BX_ROWS) return V4_UNSUPPORTED;
-    ntiles = (p.M + BX_BM - 1) / BX_BM;
+    // e(m + BM - 1) - e(m) = BM - 1 + (row wraps) + (W + 2) (plane wraps): a row wrap skips the
+    // shared pad column, a plane wrap also the shared pad row
+    const long long span =
+        (BM - 1) + ((BM - 1) / p.W + 1) + ((BM - 1) / g.HW + 1) * (long long)(p.W + 2) + 2 * g.W1 + 3;
+    if (span > BXR) return V4_UNSUPPORTED;
+    ntiles = (p.M + BM - 1) / BM;
   } else if (ks == 311) {
     if (p.pt != 1 || p.ph != 0 || p.pw != 0) return V4_UNSUPPORTED;
-    // P positions of every frame per tile, T * P <= 256 output rows (T = 2: P = 112, the last 32
-    // rows of the tile idle) and (T + 2) * P box rows
+    // P positions of every frame per tile, T * P <= BM output rows (8 waves, T = 2: P = 112, the
+    // last 32 rows of the tile idle) and (T + 2) * P box rows
     if (p.T < 1) return V4_UNSUPPORTED;
-    g.P = std::min(BX_BM / p.T, BX_ROWS / (p.T + 2));
+    g.P = std::min(BM / p.T, BXR / (p.T + 2));
     if (g.P < 1) return V4_UNSUPPORTED;
     g.fP = make_fastdiv(g.P);
     g.tpc = (g.HW + g.P - 1) / g.P;
@@ -994,63 +1049,82 @@ static int box_geo(const ConvParams& p, BoxGeo& g, int& ntiles) {
   return 0;
 }
 
+// N tile a box variant runs for the plan's N tile bn (0: none). 4-wave 16x16x32 (impl 16) runs a
+// 192-wide plan as two 96-wide N tiles (its 192-row weight stages do not fit 80 KiB next to a box).
+static int box_bn(int bn, int impl) {
+  switch (impl) {
+    case 14: return (bn == 64 || bn == 96 || bn == 128 || bn == 160) ? bn : 0;
+    case 15: return (bn == 64 || bn == 128 || bn == 192) ? bn : 0;
+    case 16: return (bn == 64 || bn == 96 || bn == 128 || bn == 160) ? bn : bn == 192 ? 96 : 0;
+    case 17: return (bn == 64 || bn == 128 || bn == 192) ? bn : 0;
+  }
+  return 0;
+}
+static int box_nw(int impl) { return impl >= 16 ? 4 : 8; }
+
 bool fwd_box_supported(const ConvParams& p, int bn, int impl) {
   BoxGeo g;
   int nt;
-  if (!((impl == 14 && (bn == 64 || bn == 96 || bn == 128 || bn == 160)) ||
-        (impl == 15 && (bn == 64 || bn == 128 || bn == 192))))
-    return false;
-  return box_geo(p, g, nt) == 0;
+  if (box_bn(bn, impl) == 0) return false;
+  return box_geo(p, g, nt, box_nw(impl)) == 0;
 }
 
-template <int BN, int KS, int EPI, int PRO, int MF>
+template <int BN, int KS, int EPI, int PRO, int MF, int NW>
 static int launch_box_t(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
-  const size_t lds = (size_t)BX_ROWS * 80 * 2 + (size_t)box_stages(BN, KS) * ((BN + 63) / 64 * 64) * BX_BK * 2 +
-                     (EPI == 2 ? 16 * BN + 256 : EPI == 1 ? 4 * BN : 0) + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
-  if (lds > 160 * 1024) return V4_UNSUPPORTED;
-  static bool attr_set = false;
-  if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)conv_box_kernel<BN, KS, EPI, PRO, MF>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr_set = true;
+  constexpr int BNR = (BN + 8 * NW - 1) / (8 * NW) * (8 * NW);
+  constexpr size_t base = (size_t)box_rows(KS, NW) * 80 * 2 + (size_t)box_stages(BN, KS, NW) * BNR * BX_BK * 2 +
+                          (EPI == 2 ? 16 * BN + 256 : EPI == 1 ? 4 * BN : 0);
+  if constexpr (base > (size_t)box_lds_limit(NW)) {  // (no kernel instance for a shape that never fits)
+    return V4_UNSUPPORTED;
+  } else {
+    const size_t lds = base + (PRO == 3 ? 28 * (size_t)p.Cin : PRO ? 8 * (size_t)p.Cin : 0);
+    if (lds > (size_t)box_lds_limit(NW)) return V4_UNSUPPORTED;
+    static bool attr_set = false;
+    if (!attr_set) {
+      HIP_RET(hipFuncSetAttribute((const void*)conv_box_kernel<BN, KS, EPI, PRO, MF, NW>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, box_lds_limit(NW)));
+      attr_set = true;
+    }
+    const int nblocks = p.num_n_tiles * p.grid_m;
+    hipLaunchKernelGGL((conv_box_kernel<BN, KS, EPI, PRO, MF, NW>), dim3(nblocks), dim3(NW * 64), lds, stream, p, g);
+    return (int)hipGetLastError();
   }
-  const int nblocks = p.num_n_tiles * p.grid_m;
-  hipLaunchKernelGGL((conv_box_kernel<BN, KS, EPI, PRO, MF>), dim3(nblocks), dim3(512), lds, stream, p, g);
-  return (int)hipGetLastError();
 }
 
-template <int BN, int KS, int MF>
+template <int BN, int KS, int MF, int NW>
 static int launch_box_epi(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
   if (g.pro_y != nullptr) {  // BN-backward prologue (dgrad), dy written as the by-product
     if constexpr (BN <= 128) {
       if (g.pro_ss == nullptr || g.pro_coef == nullptr || g.pro_z == nullptr) return V4_UNSUPPORTED;
-      if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 3, MF>(p, g, stream);
-      if (p.bn_mode == 2) return launch_box_t<BN, KS, 2, 3, MF>(p, g, stream);
+      if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 3, MF, NW>(p, g, stream);
+      if (p.bn_mode == 2) return launch_box_t<BN, KS, 2, 3, MF, NW>(p, g, stream);
     }
     return V4_UNSUPPORTED;
   }
   if (g.pro_ss != nullptr && g.pro_z != nullptr) {
-    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 2, MF>(p, g, stream);
-    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 2, MF>(p, g, stream);
+    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 2, MF, NW>(p, g, stream);
+    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 2, MF, NW>(p, g, stream);
     return V4_UNSUPPORTED;
   }
   if (g.pro_ss != nullptr) {
-    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 1, MF>(p, g, stream);
-    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 1, MF>(p, g, stream);
+    if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 1, MF, NW>(p, g, stream);
+    if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 1, MF, NW>(p, g, stream);
     return V4_UNSUPPORTED;
   }
-  if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 0, MF>(p, g, stream);
-  if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 0, MF>(p, g, stream);
-  return launch_box_t<BN, KS, 2, 0, MF>(p, g, stream);
+  if (p.bn_mode == 0) return launch_box_t<BN, KS, 0, 0, MF, NW>(p, g, stream);
+  if (p.bn_mode == 1) return launch_box_t<BN, KS, 1, 0, MF, NW>(p, g, stream);
+  return launch_box_t<BN, KS, 2, 0, MF, NW>(p, g, stream);
 }
 
-template <int BN, int MF>
+template <int BN, int MF, int NW = 8>
 static int launch_box_bn(ConvParams& p, const BoxGeo& g, hipStream_t stream) {
-  if (g.KS == 133) return launch_box_epi<BN, 133, MF>(p, g, stream);
-  return launch_box_epi<BN, 311, MF>(p, g, stream);
+  if (g.KS == 133) return launch_box_epi<BN, 133, MF, NW>(p, g, stream);
+  return launch_box_epi<BN, 311, MF, NW>(p, g, stream);
 }
 
-// impl 14: 16x16x32 MFMA (N tiles 64 / 96 / 128 / 160), 15: 32x32x16 (N tiles 64 / 128 / 192)
+// impl 14: 16x16x32 MFMA (N tiles 64 / 96 / 128 / 160), 15: 32x32x16 (N tiles 64 / 128 / 192);
+// 16 / 17: the same on 4-wave workgroups, two per CU (16: N tiles 64 / 96 / 128 / 160, a 192-wide
+// plan as two 96 tiles; 17: 64 / 128 / 192), each within the 80 KiB LDS budget or unsupported
 static uint32_t* g_box_trace = nullptr;
 // BOX_TRACE builds: the buffer ([64 workgroups][8 waves][130] uint32) the next box launches record to
 MILNCE_API int milnce_box_set_trace(void* buf) {
@@ -1062,7 +1136,14 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
   BoxGeo g;
   g.trace = g_box_trace;
   int ntiles = 0;
-  if (box_geo(p, g, ntiles) != 0) return V4_UNSUPPORTED;
+  const int nw = box_nw(impl);
+  const int bnx = box_bn(bn, impl);
+  if (bnx == 0 || box_geo(p, g, ntiles, nw) != 0) return V4_UNSUPPORTED;
+  if (bnx != bn) {  // sub-tiles of the plan's N tile (the packed weight's Npad is a multiple of both)
+    const int npad = p.num_n_tiles * bn;
+    if (npad % bnx) return V4_UNSUPPORTED;
+    p.num_n_tiles = npad / bnx;
+  }
   g.pro_ss = pro.ss;
   g.pro_z = (bf16_t*)pro.z;
   g.pro_y = (const bf16_t*)pro.y;
@@ -1086,6 +1167,15 @@ int launch_fwd_box(ConvParams& p, int bn, int impl, const BoxPro& pro, hipStream
     if (bn == 64) return launch_box_bn<64, 32>(p, g, stream);
     if (bn == 128) return launch_box_bn<128, 32>(p, g, stream);
     if (bn == 192) return launch_box_bn<192, 32>(p, g, stream);
+  } else if (impl == 16) {
+    if (bnx == 64) return launch_box_bn<64, 16, 4>(p, g, stream);
+    if (bnx == 96) return launch_box_bn<96, 16, 4>(p, g, stream);
+    if (bnx == 128) return launch_box_bn<128, 16, 4>(p, g, stream);
+    if (bnx == 160) return launch_box_bn<160, 16, 4>(p, g, stream);
+  } else if (impl == 17) {
+    if (bnx == 64) return launch_box_bn<64, 32, 4>(p, g, stream);
+    if (bnx == 128) return launch_box_bn<128, 32, 4>(p, g, stream);
+    if (bnx == 192) return launch_box_bn<192, 32, 4>(p, g, stream);
   }
   return V4_UNSUPPORTED;
 }

@@ -191,16 +191,19 @@ def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
     ``sig`` names the problem for rank-consistent tuning (tune_sync)."""
     wgs = tuple(w for w in dict.fromkeys((_FWD_WGS_PER_CU,) + _FWD_WGS_TUNE)
                 if w == _FWD_WGS_PER_CU or max_rows is None or _grid_for(M, npad, bn, w) <= max_rows)
-    code = {(i, w): 10 * i + w for i in plan_impls if i not in _V4_WIDE_M for w in wgs}
+    code = {(i, w): 10 * i + w for i in plan_impls if i not in _V4_WIDE_M + _BOX4_IMPLS for w in wgs}
     code.update({(i, w): 10 * i + w for i in plan_impls if i in _V4_WIDE_M for w in (1, 2)})
+    # 4-wave box workgroups: two per CU is their residency (80 KiB of LDS each)
+    code.update({(i, 2): 10 * i + 2 for i in plan_impls if i in _BOX4_IMPLS})
     inv = {v: k for k, v in code.items()}
-    best = _tune(lambda c: launch(inv[c][0], _grid_for(M, npad, bn, inv[c][1])), tuple(code.values()),
+    best = _tune(lambda c: launch(inv[c][0], _grid_for(M, npad, _box_eff_bn(inv[c][0], bn), inv[c][1])),
+                 tuple(code.values()),
                  default=code.get((_DEFAULT_IMPL, _FWD_WGS_PER_CU)),
                  sig=f"{sig}|M{M}|N{npad}|bn{bn}|{sorted(code.values())}")
     if best not in inv:  # autotune off: the default variant on the default grid
         return best, _grid_for(M, npad, bn, _FWD_WGS_PER_CU)
     impl, w = inv[best]
-    return impl, _grid_for(M, npad, bn, w)
+    return impl, _grid_for(M, npad, _box_eff_bn(impl, bn), w)
 
 
 # v4 forward / dgrad (csrc/conv_v4.hip): LDS-DMA ring with scalar per-stage offsets, for convs
@@ -220,17 +223,48 @@ _V4_WIDE_M = (12, 13, 14, 15)  # 8-wave workgroups, one per CU (12 / 13 v4, 14 /
 # them out.
 _BOX = os.environ.get("MILNCE_BOX", "1") != "0"
 _BOX_ROWS = 448
+# 16 / 17: the box kernels on 4-wave workgroups, two per CU (128-row tiles, a 288-row (1,3,3) /
+# 192-row (3,1,1) box, <= 80 KiB of LDS): one workgroup's barrier / stage waits / epilogue stores
+# overlap the other's MFMAs. 16 runs a 192-wide N tile as two 96-wide ones. MILNCE_BOX4=0 leaves
+# them out.
+_BOX4 = os.environ.get("MILNCE_BOX4", "1") != "0"
+_BOX4_IMPLS = (16, 17)
+
+
+def _box_eff_bn(impl: int, bn: int) -> int:
+    """N tile a (box) variant runs for the plan's N tile (csrc/conv_box.hip box_bn)."""
+    return 96 if impl == 16 and bn == 192 else bn
+
+
+def _box4_lds(bn: int, ks: tuple, pro: int = 0, epi: int = 0, cin: int = 0) -> int:
+    """LDS bytes of a 4-wave box variant (csrc/conv_box.hip launch_box_t)."""
+    k133 = tuple(ks) == (1, 3, 3)
+    stages = (3 if bn <= 64 else 2) if k133 else (4 if bn <= 64 else 3 if bn <= 128 else 2)
+    bnr = _ceil(bn, 32) * 32
+    return ((288 if k133 else 192) * 160 + stages * bnr * 128 + (16 * bn + 256 if epi == 2 else 4 * bn if epi == 1 else 0)
+            + (28 * cin if pro == 3 else 8 * cin if pro else 0))
 # N tiles 96 / 160 and temporal tiles of T * P < 256 rows (T = 2); MILNCE_BOX_EXT=0 leaves them out
 _BOX_EXT = os.environ.get("MILNCE_BOX_EXT", "1") != "0"
 
 
 def _box_ok(bn: int, cin: int, kpad: int, impl: int, geo) -> bool:
     """Mirror of csrc/conv_box.hip fwd_box_supported; geo = (T, H, W, k, padding)."""
-    if geo is None or impl not in (14, 15):
+    if geo is None or impl not in _BOX_IMPLS:
         return False
-    if not ((impl == 14 and bn in (64, 96, 128, 160)) or (impl == 15 and bn in (64, 128, 192))):
+    if not ((impl in (14, 16) and bn in (64, 96, 128, 160)) or (impl in (15, 17) and bn in (64, 128, 192))
+            or (impl == 16 and bn == 192)):
         return False
     T, H, W, k, pad = geo
+    if impl in _BOX4_IMPLS:
+        if not _BOX4 or _box4_lds(_box_eff_bn(impl, bn), k) > 80 * 1024:
+            return False
+        if cin % 8 or kpad < (k[0] * k[1] * k[2] - 1) * cin + _ceil(cin, 64) * 64:
+            return False
+        if tuple(k) == (1, 3, 3) and tuple(pad) == (0, 1, 1):
+            return 127 + (127 // W + 1) + (127 // (H * W) + 1) * (W + 2) + 2 * (W + 1) + 3 <= 288
+        if tuple(k) == (3, 1, 1) and tuple(pad) == (1, 0, 0):
+            return min(128 // T, 192 // (T + 2)) >= 1
+        return False
     if not _BOX_EXT and (bn in (96, 160) or (tuple(k) == (3, 1, 1) and 256 % T)):
         return False
     # a partial last 64-channel block is zero-filled; its weight stage (past the tap's columns) must
@@ -266,7 +300,7 @@ def _fwd_impls(bn: int, kpad: int, cin: int = 0, taps: int = 0, geo=None) -> Tup
     if _V4 and cin:
         base = base + tuple(i for i in _V4_IMPLS if _v4_ok(bn, cin, taps, kpad, i))
     if _BOX and cin:
-        base = base + tuple(i for i in (14, 15) if _box_ok(bn, cin, kpad, i, geo))
+        base = base + tuple(i for i in _BOX_IMPLS if _box_ok(bn, cin, kpad, i, geo))
     return base
 
 
@@ -652,7 +686,7 @@ def _tune_dgrad_bnbwd(plan: ConvPlan, dz, weight, y, ss, gamma, part, nparts, ps
     pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
 
     def launch(impl, grid):
-        if impl in _BOX_IMPLS and plan.d_bn <= 128:
+        if _box_pro3_ok(impl, plan):
             conv_dgrad_bnbwd(dz, wd, plan, x_bn, y, ss, coef, dy_s, impl, grid, dx_s)
             return
         call("milnce_bn_bwd", ptr(dz), C, ptr(y), C, ptr(ss), C, plan.M, ptr(gamma), ptr(part), nparts, ps, 1,
@@ -677,9 +711,19 @@ def _tune_dgrad_bnbwd(plan: ConvPlan, dz, weight, y, ss, gamma, part, nparts, ps
 _BNBWD_FUSE = os.environ.get("MILNCE_BNBWD_FUSE", "1") != "0"
 
 
+def _box_pro3_ok(impl: int, plan: ConvPlan) -> bool:
+    """Box variant ``impl`` can run this plan's dgrad with the BN-backward prologue (PRO 3: N tiles
+    <= 128; a 4-wave one also within 80 KiB with the prologue constants and producer partials)."""
+    if impl not in _BOX_IMPLS or _box_eff_bn(impl, plan.d_bn) > 128:
+        return False
+    if impl in _BOX4_IMPLS:
+        return _box4_lds(_box_eff_bn(impl, plan.d_bn), plan.k, pro=3, epi=2, cin=plan.Cout) <= 80 * 1024
+    return True
+
+
 def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
     """The dgrad can take over this layer's BN-backward apply (``conv_dgrad_bnbwd``)."""
-    return (_BNBWD_FUSE and _PRO_FUSE and plan.d_impl in _BOX_IMPLS and plan.d_bn <= 128 and _box_geo(plan) is not None
+    return (_BNBWD_FUSE and _PRO_FUSE and _box_pro3_ok(plan.d_impl, plan) and _box_geo(plan) is not None
             and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 8 == 0)
 
 
@@ -734,7 +778,7 @@ def _is_lazy(t) -> bool:
 # (read y, write z) and the consumer's re-read of z become one read of y inside the conv. Other
 # consumer kernels materialise z first (the old cost). MILNCE_PRO_FUSE=0 disables.
 _PRO_FUSE = os.environ.get("MILNCE_PRO_FUSE", "1") != "0"
-_BOX_IMPLS = (14, 15)
+_BOX_IMPLS = (14, 15, 16, 17)
 
 
 def _pro_z(shape, device, bn_info) -> torch.Tensor:
@@ -1004,14 +1048,25 @@ def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accu
 # same-box bench A/B 4012 pairs/s inline vs 4003 deferred -- the big kernels it would overlap
 # already fill the chip, so there is no idle gap for the reduce to hide in.
 _DEFER_WGRAD = os.environ.get("MILNCE_DEFER_WGRAD", "0") == "1"
+# Side-stream weight gradients (default; MILNCE_WGRAD_SIDE=0 disables): the whole wgrad (kernel +
+# slab reduction) of every conv+BN layer runs on the side stream, so the MFMA-heavy weight
+# gradients overlap the rest of the backward chain (dgrads, BN / pool / gate backward passes) of the
+# next layers; grad_sink joins them before the gradients are read. Same-box bench A/Bs
+# (profiles/r5_wgrad_side.md): +2.8 / +3.2 % pairs/s; variants that kept the persistent dgrads off
+# the side stream's work (dgrads waiting for it: +1 %) or enqueued each wgrad ahead of its layer's
+# dgrad (+2.4 %), high-priority streams for either side (+1-2 %) and CU-masked side streams
+# (-15 %) all measured lower.
+_WGRAD_SIDE = os.environ.get("MILNCE_WGRAD_SIDE", "1") != "0"
 _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
+
 
 
 def _side_stream(device: torch.device) -> "torch.cuda.Stream":
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE_STREAMS.get(idx)
     if s is None:
-        s = _SIDE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        s = torch.cuda.Stream(device=idx)
+        _SIDE_STREAMS[idx] = s
     return s
 
 
@@ -1101,7 +1156,21 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             if impl < 100:
                 plan.w_tk = tk
             plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
-    if defer and out is not None and _DEFER_WGRAD:
+    if defer and out is not None and _WGRAD_SIDE:
+        # the whole weight gradient on the side stream, overlapping the rest of the backward
+        # pass (its operands are kept alive for that stream; grad_sink joins it)
+        main = torch.cuda.current_stream(dy.device)
+        side = _side_stream(dy.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
+        for t in (dy, x, xss):
+            if t is not None:
+                t.record_stream(side)
+        ev = torch.cuda.Event()
+        ev.record(side)
+        grad_sink.defer(ev)
+    elif defer and out is not None and _DEFER_WGRAD:
         slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, acc)
         _reduce_on_side(slab, dw, splits, npad, kpad, plan, acc)
     else:

@@ -14,17 +14,103 @@ rank whose signature differs from rank 0's raises instead of silently using a ke
 another shape. ``plan_hash()`` digests the decisions this process made (bench.py reports it per
 rank). The reference has no autotuning; cuDNN's benchmark mode (``--cudnn_benchmark``,
 ``main_distributed.py:177-178``) is per process, which is what this replaces for the HIP kernels.
+
+Plan table. Timing on first use makes the kernel plan a property of the run (two runs on two
+boxes could pick different variants for a near-tie). ``ops/plans/gfx950.json`` holds decisions
+recorded on an MI355X, keyed by the same problem signatures, and is valid only for the kernel
+sources it was recorded with (``src_sha``: a digest of ``csrc/*.hip`` / ``*.h``) and the arch.
+``decide()`` takes a valid table's entry without timing anything (every rank reads the same file,
+so no store traffic either) and times only signatures the table lacks. ``plan_source()`` says
+where this process's decisions came from; ``save_table()`` (bench.py ``--save_plan``) writes the
+decisions of a run. ``MILNCE_PLAN_TABLE``: another table file, or ``0`` to ignore the table.
 """
 from __future__ import annotations
 
 import contextlib
+import glob
 import hashlib
 import json
-from typing import Callable, Optional
+import os
+from typing import Callable, Dict, Optional
 
 _STATE = {"store": None, "rank": 0, "world": 1, "active": 0, "n": 0, "prefix": "milnce_tune"}
 _HASH = hashlib.sha1()
 _COUNT = [0]
+_ARCH = "gfx950"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_CSRC = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "csrc")
+DEFAULT_TABLE = os.path.join(_HERE, "plans", _ARCH + ".json")
+# table state: entries (None until loaded), why it is unusable, hits / timed decisions, all decisions
+_TABLE = {"entries": None, "status": "", "hits": 0, "timed": 0, "path": ""}
+_MADE: Dict[str, int] = {}
+
+
+def source_sha() -> str:
+    """Digest of the kernel sources (csrc/*.hip, csrc/*.h) the plan table is valid for."""
+    h = hashlib.sha1()
+    for f in sorted(glob.glob(os.path.join(_CSRC, "*.hip")) + glob.glob(os.path.join(_CSRC, "*.h"))):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _table_path() -> str:
+    v = os.environ.get("MILNCE_PLAN_TABLE", "")
+    return "" if v == "0" else (v or DEFAULT_TABLE)
+
+
+def _load_table() -> Dict[str, int]:
+    if _TABLE["entries"] is not None:
+        return _TABLE["entries"]
+    path = _table_path()
+    _TABLE.update(entries={}, path=path)
+    if not path:
+        _TABLE["status"] = "disabled"
+    elif not os.path.isfile(path):
+        _TABLE["status"] = "absent"
+    else:
+        with open(path) as f:
+            t = json.load(f)
+        if t.get("arch") != _ARCH:
+            _TABLE["status"] = f"arch {t.get('arch')}"
+        elif t.get("src_sha") != source_sha():
+            _TABLE["status"] = "stale (kernel sources changed since it was recorded)"
+        else:
+            _TABLE.update(entries={str(k): int(v) for k, v in t.get("entries", {}).items()}, status="valid")
+    return _TABLE["entries"]
+
+
+def plan_source() -> str:
+    """'table' (every decision from the plan table), 'tuned' (none), 'mixed', or 'none'."""
+    hits, timed = _TABLE["hits"], _TABLE["timed"]
+    if hits and not timed:
+        return "table"
+    if timed and not hits:
+        return "tuned"
+    return "mixed" if hits else "none"
+
+
+def table_info() -> dict:
+    _load_table()
+    return {"source": plan_source(), "table_hits": _TABLE["hits"], "timed": _TABLE["timed"],
+            "table": os.path.relpath(_TABLE["path"], os.path.dirname(_CSRC)) if _TABLE["path"] else "",
+            "table_status": _TABLE["status"]}
+
+
+def save_table(path: str = "") -> str:
+    """Write this process's decisions (merged over a valid table's entries) as a plan table."""
+    path = path or DEFAULT_TABLE
+    entries = dict(_load_table())
+    entries.update(_MADE)
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump({"version": 1, "arch": _ARCH, "src_sha": source_sha(), "entries": dict(sorted(entries.items()))},
+                  f, indent=0, sort_keys=False)
+        f.write("\n")
+    os.replace(tmp, path)
+    return path
 
 
 def configure(store, rank: int, world: int, prefix: str = "milnce_tune") -> None:
@@ -60,21 +146,37 @@ def synced() -> bool:
 
 
 def decide(sig: str, tune: Callable[[], int]) -> int:
-    """The variant code for problem ``sig``: ``tune()`` here, or rank 0's choice when synced."""
-    if synced():
+    """The variant code for problem ``sig``: the plan table's entry, else ``tune()`` here, or rank
+    0's choice when synced. A rank-0 ``tune()`` that raises publishes the error, so the other ranks
+    raise too instead of waiting for a decision that never comes."""
+    table = _load_table()
+    if sig in table:
+        value = table[sig]
+        _TABLE["hits"] += 1
+    elif synced():
+        _TABLE["timed"] += 1
         _STATE["n"] += 1
         key = f"{_STATE['prefix']}/{_STATE['n']}"
         store = _STATE["store"]
         if _STATE["rank"] == 0:
-            value = int(tune())
+            try:
+                value = int(tune())
+            except BaseException as e:
+                store.set(key, json.dumps([sig, None, f"{type(e).__name__}: {e}"]))
+                raise
             store.set(key, json.dumps([sig, value]))
         else:
-            sig0, value = json.loads(store.get(key).decode())
+            got = json.loads(store.get(key).decode())
+            sig0, value = got[0], got[1]
+            if value is None:
+                raise RuntimeError(f"rank {_STATE['rank']}: rank 0 failed to tune {sig0!r}: {got[2]}")
             if sig0 != sig:
                 raise RuntimeError(f"rank {_STATE['rank']}: tuning call {_STATE['n']} is for {sig!r}, rank 0 tuned "
                                    f"{sig0!r}: the ranks ran different shapes inside a synced tuning region")
     else:
+        _TABLE["timed"] += 1
         value = int(tune())
+    _MADE[sig] = value
     _HASH.update(f"{sig}={value};".encode())
     _COUNT[0] += 1
     return value

@@ -144,8 +144,9 @@ class Trainer:
         finally:
             if arena:
                 hip_ops.zero_arena_end()
-                if self.global_step == 0:
-                    hip_ops.release_tuning_buffers()  # every shape of the step is tuned by now
+                # the cold-cache flush buffer lives only through the step that tuned (a no-op when
+                # nothing was tuned; a resumed run or a new shape tunes at any global_step)
+                hip_ops.release_tuning_buffers()
         with self.timer.phase("allreduce_wait"):
             self.bucketer.finish()
         with self.timer.phase("optimizer"):
@@ -171,6 +172,7 @@ class Trainer:
         if getattr(self, "_auto_chunks", None) is not None:
             return self._auto_chunks
         chunks = 0
+        short = ""  # this rank cannot fit one clip: raised on EVERY rank after the collective
         if video_batch is not None:
             v = video_batch
             b = v.shape[0]
@@ -180,13 +182,18 @@ class Trainer:
             budget = self._memory_budget()
             if budget is not None:
                 if budget <= est / b:
-                    raise RuntimeError(f"--grad_cache_chunks -1: {budget / 2 ** 30:.2f} GiB left for the step, less than "
-                                       f"one clip's activations ({est / b / 2 ** 30:.3f} GiB); free device memory or "
-                                       f"lower --batch_size")
-                if est > budget:
+                    short = (f"{budget / 2 ** 30:.2f} GiB left for the step, less than one clip's activations "
+                             f"({est / b / 2 ** 30:.3f} GiB)")
+                    chunks = -1  # the max over ranks below is inf: every rank raises
+                elif est > budget:
                     chunks = int(min(b, -(-est // budget)))
         if self.ctx.world_size > 1:
-            chunks = int(pdist.all_reduce_max(float(chunks)))
+            # (a rank that raised before this collective would leave its peers waiting in it)
+            chunks = pdist.all_reduce_max(float("inf") if chunks < 0 else float(chunks))
+        if chunks < 0 or chunks == float("inf"):
+            why = short or "another rank has less than one clip's activations of device memory left"
+            raise RuntimeError(f"--grad_cache_chunks -1: {why}; free device memory or lower --batch_size")
+        chunks = int(chunks)
         self._auto_chunks = chunks if chunks > 1 else 0
         if self.ctx.is_main and getattr(self.args, "checkpoint_dir", ""):  # a real run's log, not bench / tests
             log(f"grad_cache_chunks -1 resolved to {self._auto_chunks} "

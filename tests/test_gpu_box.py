@@ -1,11 +1,14 @@
-"""Box-tiled forward / dgrad (csrc/conv_box.hip, impls 14 / 15) against the fp32 reference.
+"""Box-tiled forward / dgrad (csrc/conv_box.hip, impls 14 / 15 on 8-wave workgroups, 16 / 17 on
+4-wave workgroups two per CU) against the fp32 reference.
 
 The box kernels sum the taps in (channel block, tap) order instead of v3/v4's (tap, channel
 block), so they are compared with the fp32 conv (bf16-rounded operands) and with v3's BN
 statistics / producer-BN partials, not bitwise. Shapes cover the layouts' edge cases: tiles that
 cross many (clip, frame) planes (small and odd planes), the conv_2c plane (50 x 50), every
 supported T for the temporal box (P = min(256 / T, 448 / (T + 2)) positions per tile), N tiles 64 / 96 / 128 / 160 / 192, and a
-channel count over several 64-wide blocks (box reloads mid-tile).
+channel count over several 64-wide blocks (box reloads mid-tile). The 4-wave variants sum every
+output in the same order as the 8-wave ones of the same MFMA shape (16 vs 14, 17 vs 15), so their
+outputs and input gradients must be bitwise equal.
 """
 import pytest
 import torch
@@ -44,6 +47,17 @@ CASES = [
     # T = 2: P = 112 positions per frame, the tile's last 32 rows idle
     (3, 2, 7, 7, 192, 384, (3, 1, 1), (1, 0, 0)),
     (2, 2, 11, 11, 96, 160, (3, 1, 1), (1, 0, 0)),
+    # the layers of a 8 x 64^2 clip (tests/test_gpu_gradcache.py): tiny planes, T = 1 (only the
+    # centre tap of a (3,1,1) conv in range), tiles spanning many clips
+    (4, 4, 16, 16, 64, 192, (1, 3, 3), (0, 1, 1)),
+    (4, 4, 16, 16, 192, 192, (3, 1, 1), (1, 0, 0)),
+    (4, 4, 8, 8, 16, 32, (1, 3, 3), (0, 1, 1)),
+    (4, 4, 8, 8, 32, 32, (3, 1, 1), (1, 0, 0)),
+    (4, 2, 4, 4, 96, 208, (1, 3, 3), (0, 1, 1)),
+    (4, 2, 4, 4, 208, 208, (3, 1, 1), (1, 0, 0)),
+    (4, 1, 2, 2, 160, 320, (1, 3, 3), (0, 1, 1)),
+    (4, 1, 2, 2, 320, 320, (3, 1, 1), (1, 0, 0)),
+    (4, 1, 2, 2, 48, 128, (3, 1, 1), (1, 0, 0)),
 ]
 
 
@@ -64,14 +78,15 @@ def test_conv_box_matches_reference(case):
     yr = F.conv3d(xr.permute(0, 4, 1, 2, 3), w.to(torch.bfloat16).float(), None, 1, p).permute(0, 2, 3, 4, 1)
     yr.backward(dy.float())
     geo = h._box_geo(plan)
-    fw = [i for i in (14, 15) if h._box_ok(plan.bn, cin, plan.Kpad, i, geo)]
-    dg = [i for i in (14, 15) if h._box_ok(plan.d_bn, cout, plan.d_Kpad, i, geo)]
-    assert fw or dg, (plan.bn, plan.d_bn, geo)
+    fw = [i for i in h._BOX_IMPLS if h._box_ok(plan.bn, cin, plan.Kpad, i, geo)]
+    dg = [i for i in h._BOX_IMPLS if h._box_ok(plan.d_bn, cout, plan.d_Kpad, i, geo)]
+    if not (fw or dg):
+        pytest.skip(f"no box variant for N tiles {plan.bn} / {plan.d_bn} at {geo}")
 
     def run(fi, di, grid_wgs):
         plan.impl, plan.d_impl = fi, di
-        plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, grid_wgs)
-        plan.d_grid_m = h._grid_for(plan.M, plan.d_Npad, plan.d_bn, grid_wgs)
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(fi, plan.bn), grid_wgs)
+        plan.d_grid_m = h._grid_for(plan.M, plan.d_Npad, h._box_eff_bn(di, plan.d_bn), grid_wgs)
         y = h.conv_forward_raw(x, wp, plan, stats)
         st = stats[:plan.grid_m * 2 * plan.Npad].view(plan.grid_m, 2, plan.Npad).double().sum(0)
         dx = h.conv_dgrad(dy, wd, plan, (x, ss, cin))
@@ -80,12 +95,19 @@ def test_conv_box_matches_reference(case):
         return y, st, dx, pst
 
     ref = run(4, 4, 2)
+    got = {}
     try:
         for impl in sorted(set(fw) | set(dg)):
             for wgs in (1, 2):
                 fi = impl if impl in fw else 4
                 di = impl if impl in dg else 4
-                y, st, dx, pst = run(fi, di, wgs)
+                try:
+                    y, st, dx, pst = run(fi, di, wgs)
+                except h.UnsupportedVariant:
+                    # a 4-wave variant whose epilogue / prologue constants overflow its 80 KiB (the
+                    # tuner skips it the same way)
+                    assert impl in h._BOX4_IMPLS, impl
+                    break
                 assert _rel(y, yr) < 1e-2, (impl, wgs)
                 assert torch.allclose(st, ref[1], rtol=2e-3, atol=1e-1), ("stats", impl, wgs)
                 assert _rel(dx, xr.grad) < 1e-2, (impl, wgs)
@@ -93,19 +115,29 @@ def test_conv_box_matches_reference(case):
                 # deterministic outputs (the statistics go through LDS atomics: not bitwise)
                 y2, _, dx2, _ = run(fi, di, wgs)
                 assert torch.equal(y, y2) and torch.equal(dx, dx2), (impl, wgs)
+                got[impl] = (y if impl in fw else None, dx if impl in dg else None)
+        # 4-wave vs 8-wave workgroups of the same MFMA shape: the same sums in the same order
+        for i8, i4 in ((14, 16), (15, 17)):
+            if i8 in got and i4 in got:
+                for a, b, what in zip(got[i8], got[i4], ("y", "dx")):
+                    if a is not None and b is not None:
+                        assert torch.equal(a, b), (what, i8, i4)
     finally:
         plan.impl = plan.d_impl = 0
 
 
-def _box_impl(bn):
+def _box_impl(bn, nw=8):
+    if nw == 4:  # (a 192-wide tile with the prologue constants overflows impl 17's 80 KiB: 16 splits it)
+        return 17 if bn in (64, 128) else 16
     return 15 if bn in (64, 128, 192) else 14
 
 
+@pytest.mark.parametrize("nw", [8, 4])
 @pytest.mark.parametrize("shape,cin,cmid,k", [((2, 8, 50, 50), 64, 192, (3, 3, 3)),
                                              ((3, 8, 11, 13), 128, 128, (3, 3, 3)),
                                              ((3, 4, 13, 13), 112, 224, (3, 3, 3)),
                                              ((3, 4, 13, 13), 96, 160, (3, 3, 3))])
-def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
+def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k, nw):
     """A separable S3D-G unit (spatial conv -> BN -> ReLU -> temporal conv) with the spatial BN +
     ReLU applied inside the temporal conv's box kernel (hip_ops "pro" placeholders, csrc/conv_box.hip
     PRO 2: z written as the kernel's by-product) and the spatial BN's backward apply inside its
@@ -122,19 +154,32 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k):
     old, old_b = h._PRO_FUSE, h._BNBWD_FUSE
     res = {}
     try:
+        # tune every plan of both paths first, then pin the box kernels: both arms must run the
+        # same kernels from their first forward on (its BN statistics set the running mean, i.e.
+        # the pre-BN storage shift of the second forward)
+        for fuse in (False, True):
+            h._PRO_FUSE = h._BNBWD_FUSE = fuse
+            copy.deepcopy(unit)(x.clone().requires_grad_(True)).backward(g)
+        # the box-tiled kernel on the temporal conv
+        plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
+        plan.impl = _box_impl(plan.bn, nw)
+        if not h._box_ok(plan.bn, cmid, plan.Kpad, plan.impl, h._box_geo(plan)):
+            pytest.skip(f"no {nw}-wave box variant for N tile {plan.bn}")
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(plan.impl, plan.bn), 2 if nw == 4 else 1)
+        # and on the spatial conv's dgrad: its BN backward (dy) is then staged by that dgrad
+        # (conv_dgrad_bnbwd, PRO 3) when fused
+        plan1 = h.conv_plan(tuple(shape) + (cin,), (cmid, cin, 1, k[1], k[2]), (1, 1, 1), (0, 1, 1))
+        if plan1.d_bn <= 128:
+            plan1.d_impl = _box_impl(plan1.d_bn, nw)
+            if not h._box_pro3_ok(plan1.d_impl, plan1):
+                pytest.skip(f"the {nw}-wave dgrad of N tile {plan1.d_bn} has no room for the BN prologue")
+            plan1.d_grid_m = h._grid_for(plan1.M, plan1.d_Npad, h._box_eff_bn(plan1.d_impl, plan1.d_bn),
+                                         2 if nw == 4 else 1)
         for fuse in (False, True, False):
             h._PRO_FUSE = h._BNBWD_FUSE = fuse
             u = copy.deepcopy(unit)
             xi = x.clone().requires_grad_(True)
-            out = u(xi)
-            # force the box-tiled kernel on the temporal conv (the tuner picked on the first call)
-            plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
-            plan.impl = _box_impl(plan.bn)
-            # and on the spatial conv's dgrad: its BN backward (dy) is then staged by that dgrad
-            # (conv_dgrad_bnbwd, PRO 3) when fused
-            plan1 = h.conv_plan(tuple(shape) + (cin,), (cmid, cin, 1, k[1], k[2]), (1, 1, 1), (0, 1, 1))
-            if plan1.d_bn <= 128:
-                plan1.d_impl = _box_impl(plan1.d_bn)
+            u(xi)  # non-zero running means: the second forward stores shifted pre-BN outputs
             xi.grad = None
             u.zero_grad()
             out = u(xi)

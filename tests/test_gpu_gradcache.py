@@ -47,4 +47,8 @@ def test_gradcache_in_arena_matches_full_batch_on_gpu():
         assert torch.isfinite(ga).all() and torch.isfinite(gb).all()
         assert abs(float(loss_a) - float(loss_b)) < 2e-2 * max(1.0, abs(float(loss_a))), step
         rel = ((ga - gb).norm() / ga.norm()).item()
-        assert rel < 5e-2, (step, rel)
+        # two bf16 runs whose convs pick different kernel variants per micro-batch shape (different
+        # summation orders): each is ~2 % from an fp64 oracle over the whole gradient at this size
+        # with eval-mode BN at random init (tools/dbg/box4_model_err.py), so they differ by up to
+        # ~6 %; an arena / GradCache mistake is O(1)
+        assert rel < 1e-1, (step, rel)

@@ -105,7 +105,73 @@ def test_grad_cache_auto_is_collective(budgets, expect):
 def test_grad_cache_auto_raises_below_one_clip():
     world, port = 2, _port()
     with tempfile.TemporaryDirectory() as out:
-        # one process: a rank that raises here would leave its peers waiting in the collective
         mp.spawn(_worker_chunks, args=(1, port, out, (0.5,)), nprocs=1)
         res = torch.load(os.path.join(out, "r0.pt"))
     assert "less than one clip" in res["error"]
+
+
+def test_grad_cache_auto_raises_on_every_rank():
+    # only rank 1 is short of memory: both ranks raise (after the collective), neither hangs
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_chunks, args=(world, port, out, (10.0, 0.5)), nprocs=world)
+        res = [torch.load(os.path.join(out, f"r{r}.pt")) for r in range(world)]
+    assert all("less than one clip" in r.get("error", "") for r in res), res
+
+
+def _worker_tune_fail(rank, world, port, outdir):
+    _init(rank, world, port)
+    from mil_nce_howto100m_amd.ops import tune_sync
+    assert tune_sync.configure_from_process_group()
+
+    def bad():
+        raise ValueError("no kernel variant supports this shape")
+
+    err = None
+    with tune_sync.region():
+        try:
+            tune_sync.decide("fwd|unsupported", bad)
+        except Exception as e:  # rank 0: its own error; rank 1: the published one (no hang)
+            err = f"{type(e).__name__}: {e}"
+    torch.save({"err": err}, os.path.join(outdir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_rank0_tune_error_reaches_every_rank():
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_tune_fail, args=(world, port, out), nprocs=world)
+        r0, r1 = (torch.load(os.path.join(out, f"r{r}.pt")) for r in range(world))
+    assert r0["err"].startswith("ValueError")
+    assert "rank 0 failed to tune" in r1["err"] and "no kernel variant" in r1["err"]
+
+
+def test_plan_table_hit_miss_and_staleness(tmp_path, monkeypatch):
+    from mil_nce_howto100m_amd.ops import tune_sync as ts
+    path = str(tmp_path / "plan.json")
+    monkeypatch.setenv("MILNCE_PLAN_TABLE", path)
+
+    def reset():
+        ts._TABLE.update(entries=None, status="", hits=0, timed=0, path="")
+        ts._MADE.clear()
+
+    reset()
+    timed = []
+    assert ts.decide("fwd|a", lambda: timed.append("a") or 7) == 7  # no table: timed
+    assert ts.table_info()["table_status"] == "absent" and ts.plan_source() == "tuned"
+    ts.save_table(path)
+    reset()
+    assert ts.decide("fwd|a", lambda: timed.append("a2") or 9) == 7  # from the table, nothing timed
+    assert timed == ["a"] and ts.plan_source() == "table"
+    assert ts.decide("fwd|b", lambda: 3) == 3 and ts.plan_source() == "mixed"
+    # a table recorded for other kernel sources is ignored
+    import json
+    with open(path) as f:
+        t = json.load(f)
+    t["src_sha"] = "0" * 16
+    with open(path, "w") as f:
+        json.dump(t, f)
+    reset()
+    assert ts.decide("fwd|a", lambda: 11) == 11 and ts.table_info()["table_status"].startswith("stale")
+    reset()

@@ -15,9 +15,23 @@ import torch  # noqa: E402
 from mil_nce_howto100m_amd.ops import hip_ops as h  # noqa: E402
 
 
+FLUSH = None
+
+
 def timeit(fn, reps=10):
     fn()
     torch.cuda.synchronize()
+    if FLUSH is not None:  # cold caches before every launch, as inside the step (hip_ops._tune_local)
+        tot = 0.0
+        for _ in range(reps):
+            FLUSH.zero_()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            b.synchronize()
+            tot += a.elapsed_time(b)
+        return tot / reps
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(reps):
@@ -38,7 +52,11 @@ def main():
     ap.add_argument("--impls", type=int, nargs="+", default=[3, 4, 5, 7])
     ap.add_argument("--producer", type=int, default=0,
                     help="1: dgrad with the producer-BN partials epilogue (as in the training step)")
+    ap.add_argument("--cold", type=int, default=1, help="flush L2 / MALL before each timed launch")
     o = ap.parse_args()
+    global FLUSH
+    if o.cold:
+        FLUSH = torch.empty((384 << 20) // 4, device="cuda")
     k = tuple(o.k)
     pad = tuple(kk // 2 for kk in k)
     x = torch.randn(o.batch, o.t, o.hw, o.hw, o.cin, device="cuda").to(torch.bfloat16)
@@ -60,8 +78,13 @@ def main():
         plan.impl = plan.d_impl = impl
         # the 256-row variants hold one workgroup per CU: persistent grid of 1 per CU
         wide = impl in h._V4_WIDE_M
-        plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, 1) if wide else g0
-        plan.d_grid_m = h._grid_for(plan.B * plan.T * plan.H * plan.W, plan.d_Npad, plan.d_bn, 1) if wide else dg0
+        md = plan.B * plan.T * plan.H * plan.W
+        if impl in h._BOX4_IMPLS:  # 4-wave box workgroups: two per CU
+            plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(impl, plan.bn), 2)
+            plan.d_grid_m = h._grid_for(md, plan.d_Npad, h._box_eff_bn(impl, plan.d_bn), 2)
+        else:
+            plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, 1) if wide else g0
+            plan.d_grid_m = h._grid_for(md, plan.d_Npad, plan.d_bn, 1) if wide else dg0
         try:
             tf = timeit(lambda: h.conv_forward_raw(x, wp, plan, stats))
             td = timeit(lambda: h.conv_dgrad(dy, wd, plan, prod))
