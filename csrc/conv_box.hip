@@ -413,14 +413,21 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
   for (int i = 0; i < B_INST; ++i)
     ob[i] = (uint32_t)(((long long)(n0 + i * NWAVES * RPI + lrow) * p.Kpad + src_chunk * 8) * 2);
   // stage s of a tile = (cb, tap) = (s / TAPS, s % TAPS): weight columns tap * Cin + cb * 64
+  // The counted vmcnt waits (BoxWaits) assume the vector-memory ops of a tap issue in program
+  // order: the stage's DMA pieces, then the box loads, then the y prefetch. The scheduler may
+  // otherwise interleave independent loads with the DMA pieces (it put box loads between them),
+  // and a wait that leaves the "box load" outstanding then leaves a DMA piece in flight (a race
+  // that shows with cold caches on 2-stage rings): every such group is fenced by sched_barriers.
   auto fire = [&](int gslot, int s_in_tile) {
     const int cb = s_in_tile / TAPS, tap = s_in_tile - cb * TAPS;
     bf16_t* sb = ring + gslot * STAGE_ELEMS;
     const int woff = __builtin_amdgcn_readfirstlane((tap * Cin + cb * BK) * 2);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < B_INST; ++i)
       if (!(BOX_ABLATE & 2)) __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lds_ptr_t)(sb + (i * NWAVES * RPI + wave * RPI) * BK), 16, ob[i],
                                                woff, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   // ---- tile geometry ----
@@ -506,6 +513,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
   auto box_load = [&](__amdgpu_buffer_rsrc_t rs, int cb, int k0, int k1) {
     const int coff = __builtin_amdgcn_readfirstlane(cb * BK * 2);
     const bool cv = chv(cb);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {  // (constant bounds: xr stays in registers; k0 / k1 fold per tap)
       if (k < k0 || k >= k1) continue;
@@ -515,6 +523,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
         yr[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(yrs_box, cv ? zoff(xo[k]) : 0x80000000u,
                                                                                 coff, 0));
     }
+    __builtin_amdgcn_sched_barrier(0);
   };
   auto yrsrc = [&](const TileInfo& bt, bool valid) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)((const char*)g.pro_y + bt.zbase), (short)0,
@@ -579,6 +588,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
   // offsets for the others) so the vmcnt accounting stays exact
   auto box_store = [&](int cb, const TileInfo& bt, __amdgpu_buffer_rsrc_t zs) {
     if constexpr (XF_LAG < 0) box_xform(cb, 0, NBX);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < NBX; ++k) {
       const uint4 v = xr[k];
@@ -594,6 +604,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
                                                __builtin_amdgcn_readfirstlane(cb * BK * 2), 0);
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
   };
   auto zrsrc = [&](const TileInfo& bt, bool valid) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)((char*)g.pro_z + bt.zbase), (short)0,
@@ -642,6 +653,7 @@ __global__ __launch_bounds__(NW * 64, NW == 4 ? 2 : 1) void conv_box_kernel(Conv
       const long long row0 = KS == 133 ? (long long)tt.m0 : (long long)tt.b * p.T * g.HW + tt.p0;
       const auto prs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bn_y + row0 * p.bn_ld), (short)0, 0x7FFFFFF0,
                                                          0x00020000);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < PF_INST; ++k) {
         const int L = wave * LPW + min(k * 64 + lane, LPW - 1);

@@ -239,3 +239,43 @@ def test_inception_head_prologue_fusion():
             assert _rel(g1[n], g0[n]) < 1e-2, n
     finally:
         h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
+
+
+@pytest.mark.parametrize("impl", [14, 15, 16, 17])
+@pytest.mark.parametrize("case", [((4, 4, 8, 8), 176, 64, 96, 128, (1, 3, 3), (0, 1, 1)),
+                                  ((8, 8, 25, 25), 128, 0, 128, 128, (1, 3, 3), (0, 1, 1)),
+                                  ((8, 8, 25, 25), 192, 0, 192, 192, (3, 1, 1), (1, 0, 0))])
+def test_box_cold_cache_deterministic(case, impl):
+    """Every launch gives the same bytes whether its operands come from HBM or from L2 / MALL.
+
+    The counted vmcnt waits of the box kernels assume each tap's weight-stage DMA pieces issue
+    before its box loads; the scheduler interleaved them, so a wait could leave a DMA piece in
+    flight, which only shows when the weights come from HBM slowly enough (2-stage rings, cold
+    caches). A flush of L2 and the MALL before every other launch exposes that."""
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    from mil_nce_howto100m_amd.ops._lib import call, ptr, stream
+    (B, T, H, W), ld, c0, cin, cout, k, p = case
+    torch.manual_seed(3)
+    plan = h.conv_plan((B, T, H, W, cin), (cout, cin, *k), (1, 1, 1), p)
+    if not h._box_ok(plan.bn, cin, plan.Kpad, impl, h._box_geo(plan)):
+        pytest.skip("variant does not take this shape")
+    wp = h._pack(torch.randn(cout, cin, *k, device=DEV) * 0.05, plan, 0)
+    full = torch.randn(B, T, H, W, ld, device=DEV).to(torch.bfloat16)
+    ss = torch.cat([torch.randn(cin, device=DEV) * 0.1, torch.rand(cin, device=DEV) + 0.5,
+                    torch.rand(cin, device=DEV) + 0.5, torch.randn(cin, device=DEV) * 0.2])
+    flush = torch.empty((384 << 20) // 4, device=DEV)
+    grid = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(impl, plan.bn), 2 if impl in h._BOX4_IMPLS else 1)
+    outs = []
+    for rep in range(8):
+        if rep % 2 == 0:
+            flush.zero_()
+        y = torch.empty((B, T, H, W, cout), dtype=torch.bfloat16, device=DEV)
+        z = torch.empty((B, T, H, W, cin), dtype=torch.bfloat16, device=DEV)
+        try:
+            call("milnce_conv_fwd_pro", ptr(full[..., c0:]), ld, ptr(wp), ptr(y), None, None, ptr(ss), ptr(z),
+                 B, T, H, W, cin, cout, *k, *p, plan.Kpad, plan.Npad, cout, plan.bn, grid, impl, stream())
+        except h.UnsupportedVariant:
+            pytest.skip("variant declines the shape (LDS budget)")
+        outs.append((y, z))
+    for y, z in outs[1:]:
+        assert torch.equal(y, outs[0][0]) and torch.equal(z, outs[0][1])

@@ -10,7 +10,7 @@ DEV = "cuda"
 torch.manual_seed(3)
 
 
-def check(shape, ld, c0, cin, cout, k, p):
+def check(shape, ld, c0, cin, cout, k, p, zmode=0, epi=0):
     B, T, H, W = shape
     plan = h.conv_plan((B, T, H, W, cin), (cout, cin, *k), (1, 1, 1), p)
     w = torch.randn(cout, cin, *k, device=DEV) * 0.05
@@ -28,8 +28,10 @@ def check(shape, ld, c0, cin, cout, k, p):
         ys = []
         for rep in range(5):
             y = torch.full((B, T, H, W, cout), 3.0, dtype=torch.bfloat16, device=DEV)
+            z = torch.full((B, T, H, W, cin), 5.0, dtype=torch.bfloat16, device=DEV) if zmode else None
+            stats = torch.zeros(h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad, device=DEV) if epi else None
             try:
-                call("milnce_conv_fwd_pro", ptr(yp), ld, ptr(wp), ptr(y), None, None, ptr(ss), None,
+                call("milnce_conv_fwd_pro", ptr(yp), ld, ptr(wp), ptr(y), ptr(stats), None, ptr(ss), ptr(z),
                      B, T, H, W, cin, cout, *k, *p, plan.Kpad, plan.Npad, cout, plan.bn, grid, impl, stream())
             except h.UnsupportedVariant:
                 ys = None
@@ -48,11 +50,10 @@ def check(shape, ld, c0, cin, cout, k, p):
               "vs unfused", (ys[0] != yref).sum().item(), flush=True)
 
 
-check((4, 4, 8, 8), 176, 64, 96, 128, (1, 3, 3), (0, 1, 1))
-check((4, 4, 8, 8), 176, 160, 16, 32, (1, 3, 3), (0, 1, 1))
-check((4, 4, 8, 8), 128, 0, 128, 128, (3, 1, 1), (1, 0, 0))
-check((4, 4, 8, 8), 352, 128, 128, 192, (1, 3, 3), (0, 1, 1))
-check((4, 4, 8, 8), 192, 0, 192, 192, (3, 1, 1), (1, 0, 0))
-check((4, 4, 8, 8), 96, 0, 96, 96, (3, 1, 1), (1, 0, 0))
-check((4, 4, 16, 16), 64, 0, 64, 192, (1, 3, 3), (0, 1, 1))
-check((4, 4, 16, 16), 192, 0, 192, 192, (3, 1, 1), (1, 0, 0))
+for zm, ep in ((1, 0), (1, 1), (0, 1)):
+    print("== z written" if zm else "== no z", "stats" if ep else "no stats", flush=True)
+    check((4, 4, 8, 8), 176, 64, 96, 128, (1, 3, 3), (0, 1, 1), zm, ep)
+    check((4, 4, 8, 8), 128, 0, 128, 128, (3, 1, 1), (1, 0, 0), zm, ep)
+    check((4, 4, 8, 8), 352, 128, 128, 192, (1, 3, 3), (0, 1, 1), zm, ep)
+    check((4, 4, 8, 8), 96, 0, 96, 96, (3, 1, 1), (1, 0, 0), zm, ep)
+    check((4, 4, 8, 8), 192, 0, 192, 192, (3, 1, 1), (1, 0, 0), zm, ep)
