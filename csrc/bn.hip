@@ -16,7 +16,10 @@
 // latency-bound (a few MB over few channels), so a block is 8 channels x 128 row groups of
 // 1024 threads: each thread sums ~nparts/128 rows with two chains in flight, then a fixed-order
 // LDS tree reduces the 128 groups (deterministic).
-constexpr int FIN_CH = 8, FIN_RG = 128;
+#ifndef MILNCE_FIN_RG
+#define MILNCE_FIN_RG 128  // (256-thread finalize workgroups, FIN_RG 32, measured the same: r5)
+#endif
+constexpr int FIN_CH = 8, FIN_RG = MILNCE_FIN_RG;
 #ifndef MILNCE_BN_U
 #define MILNCE_BN_U 4
 #endif
@@ -57,7 +60,7 @@ __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int n
   s2 = red[1][0][cl];
 }
 
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(
+__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_kernel(
     const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
     float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */,
@@ -238,7 +241,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
 // part rows have stride 2*ps (ps = C for bn_bwd_reduce partials, Npad for conv-epilogue partials).
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps,
+__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps,
                                                                int C, double count, const float* __restrict__ gamma,
                                                                const float* __restrict__ ss,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
