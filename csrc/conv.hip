@@ -1973,7 +1973,9 @@ __global__ void pack_weight_kernel(const float* __restrict__ w, bf16_t* __restri
 struct PackDesc {
   const float* w;
   bf16_t* out;
-  int Cout, Cin, Cin_p, KT, KH, KW, Npad, Kpad, mode, blk0, pad0, pad1;
+  // ldo: row stride of out (0: Kpad). A concatenated 1x1 group weight packs as one descriptor
+  // per member weight writing its row (mode 0) or column (mode 1) slice of the shared buffer.
+  int Cout, Cin, Cin_p, KT, KH, KW, Npad, Kpad, mode, blk0, ldo, pad1;
 };
 static_assert(sizeof(PackDesc) == 64, "PackDesc layout is mirrored by a ctypes.Structure");
 constexpr int PACK_ITEMS = 8;  // elements per thread per block
@@ -2002,7 +2004,7 @@ __global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackDesc* 
       const int tap2 = k / d.Cout, co = k % d.Cout;
       if (nn < d.Cin_p && tap2 < taps) v = d.w[((long long)co * d.Cin_p + nn) * taps + (taps - 1 - tap2)];
     }
-    d.out[idx] = f2bf(v);
+    d.out[d.ldo ? (long long)nn * d.ldo + k : idx] = f2bf(v);
   }
 }
 

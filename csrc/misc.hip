@@ -105,6 +105,39 @@ __global__ __launch_bounds__(256) void synth_video_kernel(const int* __restrict_
   }
 }
 
+// Per-sample metadata of a synthetic batch (data/synthetic.py SyntheticClips.labels / .text), one
+// thread per caption word: sample id = base + b, its latent class and the K x W caption tokens
+// (class-carrying leading words, hashed random words after), plus the int32 label / id rows the
+// video kernel reads. Replaces ~40 small int64 elementwise launches per step.
+__global__ __launch_bounds__(256) void synth_meta_kernel(long long base, int B, int K, int W, int vocab, int ncls,
+                                                         int seed, int class_words, long long* __restrict__ tok,
+                                                         long long* __restrict__ labels64, int* __restrict__ labels32,
+                                                         int* __restrict__ ids32) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * K * W) return;
+  const int w = i % W, k = (i / W) % K, b = i / (W * K);
+  const long long id = base + b;
+  const uint32_t lab = mix32((uint32_t)(id * 7919 + seed)) % (uint32_t)ncls;
+  const uint32_t h = mix32((uint32_t)(id * 1000003 + k * 8191 + w * 131 + seed));
+  const uint32_t v1 = (uint32_t)(vocab - 1);
+  tok[i] = w < class_words ? 1 + (long long)((lab * (uint32_t)class_words + (uint32_t)w) % v1)
+                           : 1 + (long long)(h % v1);
+  if (k == 0 && w == 0) {
+    labels64[b] = lab;
+    labels32[b] = (int)lab;
+    ids32[b] = (int)id;
+  }
+}
+
+MILNCE_API int milnce_synth_meta(long long base, int B, int K, int W, int vocab, int ncls, int seed, int class_words,
+                                 long long* tok, long long* labels64, int* labels32, int* ids32, hipStream_t stream) {
+  const int n = B * K * W;
+  if (n <= 0 || vocab < 2 || ncls < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(synth_meta_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, base, B, K, W, vocab, ncls, seed,
+                     class_words, tok, labels64, labels32, ids32);
+  return (int)hipGetLastError();
+}
+
 MILNCE_API int milnce_synth_video(const int* labels, const int* ids, int B, int T, int S, void* out,
                                   hipStream_t stream) {
   const long long nrows = (long long)B * T * S;

@@ -15,6 +15,7 @@ reproducible shards. On GPU the video is produced by a HIP kernel (``csrc/misc.h
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -23,6 +24,7 @@ from .. import ops
 
 
 M32 = 0xFFFFFFFF
+_SYNTH_META = os.environ.get("MILNCE_SYNTH_META", "1") != "0"
 
 
 def _mix(x: torch.Tensor) -> torch.Tensor:
@@ -96,6 +98,16 @@ class SyntheticClips:
         return torch.cat([v, pad], dim=-1).contiguous()
 
     def batch(self, step: int) -> Dict[str, torch.Tensor]:
+        if self.device.type == "cuda" and _SYNTH_META and ops.use_hip(torch.empty(0, device=self.device)):
+            # labels + captions in one launch, then the video kernel (same formulas as below)
+            from ..ops import hip_ops
+            base = (step * self.world + self.rank) * self.b
+            tok, labels, lab32, ids32 = hip_ops.synth_meta(base, self.b, self.k, self.w, self.vocab, self.ncls,
+                                                           self.seed, self.class_words, self.device)
+            v = hip_ops.synth_video(lab32, ids32, self.t, self.s, self.seed)
+            if self.layout == "reference":
+                v = v[..., :3].permute(0, 4, 1, 2, 3).contiguous()
+            return {"video": v, "text": tok, "label": labels}
         ids = self.sample_ids(step)
         labels = self.labels(ids)
         return {"video": self.video(ids, labels), "text": self.text(ids, labels), "label": labels}

@@ -369,20 +369,41 @@ class _PackDesc(ctypes.Structure):
     """Mirror of csrc/conv.hip ``PackDesc`` (64 bytes)."""
     _fields_ = [("w", ctypes.c_void_p), ("out", ctypes.c_void_p)] + \
         [(f, ctypes.c_int) for f in ("Cout", "Cin", "Cin_p", "KT", "KH", "KW", "Npad", "Kpad", "mode", "blk0",
-                                     "pad0", "pad1")]
+                                     "ldo", "pad1")]
+
+
+def _pack_pieces(ws, plan: ConvPlan, mode: int, out: torch.Tensor):
+    """(weight, out address, Cout, Npad, Kpad, ldo) per descriptor packing ``ws`` into ``out``.
+    One weight: the whole buffer. A concatenated group (``ws`` stacked along Cout): member i owns
+    rows [off, off + c) of the mode-0 buffer, or columns [off, off + c) of the mode-1 buffer
+    (row stride d_Kpad); the last member also zero-fills the padding rows / columns."""
+    npad, kpad = (plan.Npad, plan.Kpad) if mode == 0 else (plan.d_Npad, plan.d_Kpad)
+    if len(ws) == 1:
+        return [(ws[0], out.data_ptr(), plan.Cout, npad, kpad, 0)]
+    pieces, off = [], 0
+    for i, w in enumerate(ws):
+        c, last = int(w.shape[0]), i == len(ws) - 1
+        if mode == 0:
+            pieces.append((w, out.data_ptr() + off * kpad * 2, c, npad - off if last else c, kpad, 0))
+        else:
+            pieces.append((w, out.data_ptr() + off * 2, c, npad, kpad - off if last else c, kpad))
+        off += c
+    return pieces
 
 
 class _WeightPacker:
     """Packs every conv weight of a training step in ONE kernel launch at step start (the weights
     are fixed between the previous optimizer step and this one), instead of one small pack launch
-    per conv and direction. Entries register themselves the first time ``_pack`` sees a parameter
-    weight inside a step (that step packs per call); from the next step on ``_pack`` returns the
-    pre-packed persistent buffer. Outside a step, or for weights that are not parameters (the
-    concatenated 1x1 group weights), packing stays per call."""
+    per conv and direction. Entries register themselves the first time ``_pack`` / ``_pack_group``
+    sees parameter weights inside a step (that step packs per call); from the next step on they
+    return the pre-packed persistent buffer. The concatenated 1x1 group weights pack straight from
+    their member parameters (no per-step torch.cat). Outside a step, or for weights that are not
+    parameters, packing stays per call."""
 
     def __init__(self):
-        self.entries: Dict[Tuple[int, int, int], list] = {}  # (w ptr, mode, plan) -> [weight, plan, mode, out]
+        self.entries: Dict[tuple, list] = {}  # (w ptrs, mode, plan) -> [weights, plan, mode, out]
         self.descs: Optional[torch.Tensor] = None
+        self.ndescs = 0
         self.total_blocks = 0
         self.active = False
         self.packed = False
@@ -393,37 +414,43 @@ class _WeightPacker:
         if not self.entries:
             return
         if self.descs is None:
-            arr = (_PackDesc * len(self.entries))()
+            pieces = [(pc, plan, mode) for ws, plan, mode, out in self.entries.values()
+                      for pc in _pack_pieces(ws, plan, mode, out)]
+            arr = (_PackDesc * len(pieces))()
             blk = 0
-            for i, (w, plan, mode, out) in enumerate(self.entries.values()):
+            for i, ((w, optr, cout, npad, kpad, ldo), plan, mode) in enumerate(pieces):
                 kt, kh, kw = plan.k
-                npad, kpad = (plan.Npad, plan.Kpad) if mode == 0 else (plan.d_Npad, plan.d_Kpad)
-                arr[i] = _PackDesc(w.data_ptr(), out.data_ptr(), plan.Cout, plan.Cin, plan.Cin_p, kt, kh, kw,
-                                   npad, kpad, mode, blk, 0, 0)
+                arr[i] = _PackDesc(w.data_ptr(), optr, cout, plan.Cin, plan.Cin_p, kt, kh, kw,
+                                   npad, kpad, mode, blk, ldo, 0)
                 blk += _ceil(npad * kpad, 256 * 8)
             host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
             self.descs = host.to(device)
+            self.ndescs = len(pieces)
             self.total_blocks = blk
-        call("milnce_pack_weights_multi", ptr(self.descs), len(self.entries), self.total_blocks, stream())
+        call("milnce_pack_weights_multi", ptr(self.descs), self.ndescs, self.total_blocks, stream())
         self.packed = True
 
     def end(self) -> None:
         self.active = False
         self.packed = False
 
-    def lookup(self, weight: torch.Tensor, plan: ConvPlan, mode: int) -> Optional[torch.Tensor]:
+    @staticmethod
+    def _key(ws, plan: ConvPlan, mode: int) -> tuple:
+        return (tuple(w.data_ptr() for w in ws), mode, id(plan))
+
+    def lookup(self, ws, plan: ConvPlan, mode: int) -> Optional[torch.Tensor]:
         if not self.active:
             return None
-        e = self.entries.get((weight.data_ptr(), mode, id(plan)))
+        e = self.entries.get(self._key(ws, plan, mode))
         return e[3] if e is not None and self.packed else None
 
-    def register(self, weight: torch.Tensor, plan: ConvPlan, mode: int, out: torch.Tensor) -> None:
+    def register(self, ws, plan: ConvPlan, mode: int, out: torch.Tensor) -> None:
         # parameters only (leaf, requires grad): their storage is fixed for the whole step; the
         # entry keeps a reference, so the address cannot be recycled for another tensor
-        if self.active and weight.is_leaf and weight.requires_grad and weight.is_contiguous():
-            key = (weight.data_ptr(), mode, id(plan))
+        if self.active and all(w.is_leaf and w.requires_grad and w.is_contiguous() for w in ws):
+            key = self._key(ws, plan, mode)
             if key not in self.entries:
-                self.entries[key] = [weight, plan, mode, out]
+                self.entries[key] = [tuple(ws), plan, mode, out]
                 self.descs = None  # rebuilt at the next step start
 
 
@@ -431,11 +458,27 @@ _PACKER = _WeightPacker()
 
 
 def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
-    pre = _PACKER.lookup(weight, plan, mode)
+    pre = _PACKER.lookup((weight,), plan, mode)
     if pre is not None:
         return pre
     out = _pack_now(weight, plan, mode)
-    _PACKER.register(weight, plan, mode, out)
+    _PACKER.register((weight,), plan, mode, out)
+    return out
+
+
+_GROUP_PREPACK = os.environ.get("MILNCE_GROUP_PREPACK", "1") != "0"
+_GROUP_WGRAD_DIRECT = os.environ.get("MILNCE_GROUP_WGRAD_DIRECT", "1") != "0"
+
+
+def _pack_group(ws, plan: ConvPlan, mode: int) -> torch.Tensor:
+    """Packed buffer of the weights ``ws`` concatenated along Cout (the fused 1x1 group GEMM)."""
+    if not _GROUP_PREPACK:
+        return _pack_now(torch.cat([w.detach() for w in ws], 0), plan, mode)
+    pre = _PACKER.lookup(ws, plan, mode)
+    if pre is not None:
+        return pre
+    out = _pack_now(torch.cat([w.detach() for w in ws], 0), plan, mode)
+    _PACKER.register(ws, plan, mode, out)
     return out
 
 
@@ -1084,16 +1127,20 @@ def _reduce_on_side(slab: torch.Tensor, dw: torch.Tensor, splits: int, npad: int
 
 
 def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[torch.Tensor] = None,
-               defer: bool = False) -> torch.Tensor:
+               defer: bool = False, outs=None) -> Optional[torch.Tensor]:
     """dW of the conv; with ``out`` the result is accumulated into it (a parameter's grad).
     The first call of a plan tunes over (N tile, kernel variant) pairs on the real operands.
-    ``defer`` (with ``out``): the final split-K reduction into ``out`` runs on a side stream and
-    is only complete after grad_sink.drain() (see _reduce_on_side)."""
+    ``defer`` (with ``out``): the whole wgrad runs on the side stream and is only complete after
+    grad_sink.drain(). ``outs`` = [(row offset, rows, grad)]: the Cout rows are split over several
+    parameters (a concatenated 1x1 group); each slice of the split-K reduction is accumulated
+    into its own gradient and nothing is returned."""
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
-    acc = int(out is not None)
-    dw = out if out is not None else torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
+    acc = int(out is not None or outs is not None)
+    dw = out
+    if dw is None and (outs is None or plan.w_impl == 0):  # (split outputs: only the tuner's scratch shape)
+        dw = torch.empty((plan.Cout, plan.Cin_p, kt, kh, kw), dtype=F32, device=dy.device)
     ldd = plan.Cout
     xss = None
     if _is_pro(x):  # x stands for relu(y * scale + shift) of its producer BN (_TW_PRO)
@@ -1156,20 +1203,37 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             if impl < 100:
                 plan.w_tk = tk
             plan.w_Npad, plan.w_Kpad, plan.w_splits = _wgrad_geom(plan.Cout, plan.Ktot, plan.M, tn, plan.w_tk, occ)
-    if defer and out is not None and _WGRAD_SIDE:
+    if outs is not None:
+        if plan.w_impl >= 100:
+            raise RuntimeError(f"split wgrad outputs need a split-K slab kernel, got impl {plan.w_impl}")
+
+        def launch_split():
+            slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
+            for off, rows, g in outs:
+                call("milnce_wgrad_reduce", ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows,
+                     plan.Cin, plan.Cin_p, kt * kh * kw, 1, stream())
+        if not (defer and _WGRAD_SIDE):
+            launch_split()
+            return None
+    if defer and (out is not None or outs is not None) and _WGRAD_SIDE:
         # the whole weight gradient on the side stream, overlapping the rest of the backward
         # pass (its operands are kept alive for that stream; grad_sink joins it)
         main = torch.cuda.current_stream(dy.device)
         side = _side_stream(dy.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
+            if outs is not None:
+                launch_split()
+            else:
+                launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
         for t in (dy, x, xss):
             if t is not None:
                 t.record_stream(side)
         ev = torch.cuda.Event()
         ev.record(side)
         grad_sink.defer(ev)
+        if outs is not None:
+            return None
     elif defer and out is not None and _DEFER_WGRAD:
         slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, acc)
         _reduce_on_side(slab, dw, splits, npad, kpad, plan, acc)
@@ -1575,10 +1639,9 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
     bns = [args[n + 5 * i: n + 5 * i + 5] for i in range(n)]  # gamma, beta, rmean, rvar, nbt
     widths = [int(w.shape[0]) for w in ws]
     ctot = sum(widths)
-    wcat = torch.cat([w.detach() for w in ws], 0)
-    plan = conv_plan(x.shape, wcat.shape, (1, 1, 1), (0, 0, 0))
+    plan = conv_plan(x.shape, (ctot,) + tuple(ws[0].shape[1:]), (1, 1, 1), (0, 0, 0))
     dev = x.device
-    wp = _pack(wcat, plan, 0)
+    wp = _pack_group(ws, plan, 0)
     stats = (torch.empty((_stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), dtype=F32, device=dev)
              if training else None)
     shift = _bn_shift([b[2] for b in bns], training)
@@ -1613,7 +1676,8 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
         if g is not None:
             gsum = g
         off += c
-    ctx.save_for_backward(x, wcat, y, *sss, *[b[0] for b in bns], *extra_saved)
+    ctx.save_for_backward(x, y, *sss, *[b[0] for b in bns], *extra_saved)
+    ctx.ws = ws  # the member parameters (packed for the dgrad, direct wgrad targets)
     ctx.betas = [b[1] for b in bns]
     ctx.training = bool(training)
     ctx.plan, ctx.widths, ctx.n = plan, widths, n
@@ -1628,9 +1692,9 @@ def _group_backward(ctx, grads, saved=None):
     """Backward of the fused 1x1 group: returns (dX of the GEMM, the remaining grads tuple)."""
     n, widths, plan = ctx.n, ctx.widths, ctx.plan
     saved = ctx.saved_tensors if saved is None else saved
-    x, wcat, y = saved[:3]
-    sss = saved[3:3 + n]
-    gammas = saved[3 + n:3 + 2 * n]
+    x, y = saved[:2]
+    sss = saved[2:2 + n]
+    gammas = saved[2 + n:2 + 2 * n]
     ctot = sum(widths)
     dev = y.device
     dY = torch.empty((plan.M, ctot), dtype=BF16, device=dev)
@@ -1675,12 +1739,22 @@ def _group_backward(ctx, grads, saved=None):
     dYv = dY.view(plan.B, plan.To, plan.Ho, plan.Wo, ctot)
     dx = None
     if ctx.needs_input_grad[0]:
-        dx = conv_dgrad(dYv, _pack(wcat, plan, 1), plan, ctx.x_bn)
-    dwcat = conv_wgrad(dYv, x, plan)
-    dws, off = [], 0
-    for c in widths:
-        dws.append(dwcat[off:off + c])
-        off += c
+        dx = conv_dgrad(dYv, _pack_group(ctx.ws, plan, 1), plan, ctx.x_bn)
+    directs = [_direct_grad(w) for w in ctx.ws]
+    if _GROUP_WGRAD_DIRECT and all(d is not None for d in directs):
+        # each member's slice of the split-K reduction lands in its flat-buffer gradient (on the
+        # side stream, with the wgrad): no dW concat tensor, no AccumulateGrad adds
+        offs = [sum(widths[:i]) for i in range(n)]
+        conv_wgrad(dYv, x, plan, defer=True, outs=list(zip(offs, widths, directs)))
+        for w in ctx.ws:
+            _grad_done(w)
+        dws = [None] * n
+    else:
+        dwcat = conv_wgrad(dYv, x, plan)
+        dws, off = [], 0
+        for c in widths:
+            dws.append(dwcat[off:off + c])
+            off += c
     bn_grads = []
     for dg, db in zip(dgs, dbs):
         bn_grads += [dg, db, None, None, None]
@@ -2272,6 +2346,18 @@ def milnce_loss(video_embd, text_embd, fused: Optional[bool] = None):
 def adam_step(p, g, m, v, lr, b1, b2, eps, wd, bc1, bc2, grad_scale):
     call("milnce_adam", ptr(p), ptr(g), ptr(m), ptr(v), p.numel(), float(lr), float(b1), float(b2), float(eps),
          float(wd), float(bc1), float(bc2), float(grad_scale), stream())
+
+
+def synth_meta(base: int, B: int, K: int, W: int, vocab: int, ncls: int, seed: int, class_words: int,
+               device: torch.device):
+    """(tokens int64 [B, K, W], labels int64 [B], labels int32 [B], ids int32 [B]) of the synthetic
+    samples base .. base + B - 1 in one launch (data/synthetic.py holds the torch formula)."""
+    tok = torch.empty((B, K, W), dtype=torch.int64, device=device)
+    lab = torch.empty((B,), dtype=torch.int64, device=device)
+    small = torch.empty((2, B), dtype=torch.int32, device=device)
+    call("milnce_synth_meta", base, B, K, W, vocab, ncls, seed, class_words, ptr(tok), ptr(lab), ptr(small[0]),
+         ptr(small[1]), stream())
+    return tok, lab, small[0], small[1]
 
 
 def synth_video(labels_i32, ids_i32, T, S, seed):

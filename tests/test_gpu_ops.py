@@ -593,6 +593,22 @@ def test_synth_video_matches_torch():
     assert (a.int() - b.int()).abs().max().item() <= 1
 
 
+@pytest.mark.parametrize("step,world,rank", [(0, 1, 0), (7, 1, 0), (1_000_003, 8, 5)])
+def test_synth_batch_one_launch_matches_torch(step, world, rank):
+    """batch() on the GPU (labels + captions in one synth_meta launch) == the int64 torch formulas,
+    also for sample ids whose hash inputs wrap 32 bits."""
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    s = SyntheticClips(5, 4, 32, num_candidates=3, max_words=11, vocab_size=997, num_classes=13, seed=9,
+                       device=torch.device(DEV), rank=rank, world_size=world)
+    got = s.batch(step)
+    ids = s.sample_ids(step)
+    lab = s.labels(ids)
+    assert torch.equal(got["label"], lab)
+    assert torch.equal(got["text"], s.text(ids, lab))
+    assert got["text"].dtype == torch.int64 and got["label"].dtype == torch.int64
+    assert (got["video"].int() - s._video_torch(ids, lab).int()).abs().max().item() <= 1
+
+
 def test_stem_prep_reference_layout():
     h = hip()
     v = torch.randint(0, 256, (2, 3, 4, 6, 6), dtype=torch.uint8, device=DEV)
@@ -1247,6 +1263,40 @@ def test_step_weight_prepack_matches_per_call_pack():
                 torch.cuda.synchronize()
                 want = h._pack_now(w, p, m)
                 assert torch.equal(got.view(torch.int16), want.view(torch.int16))
+    finally:
+        h.zero_arena_end()
+        h._PACKER.entries.clear()
+        h._PACKER.descs = None
+
+
+@pytest.mark.parametrize("widths,cin", [((64, 96, 16), 192), ((128, 128, 32), 256), ((112, 144, 32), 512),
+                                        ((24, 40, 8), 24)])
+def test_step_group_prepack_matches_concat_pack(widths, cin):
+    """The concatenated 1x1 group weights pre-packed from their member parameters (one
+    descriptor per member, row / column slices of the shared buffer incl. the zero padding) are
+    bitwise identical to packing torch.cat of the members."""
+    h = hip()
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    ws = [nn.Parameter(torch.randn((c, cin, 1, 1, 1), device=dev)) for c in widths]
+    plan = h.conv_plan((2, 4, 6, 6, cin), (sum(widths), cin, 1, 1, 1), (1, 1, 1), (0, 0, 0))
+    h._PACKER.entries.clear()
+    h._PACKER.descs = None
+    h.zero_arena_begin(dev)
+    first = [h._pack_group(ws, plan, m) for m in (0, 1)]
+    h.zero_arena_end()
+    assert len(h._PACKER.entries) == 2
+    with torch.no_grad():
+        for w in ws:
+            w.mul_(-0.5)
+    h.zero_arena_begin(dev)
+    try:
+        for m in (0, 1):
+            got = h._pack_group(ws, plan, m)
+            assert got.data_ptr() == first[m].data_ptr()
+            torch.cuda.synchronize()
+            want = h._pack_now(torch.cat([w.detach() for w in ws], 0), plan, m)
+            assert torch.equal(got.view(torch.int16), want.view(torch.int16))
     finally:
         h.zero_arena_end()
         h._PACKER.entries.clear()
