@@ -60,13 +60,12 @@ __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int n
   s2 = red[1][0][cl];
 }
 
-__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_kernel(
-    const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
+__device__ __forceinline__ void bn_finalize_body(
+    int blk, const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
     const float* __restrict__ beta, float* rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
-    float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */,
-    float* yshift) {
-  const int c = blockIdx.x * FIN_CH + threadIdx.x % FIN_CH;
-  if (training && blockIdx.x == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
+    float momentum, float eps, int training, float* __restrict__ out, float* yshift) {
+  const int c = blk * FIN_CH + threadIdx.x % FIN_CH;
+  if (training && blk == 0 && threadIdx.x == 0 && nbt != nullptr) nbt[0] += 1;
   double s, q;
   fin_reduce(part, training ? nparts : 0, Npad, c, training && c < C, s, q);
   if (threadIdx.x >= FIN_CH || c >= C) return;
@@ -97,6 +96,46 @@ __global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_kernel(
   out[C + c] = invstd;
   out[2 * C + c] = sc;
   out[3 * C + c] = beta[c] - mean * sc;
+}
+
+__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_kernel(
+    const float* __restrict__ part, int nparts, int Npad, int C, double count, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* rmean, float* __restrict__ rvar, long long* __restrict__ nbt,
+    float momentum, float eps, int training, float* __restrict__ out /* [4][C]: mean, invstd, scale, shift */,
+    float* yshift) {
+  bn_finalize_body(blockIdx.x, part, nparts, Npad, C, count, gamma, beta, rmean, rvar, nbt, momentum, eps, training,
+                   out, yshift);
+}
+
+// The BNs of a fused 1x1 group (members = channel slices [off, off + C) of one GEMM's
+// statistics slab) finalized in one launch: block -> member by its first block.
+struct FinMember {
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  long long* nbt;
+  float* out;
+  float* yshift;
+  int off, C, blk0;
+  float momentum, eps;
+  int pad;
+};
+static_assert(sizeof(FinMember) == 80, "FinMember layout is mirrored by a ctypes.Structure");
+constexpr int FIN_MAX_MEMBERS = 4;
+struct FinGroup {
+  FinMember m[FIN_MAX_MEMBERS];
+  int n;
+};
+
+__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_group_kernel(FinGroup g, const float* __restrict__ part,
+                                                                            int nparts, int Npad, double count,
+                                                                            int training) {
+  int i = 0;
+  while (i + 1 < g.n && (int)blockIdx.x >= g.m[i + 1].blk0) ++i;
+  const FinMember& m = g.m[i];
+  bn_finalize_body(blockIdx.x - m.blk0, part + m.off, nparts, Npad, m.C, count, m.gamma, m.beta, m.rmean, m.rvar,
+                   m.nbt, m.momentum, m.eps, training, m.out, training ? m.yshift : nullptr);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -241,12 +280,53 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(
 
 // coef[3][C] = {k1 = gamma*invstd, dbeta/n, dgamma/n}; dgamma/dbeta written to the grads.
 // part rows have stride 2*ps (ps = C for bn_bwd_reduce partials, Npad for conv-epilogue partials).
+__device__ __forceinline__ void bn_bwd_finalize_body(int blk, const float* __restrict__ part, int nparts, int ps, int C,
+                                                     double count, const float* __restrict__ gamma,
+                                                     const float* __restrict__ ss, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, float* __restrict__ coef,
+                                                     int accumulate, int batch_stats);
+
 __global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nparts, int ps,
                                                                int C, double count, const float* __restrict__ gamma,
                                                                const float* __restrict__ ss,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                float* __restrict__ coef, int accumulate, int batch_stats) {
-  const int c = blockIdx.x * FIN_CH + threadIdx.x % FIN_CH;
+  bn_bwd_finalize_body(blockIdx.x, part, nparts, ps, C, count, gamma, ss, dgamma, dbeta, coef, accumulate,
+                       batch_stats);
+}
+
+// The BN backwards of a fused 1x1 group's members (each with its own partial slab and
+// parameters) finalized in one launch; each member's apply pass follows separately.
+struct BwdFinMember {
+  const float* part;
+  const float* gamma;
+  const float* ss;
+  float* dgamma;
+  float* dbeta;
+  float* coef;
+  int nparts, ps, C, blk0, accumulate, pad;
+};
+static_assert(sizeof(BwdFinMember) == 72, "BwdFinMember layout is mirrored by a ctypes.Structure");
+struct BwdFinGroup {
+  BwdFinMember m[FIN_MAX_MEMBERS];
+  int n;
+};
+
+__global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_bwd_finalize_group_kernel(BwdFinGroup g, double count,
+                                                                                int batch_stats) {
+  int i = 0;
+  while (i + 1 < g.n && (int)blockIdx.x >= g.m[i + 1].blk0) ++i;
+  const BwdFinMember& m = g.m[i];
+  bn_bwd_finalize_body(blockIdx.x - m.blk0, m.part, m.nparts, m.ps, m.C, count, m.gamma, m.ss, m.dgamma, m.dbeta,
+                       m.coef, m.accumulate, batch_stats);
+}
+
+__device__ __forceinline__ void bn_bwd_finalize_body(int blk, const float* __restrict__ part, int nparts, int ps, int C,
+                                                     double count, const float* __restrict__ gamma,
+                                                     const float* __restrict__ ss, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta, float* __restrict__ coef,
+                                                     int accumulate, int batch_stats) {
+  const int c = blk * FIN_CH + threadIdx.x % FIN_CH;
   double s1, s2;
   fin_reduce(part, nparts, ps, c, c < C, s1, s2);
   if (threadIdx.x >= FIN_CH || c >= C) return;
@@ -312,6 +392,23 @@ MILNCE_API int milnce_bn_finalize(const float* part, int nparts, int Npad, int C
   return (int)hipGetLastError();
 }
 
+// members: host array of n FinMember (off / C / gamma ... filled, blk0 computed here)
+MILNCE_API int milnce_bn_finalize_group(const void* members, int n, const float* part, int nparts, int Npad,
+                                        double count, int training, hipStream_t stream) {
+  if (n < 1 || n > FIN_MAX_MEMBERS) return (int)hipErrorInvalidValue;
+  FinGroup g;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    g.m[i] = ((const FinMember*)members)[i];
+    g.m[i].blk0 = blk;
+    blk += (g.m[i].C + FIN_CH - 1) / FIN_CH;
+  }
+  g.n = n;
+  hipLaunchKernelGGL(bn_finalize_group_kernel, dim3(blk), dim3(FIN_CH * FIN_RG), 0, stream, g, part, nparts, Npad,
+                     count, training);
+  return (int)hipGetLastError();
+}
+
 static int pick_splits(long long rows, int target_rows) {
   long long s = (rows + target_rows - 1) / target_rows;
   return (int)(s < 1 ? 1 : s);
@@ -369,6 +466,37 @@ MILNCE_API int milnce_bn_bwd_finalize(const float* part, int nparts, int ps, int
                                       int accumulate, int batch_stats, hipStream_t stream) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
                      part, nparts, ps, C, count, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
+  return (int)hipGetLastError();
+}
+
+// members: host array of n BwdFinMember (blk0 computed here); count = rows of the BN
+MILNCE_API int milnce_bn_bwd_finalize_group(const void* members, int n, double count, int batch_stats,
+                                            hipStream_t stream) {
+  if (n < 1 || n > FIN_MAX_MEMBERS) return (int)hipErrorInvalidValue;
+  BwdFinGroup g;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    g.m[i] = ((const BwdFinMember*)members)[i];
+    g.m[i].blk0 = blk;
+    blk += (g.m[i].C + FIN_CH - 1) / FIN_CH;
+  }
+  g.n = n;
+  hipLaunchKernelGGL(bn_bwd_finalize_group_kernel, dim3(blk), dim3(FIN_CH * FIN_RG), 0, stream, g, count,
+                     batch_stats);
+  return (int)hipGetLastError();
+}
+
+// milnce_bn_bwd's apply pass alone (coef already finalized, e.g. by milnce_bn_bwd_finalize_group)
+MILNCE_API int milnce_bn_bwd_apply(const void* dz, int ldz, const void* y, int ldy, const float* ss, const float* coef,
+                                   int C, long long M, void* dy, int lddy, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const int rpi = 256 / (C / 8);
+  long long nblk = (M + 16LL * rpi - 1) / (16LL * rpi);
+  if (nblk > 8192) nblk = 8192;
+  if (nblk < 1) nblk = 1;
+  const int rpb = (int)((M + nblk - 1) / nblk);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3((int)nblk), dim3(256), 0, stream, (const bf16_t*)dz, ldz,
+                     (const bf16_t*)y, ldy, ss, coef, C, M, rpb, (bf16_t*)dy, lddy);
   return (int)hipGetLastError();
 }
 
@@ -433,6 +561,20 @@ MILNCE_API int milnce_bn_bwd_gate(const void* dout, int ldo, const float* g, con
                      part, nparts, ps, C, (double)B * thw, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   const int rpi = 256 / (C / 8);
   int splits = (thw + 16 * rpi - 1) / (16 * rpi);  // >= 16 rows per thread
+  if (splits < 1) splits = 1;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(bn_bwd_apply_gate_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)dout, ldo, g,
+                     dmean, ldg, 1.f / thw, thw, rpb, (const bf16_t*)y, ldy, ss, coef, C, (bf16_t*)dy, lddy);
+  return (int)hipGetLastError();
+}
+
+// milnce_bn_bwd_gate's apply pass alone (coef already finalized)
+MILNCE_API int milnce_bn_bwd_gate_apply(const void* dout, int ldo, const float* g, const float* dmean, int ldg, int B,
+                                        int thw, const void* y, int ldy, const float* ss, const float* coef, int C,
+                                        void* dy, int lddy, hipStream_t stream) {
+  if (C % 8 || C > 2048) return (int)hipErrorInvalidValue;
+  const int rpi = 256 / (C / 8);
+  int splits = (thw + 16 * rpi - 1) / (16 * rpi);
   if (splits < 1) splits = 1;
   const int rpb = (thw + splits - 1) / splits;
   hipLaunchKernelGGL(bn_bwd_apply_gate_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)dout, ldo, g,

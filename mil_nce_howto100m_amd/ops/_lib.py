@@ -31,6 +31,10 @@ SIGNATURES: Dict[str, list] = {
     "milnce_wgrad_reduce": [P, P] + [I] * 8 + [P],
     "milnce_pack_weights_multi": [P, I, I, P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
+    "milnce_bn_finalize_group": [P, I, P, I, I, D, I, P],
+    "milnce_bn_bwd_finalize_group": [P, I, D, I, P],
+    "milnce_bn_bwd_apply": [P, I, P, I, P, P, I, L, P, I, P],
+    "milnce_bn_bwd_gate_apply": [P, I, P, P, I, I, I, P, I, P, P, I, P, I, P],
     "milnce_bn_relu_apply": [P, I, P, I, P, I, I, I, P, P],
     "milnce_bn_bwd": [P, I, P, I, P, I, L, P, P, I, I, I, P, P, P, P, I, I, I, P],
     "milnce_gate_fwd": [I, P, P, P, P, P, I, I, P, P, P, P, P, P, P, I, P],

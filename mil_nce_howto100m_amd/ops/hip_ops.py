@@ -467,6 +467,20 @@ def _pack(weight: torch.Tensor, plan: ConvPlan, mode: int) -> torch.Tensor:
 
 
 _GROUP_PREPACK = os.environ.get("MILNCE_GROUP_PREPACK", "1") != "0"
+_GROUP_FIN = os.environ.get("MILNCE_GROUP_FIN", "1") != "0"  # one BN-finalize launch per fused 1x1 group
+
+
+class _BwdFinMember(ctypes.Structure):
+    """Mirror of csrc/bn.hip ``BwdFinMember`` (72 bytes)."""
+    _fields_ = [(f, ctypes.c_void_p) for f in ("part", "gamma", "ss", "dgamma", "dbeta", "coef")] + \
+        [(f, ctypes.c_int) for f in ("nparts", "ps", "C", "blk0", "accumulate", "pad")]
+
+
+class _FinMember(ctypes.Structure):
+    """Mirror of csrc/bn.hip ``FinMember`` (80 bytes)."""
+    _fields_ = [(f, ctypes.c_void_p) for f in ("gamma", "beta", "rmean", "rvar", "nbt", "out", "yshift")] + \
+        [(f, ctypes.c_int) for f in ("off", "C", "blk0")] + [("momentum", ctypes.c_float), ("eps", ctypes.c_float),
+                                                              ("pad", ctypes.c_int)]
 _GROUP_WGRAD_DIRECT = os.environ.get("MILNCE_GROUP_WGRAD_DIRECT", "1") != "0"
 
 
@@ -1650,13 +1664,25 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
     zs, sss, gsum = [], [], None
     off = 0
     y2 = y.view(-1, ctot)
+    ss_all = torch.empty((4 * ctot,), dtype=F32, device=dev)  # member i: [4][c] at 4 * off
+    if _GROUP_FIN and n <= 4:
+        members = (_FinMember * n)()
+        o = 0
+        for i, (c, (gamma, beta, rmean, rvar, nbt)) in enumerate(zip(widths, bns)):
+            members[i] = _FinMember(ptr(gamma), ptr(beta), ptr(rmean), ptr(rvar), ptr(nbt) if training else None,
+                                    ptr(ss_all) + 16 * o, ptr(shift) + 4 * o if shift is not None else None,
+                                    o, c, 0, float(hyper[i][0]), float(hyper[i][1]), 0)
+            o += c
+        call("milnce_bn_finalize_group", ctypes.addressof(members), n, ptr(stats), plan.grid_m, plan.Npad,
+             float(plan.M), int(training), stream())
     for i, (c, (gamma, beta, rmean, rvar, nbt)) in enumerate(zip(widths, bns)):
-        ss = torch.empty((4 * c,), dtype=F32, device=dev)
-        st = stats[off:] if training else None
-        call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
-             ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
-             float(hyper[i][1]), int(training), ptr(ss), ptr(shift[off:off + c] if shift is not None else None),
-             stream())
+        ss = ss_all[4 * off:4 * (off + c)]
+        if not (_GROUP_FIN and n <= 4):
+            st = stats[off:] if training else None
+            call("milnce_bn_finalize", ptr(st), plan.grid_m, plan.Npad, c, float(plan.M), ptr(gamma), ptr(beta),
+                 ptr(rmean), ptr(rvar), ptr(nbt) if training else None, float(hyper[i][0]),
+                 float(hyper[i][1]), int(training), ptr(ss), ptr(shift[off:off + c] if shift is not None else None),
+                 stream())
         g = _zeros_f32((plan.B, c), dev) if (i == 0 and want_gsum0) else None
         ysl = y2[:, off:off + c]
         zshape = (plan.B, plan.To, plan.Ho, plan.Wo, c)
@@ -1699,8 +1725,7 @@ def _group_backward(ctx, grads, saved=None):
     dev = y.device
     dY = torch.empty((plan.M, ctot), dtype=BF16, device=dev)
     y2 = y.view(-1, ctot)
-    dgs, dbs = [], []
-    off = 0
+    mem = []  # per member: dz, lazy info, partials (part, nparts, ps, fused), coef, dgamma, dbeta, direct
     for i, c in enumerate(widths):
         dz = grads[i]
         if dz is None:
@@ -1722,12 +1747,35 @@ def _group_backward(ctx, grads, saved=None):
         direct_bn = g_direct is not None and b_direct is not None
         dgamma = g_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
         dbeta = b_direct if direct_bn else torch.empty((c,), dtype=F32, device=dev)
-        if lazy is not None:
+        mem.append((dz, lazy, (part, nparts, ps, fused is not None), coef, dgamma, dbeta, direct_bn))
+    # one finalize launch for the whole group when every member's partial sums are ready and its
+    # apply pass has an apply-only entry (plain or SelfGating-lazy dz)
+    grouped = _GROUP_FIN and n <= 4 and all(m[2][3] and (m[1] is None or m[1][0] == "gate") for m in mem)
+    if grouped:
+        members = (_BwdFinMember * n)()
+        for i, (c, (dz, lazy, (part, nparts, ps, _), coef, dgamma, dbeta, direct_bn)) in enumerate(zip(widths, mem)):
+            members[i] = _BwdFinMember(ptr(part), ptr(gammas[i]), ptr(sss[i]), ptr(dgamma), ptr(dbeta), ptr(coef),
+                                       nparts, ps, c, 0, int(direct_bn), 0)
+        call("milnce_bn_bwd_finalize_group", ctypes.addressof(members), n, float(plan.M), int(ctx.training),
+             stream())
+    dgs, dbs = [], []
+    off = 0
+    for i, (c, (dz, lazy, (part, nparts, ps, have_part), coef, dgamma, dbeta, direct_bn)) in enumerate(zip(widths,
+                                                                                                       mem)):
+        if grouped and lazy is not None:
+            _, dout, goff, g, dmean, thw = lazy
+            ld = dout.shape[-1]
+            call("milnce_bn_bwd_gate_apply", ptr(dout) + 2 * goff, ld, ptr(g) + 4 * goff, ptr(dmean) + 4 * goff, ld,
+                 plan.B, thw, ptr(y2[:, off:]), ctot, ptr(sss[i]), ptr(coef), c, ptr(dY[:, off:]), ctot, stream())
+        elif grouped:
+            call("milnce_bn_bwd_apply", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), ptr(coef), c, plan.M,
+                 ptr(dY[:, off:]), ctot, stream())
+        elif lazy is not None:
             _bn_bwd_lazy(lazy, plan.B, plan.M, y2[:, off:], ctot, sss[i], c, gammas[i], part, nparts, ps, dgamma,
                          dbeta, coef, dY[:, off:], ctot, direct_bn, ctx.training)
         else:
             call("milnce_bn_bwd", ptr(dz), c, ptr(y2[:, off:]), ctot, ptr(sss[i]), c, plan.M, ptr(gammas[i]),
-                 ptr(part), nparts, ps, int(fused is not None), ptr(dgamma), ptr(dbeta), ptr(coef),
+                 ptr(part), nparts, ps, int(have_part), ptr(dgamma), ptr(dbeta), ptr(coef),
                  ptr(dY[:, off:]), ctot, int(direct_bn), int(ctx.training), stream())
         if direct_bn:
             _grad_done(gammas[i])
