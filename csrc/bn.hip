@@ -435,6 +435,91 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
 // part holds nparts rows of [2][ps] partial sums. have_part = 1: they were produced by the kernel
 // that computed dz (conv dgrad epilogue, gate / pool backward), ps = that kernel's stride;
 // have_part = 0: reduce them here (ps = C).
+// ---------------------------------------------------------------------------------------
+// Large BN-backward partial slabs (a dgrad epilogue's one row per M tile: up to ~40k rows x 64
+// channels, 20 MB) are first summed over fixed row chunks by a full-chip pass; the finalize's
+// C/8 workgroups alone stream such a slab latency-bound (0.7 ms on the conv_2b BN). Fixed
+// chunks and a fixed-order lane sum keep the result deterministic. Out: [PRE_PARTS][2][ps].
+constexpr int PRE_MIN_PARTS = 2048, PRE_PARTS = 512;
+
+__global__ __launch_bounds__(256) void bn_part_prereduce_kernel(const float* __restrict__ part, int nparts, int ps,
+                                                                int C, float* __restrict__ out) {
+  __shared__ double red[256];
+  const int ncol = 2 * C;
+  const int width = ncol >= 256 ? 256 : ncol;
+  const int lanes = 256 / width;  // rows in flight per column
+  const int lane = threadIdx.x / width, tc = threadIdx.x % width;
+  const int rpb = (nparts + gridDim.x - 1) / gridDim.x;
+  const int r0 = blockIdx.x * rpb, r1 = min(nparts, r0 + rpb);
+  for (int j0 = 0; j0 < ncol; j0 += width) {  // block-uniform
+    const int j = j0 + tc;
+    const int col = j < C ? j : ps + (j - C);
+    double s0 = 0.0, s1 = 0.0;
+    if (lane < lanes && j < ncol) {
+      int r = r0 + lane;
+      for (; r + lanes < r1; r += 2 * lanes) {
+        s0 += (double)part[(long long)r * 2 * ps + col];
+        s1 += (double)part[(long long)(r + lanes) * 2 * ps + col];
+      }
+      if (r < r1) s0 += (double)part[(long long)r * 2 * ps + col];
+    }
+    red[threadIdx.x] = s0 + s1;
+    __syncthreads();
+    if (lane == 0 && j < ncol) {
+      double acc = 0.0;
+      for (int l = 0; l < lanes; ++l) acc += red[l * width + tc];
+      out[(long long)blockIdx.x * 2 * ps + col] = (float)acc;
+    }
+    __syncthreads();
+  }
+}
+
+// Scratch for the pre-reduced slabs, one growing buffer per stream (the BN backward runs on the
+// compute stream; a buffer is only reused in its stream's order).
+struct PreBuf {
+  hipStream_t stream;
+  int device;
+  float* buf;
+  size_t cap;
+};
+static PreBuf g_pre[16];
+static int g_npre = 0;
+
+static float* pre_scratch(size_t floats, hipStream_t stream) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  PreBuf* e = nullptr;
+  for (int i = 0; i < g_npre; ++i)
+    if (g_pre[i].stream == stream && g_pre[i].device == dev) e = &g_pre[i];
+  if (e == nullptr) {
+    if (g_npre == 16) return nullptr;
+    e = &g_pre[g_npre++];
+    *e = PreBuf{stream, dev, nullptr, 0};
+  }
+  if (e->cap < floats) {
+    if (e->buf != nullptr && (hipStreamSynchronize(stream) != hipSuccess || hipFree(e->buf) != hipSuccess)) return nullptr;
+    e->buf = nullptr;
+    e->cap = 0;
+    if (hipMalloc(&e->buf, floats * sizeof(float)) != hipSuccess) return nullptr;
+    e->cap = floats;
+  }
+  return e->buf;
+}
+
+// Pre-reduces one slab into dst (PRE_PARTS x 2 x ps floats) when it is large; updates part /
+// nparts to what the finalize should read.
+static void prereduce(const float*& part, int& nparts, int ps, int C, float* dst, hipStream_t stream) {
+  if (nparts < PRE_MIN_PARTS || dst == nullptr) return;
+  hipLaunchKernelGGL(bn_part_prereduce_kernel, dim3(PRE_PARTS), dim3(256), 0, stream, part, nparts, ps, C, dst);
+  part = dst;
+  nparts = PRE_PARTS;
+}
+
+static void prereduce1(const float*& part, int& nparts, int ps, int C, hipStream_t stream) {
+  if (nparts < PRE_MIN_PARTS) return;
+  prereduce(part, nparts, ps, C, pre_scratch((size_t)PRE_PARTS * 2 * ps, stream), stream);
+}
+
 MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
                              const float* gamma, float* part, int nparts, int ps, int have_part, float* dgamma,
                              float* dbeta, float* coef, void* dy, int lddy, int accumulate, int batch_stats,
@@ -446,8 +531,10 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
                        (const bf16_t*)y, ldy, ss, C, M, rows_per_block, part);
     ps = C;
   }
+  const float* fpart = part;
+  prereduce1(fpart, nparts, ps, C, stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
-                     part, nparts, ps, C,
+                     fpart, nparts, ps, C,
                      (double)M, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   const int rpi = 256 / (C / 8);
   long long nblk = (M + 16LL * rpi - 1) / (16LL * rpi);  // >= 16 rows per thread
@@ -464,6 +551,7 @@ MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, co
 MILNCE_API int milnce_bn_bwd_finalize(const float* part, int nparts, int ps, int C, double count,
                                       const float* gamma, const float* ss, float* dgamma, float* dbeta, float* coef,
                                       int accumulate, int batch_stats, hipStream_t stream) {
+  prereduce1(part, nparts, ps, C, stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
                      part, nparts, ps, C, count, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   return (int)hipGetLastError();
@@ -475,12 +563,22 @@ MILNCE_API int milnce_bn_bwd_finalize_group(const void* members, int n, double c
   if (n < 1 || n > FIN_MAX_MEMBERS) return (int)hipErrorInvalidValue;
   BwdFinGroup g;
   int blk = 0;
+  size_t need = 0;
   for (int i = 0; i < n; ++i) {
     g.m[i] = ((const BwdFinMember*)members)[i];
     g.m[i].blk0 = blk;
     blk += (g.m[i].C + FIN_CH - 1) / FIN_CH;
+    if (g.m[i].nparts >= PRE_MIN_PARTS) need += (size_t)PRE_PARTS * 2 * g.m[i].ps;
   }
   g.n = n;
+  if (need > 0) {  // each large member slab pre-reduced into its own region of the scratch
+    float* dst = pre_scratch(need, stream);
+    for (int i = 0; i < n && dst != nullptr; ++i) {
+      if (g.m[i].nparts < PRE_MIN_PARTS) continue;
+      prereduce(g.m[i].part, g.m[i].nparts, g.m[i].ps, g.m[i].C, dst, stream);
+      dst += (size_t)PRE_PARTS * 2 * g.m[i].ps;
+    }
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_group_kernel, dim3(blk), dim3(FIN_CH * FIN_RG), 0, stream, g, count,
                      batch_stats);
   return (int)hipGetLastError();
@@ -557,8 +655,10 @@ MILNCE_API int milnce_bn_bwd_gate(const void* dout, int ldo, const float* g, con
                                   float* part, int nparts, int ps, float* dgamma, float* dbeta, float* coef, void* dy,
                                   int lddy, int accumulate, int batch_stats, hipStream_t stream) {
   if (C % 8 || C > 2048) return (int)hipErrorInvalidValue;
+  const float* fpart = part;
+  prereduce1(fpart, nparts, ps, C, stream);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FIN_CH - 1) / FIN_CH), dim3(FIN_CH * FIN_RG), 0, stream,
-                     part, nparts, ps, C, (double)B * thw, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
+                     fpart, nparts, ps, C, (double)B * thw, gamma, ss, dgamma, dbeta, coef, accumulate, batch_stats);
   const int rpi = 256 / (C / 8);
   int splits = (thw + 16 * rpi - 1) / (16 * rpi);  // >= 16 rows per thread
   if (splits < 1) splits = 1;

@@ -1062,7 +1062,7 @@ _TWGRAD = os.environ.get("MILNCE_TWGRAD", "1") != "0"
 # so the forward's box kernel runs PRO 1 (applies it, writes no z): the input-sized z write of the
 # forward is gone (conv_2c's temporal conv: 2 GB per step). MILNCE_TW_PRO=0 keeps writing z.
 _TW_PRO = os.environ.get("MILNCE_TW_PRO", "1") != "0"
-_TW_OCCS = (1, 2)
+_TW_OCCS = tuple(int(v) for v in os.environ.get("MILNCE_TW_OCCS", "1,2").split(","))
 _TW_SPLITS: Dict[Tuple[int, int, int], Tuple[int, int]] = {}
 
 

@@ -5,6 +5,7 @@ same (upcast) values, so the tolerance covers accumulation order and the bf16 ro
 outputs only. Run on an MI355X: ``pytest -m gpu``.
 """
 import copy
+import ctypes
 
 import pytest
 import torch
@@ -918,6 +919,38 @@ def test_fused_bn_backward_partials_match_unfused():
         h.set_bn_bwd_fusion(old)
     for a, b in zip(fused, plain):
         assert rel_err(a, b) < 5e-3
+
+
+@pytest.mark.parametrize("nparts,C,ps", [(100, 64, 64), (2047, 24, 32), (2048, 64, 64), (40000, 64, 64),
+                                         (5000, 192, 256), (3000, 832, 832)])
+def test_bn_bwd_finalize_large_partial_slabs(nparts, C, ps):
+    """BN-backward finalize of [nparts][2][ps] partial slabs (pre-reduced by a full-chip pass from
+    2048 rows on, single and grouped entry points) == the fp64 sums."""
+    h = hip()
+    torch.manual_seed(nparts)
+    part = torch.randn(nparts, 2, ps, device=DEV)
+    gamma = torch.rand(C, device=DEV) + 0.5
+    ss = torch.rand(4 * C, device=DEV) + 0.5
+    M = 123456.0
+    ref = part[:, :, :C].double().sum(0)
+    want_coef = torch.cat([gamma * ss[C:2 * C], (ref[0] / M).float(), (ref[1] / M).float()])
+    for grouped in (False, True):
+        dg = torch.full((C,), 0.25, device=DEV)
+        db = torch.full((C,), -0.5, device=DEV)
+        coef = torch.empty(3 * C, device=DEV)
+        if grouped:
+            mem = (h._BwdFinMember * 1)()
+            mem[0] = h._BwdFinMember(h.ptr(part), h.ptr(gamma), h.ptr(ss), h.ptr(dg), h.ptr(db), h.ptr(coef),
+                                     nparts, ps, C, 0, 1, 0)
+            h.call("milnce_bn_bwd_finalize_group", ctypes.addressof(mem), 1, M, 1, h.stream())
+        else:
+            h.call("milnce_bn_bwd_finalize", h.ptr(part), nparts, ps, C, M, h.ptr(gamma), h.ptr(ss), h.ptr(dg),
+                   h.ptr(db), h.ptr(coef), 1, 1, h.stream())
+        torch.cuda.synchronize()
+        tol = 1e-6 * max(1.0, nparts ** 0.5)
+        assert torch.allclose(db.double(), ref[0] - 0.5, rtol=1e-5, atol=tol)
+        assert torch.allclose(dg.double(), ref[1] + 0.25, rtol=1e-5, atol=tol)
+        assert torch.allclose(coef, want_coef, rtol=1e-5, atol=1e-7)
 
 
 @pytest.mark.parametrize("B,T,S", [(2, 8, 64), (1, 4, 200)])
