@@ -189,6 +189,37 @@ __global__ void u8_to_bf16_kernel(const uint2* __restrict__ src, uint4* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// One rank's slice of the one-shot peer all-gather (parallel/peer.py): copy into each peer's
+// IPC-mapped receive buffer, issued on the local stream as plain vector loads / stores (the
+// stores travel over that peer's xGMI link); one launch covers every destination.
+constexpr int PEER_MAX = 8;
+struct PeerDsts {
+  void* dst[PEER_MAX];
+};
+
+__global__ __launch_bounds__(256) void peer_scatter_kernel(const uint4* __restrict__ src, PeerDsts d, int ndst,
+                                                           long long n16) {
+  const int k = blockIdx.y;  // destination
+  uint4* __restrict__ dst = (uint4*)d.dst[k < ndst ? k : 0];
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n16; i += (long long)gridDim.x * 256) dst[i] = src[i];
+}
+
+MILNCE_API int milnce_peer_scatter(const void* src, void* const* dsts, int ndst, long long bytes, hipStream_t stream) {
+  if (ndst < 1 || ndst > PEER_MAX || bytes % 16 || ((uintptr_t)src & 15)) return (int)hipErrorInvalidValue;
+  PeerDsts d;
+  for (int k = 0; k < PEER_MAX; ++k) {
+    d.dst[k] = dsts[k < ndst ? k : 0];
+    if (((uintptr_t)d.dst[k] & 15)) return (int)hipErrorInvalidValue;
+  }
+  const long long n16 = bytes / 16;
+  long long bx = (n16 + 255) / 256;
+  if (bx > 64) bx = 64;
+  if (bx < 1) bx = 1;
+  hipLaunchKernelGGL(peer_scatter_kernel, dim3((int)bx, ndst), dim3(256), 0, stream, (const uint4*)src, d, ndst, n16);
+  return (int)hipGetLastError();
+}
+
 MILNCE_API int milnce_u8_to_bf16(const void* src, void* dst, long long n, hipStream_t stream) {
   if (n % 8) return (int)hipErrorInvalidValue;
   const long long n8 = n / 8;

@@ -91,6 +91,8 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--bucket_mb", type=float, default=8.0, help="gradient all-reduce bucket size (MiB)")
     g.add_argument("--grad_comm_dtype", type=str, default="fp32", choices=("fp32", "bf16"),
                    help="gradient all-reduce wire dtype (bf16 halves the bytes, sums in bf16)")
+    g.add_argument("--emb_gather", type=str, default="rccl", choices=("rccl", "peer"),
+                   help="MIL-NCE negatives all-gather: RCCL ring, or one-shot xGMI peer writes (same node)")
     g.add_argument("--broadcast_buffers", type=int, default=1, help="broadcast BN buffers from rank 0 each step")
     g.add_argument("--blocks", type=str, default="", help="comma list of inception blocks to keep (plumbing)")
     g.add_argument("--log_jsonl", type=str, default="", help="also write metrics as JSON lines here")

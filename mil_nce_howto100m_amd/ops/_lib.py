@@ -64,6 +64,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_adam": [P, P, P, P, L, F, F, F, F, F, F, F, F, P],
     "milnce_synth_video": [P, P, I, I, I, P, P],
     "milnce_synth_meta": [L, I, I, I, I, I, I, I, P, P, P, P, P],
+    "milnce_peer_scatter": [P, P, I, L, P],
     "milnce_stem_prep": [P, I, I, I, I, I, P, P],
     "milnce_u8_to_bf16": [P, P, L, P],
     "milnce_text_relu_max": [P, I, I, I, P, P, P],

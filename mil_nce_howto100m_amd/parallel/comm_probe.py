@@ -89,4 +89,18 @@ def probe(grad_numel: int, buckets: Sequence[Sequence[int]], emb_rows: int, emb_
     out["allgather_kib"] = round(gbytes / 1024, 1)
     out["allgather_ms"] = round(ag * 1e3, 3)
     out["allgather_busbw_gbps"] = round(gbytes * (world - 1) / world / ag / 1e9, 2)
+    if cuda:  # the one-shot peer-write path (--emb_gather peer, parallel/peer.py) on the same sizes
+        from .peer import PeerAllGather
+        pg = PeerAllGather()
+        want = gathered.clone()
+        ok = True
+        try:
+            got = pg.gather(emb)
+            if want is not None:
+                ok = bool(torch.equal(got, want))
+            pag = _timed(lambda: pg.gather(emb), reps, cuda)
+            out["peer_allgather_ms"] = round(pag * 1e3, 3)
+            out["peer_allgather_matches"] = ok
+        except Exception as e:  # e.g. no IPC between these processes: recorded, not fatal
+            out["peer_allgather_error"] = f"{type(e).__name__}: {e}"[:200]
     return out

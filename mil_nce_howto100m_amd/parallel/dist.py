@@ -106,11 +106,28 @@ def destroy() -> None:
         dist.destroy_process_group()
 
 
+_EMB_GATHER = "rccl"
+
+
+def set_emb_gather(mode: str) -> None:
+    """Embedding all-gather path: "rccl" (ring all-gather) or "peer" (one-shot xGMI peer writes,
+    parallel/peer.py; same-node process groups only)."""
+    global _EMB_GATHER
+    if mode not in ("rccl", "peer"):
+        raise ValueError(f"unknown embedding gather {mode!r}")
+    _EMB_GATHER = mode
+
+
 class _GatherLocalGrad(torch.autograd.Function):
     """all_gather forward, local-slice backward (utils.py:8-24)."""
 
     @staticmethod
     def forward(ctx, packed: torch.Tensor, world: int, rank: int):
+        ctx.rows = packed.shape[0]
+        ctx.rank = rank
+        if packed.is_cuda and _EMB_GATHER == "peer":
+            from .peer import peer_all_gather
+            return peer_all_gather(packed)
         out = packed.new_empty((world * packed.shape[0],) + tuple(packed.shape[1:]))
         if packed.is_cuda and dist.get_backend() == "gloo":
             # gloo over device tensors (multi-rank tests sharing one GPU): gather on the host

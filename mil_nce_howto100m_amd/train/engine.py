@@ -60,6 +60,7 @@ class Trainer:
         self.device = ctx.device
         # the reference overwrites --rank / --world-size with the process's own (main_distributed.py:46-47,69)
         args.rank, args.world_size = ctx.rank, ctx.world_size
+        pdist.set_emb_gather(getattr(args, "emb_gather", "rccl"))
         broadcast_parameters(model, ctx.world_size)
         params = list(model.parameters())
         scale = 1.0 / ctx.world_size if getattr(args, "grad_scale", "reference") == "reference" else 1.0

@@ -46,9 +46,14 @@ def _args(extra=()):
                           "--lr", "1e-3", *extra])
 
 
-def _worker_gather(rank, world, port, outdir):
+def _worker_gather(rank, world, port, outdir, mode="rccl"):
     ctx = _init(rank, world, port)
-    from mil_nce_howto100m_amd.parallel.dist import all_gather_embeddings
+    from mil_nce_howto100m_amd.parallel.dist import all_gather_embeddings, set_emb_gather
+    set_emb_gather(mode)
+    if mode == "peer":  # the peer path's host fallback (CPU tensors) keeps the rank-major layout
+        from mil_nce_howto100m_amd.parallel.peer import PeerAllGather
+        got = PeerAllGather().gather(torch.full((3, 2), float(rank)))
+        assert torch.equal(got[:, 0], torch.tensor([0.0] * 3 + [1.0] * 3))
     v = torch.full((2, 3), float(rank), requires_grad=True)
     t = torch.full((4, 3), 10.0 + rank, requires_grad=True)
     gv, gt = all_gather_embeddings(v, t, ctx)
@@ -57,10 +62,11 @@ def _worker_gather(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_allgather_semantics():
+@pytest.mark.parametrize("mode", ["rccl", "peer"])
+def test_allgather_semantics(mode):
     world, port = 2, _port()
     with tempfile.TemporaryDirectory() as out:
-        mp.spawn(_worker_gather, args=(world, port, out), nprocs=world)
+        mp.spawn(_worker_gather, args=(world, port, out, mode), nprocs=world)
         res = _collect(out, world)
     for rank, gv, gt, vg, tg in res:
         assert torch.equal(gv[:, 0], torch.tensor([0.0, 0.0, 1.0, 1.0]))
