@@ -1271,16 +1271,15 @@ __global__ __launch_bounds__(256, 1) void conv_wgrad_v3_kernel(WgradParams p) {
 // split slabs of the wide-occupancy wgrad tilings no longer run one latency-bound chain per thread.
 constexpr int WR_GROUPS = 4;
 
-__global__ __launch_bounds__(64 * WR_GROUPS) void wgrad_reduce_kernel(const float* __restrict__ slab,
-                                                                     float* __restrict__ dw, int splits, int Npad,
-                                                                     int Kpad, int Cout, int Cin, int Cin_param,
-                                                                     int taps, int accumulate) {
+__device__ __forceinline__ void wgrad_reduce_body(int blk, int nblk, const float* __restrict__ slab,
+                                                  float* __restrict__ dw, int splits, int Npad, int Kpad, int Cout,
+                                                  int Cin, int Cin_param, int taps, int accumulate) {
   __shared__ float part[WR_GROUPS][64];
   const int Ktot = taps * Cin;
   const long long total = (long long)Cout * Ktot;
   const long long plane = (long long)Npad * Kpad;
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  for (long long base = blockIdx.x * 64LL; base < total; base += gridDim.x * 64LL) {  // block-uniform
+  for (long long base = blk * 64LL; base < total; base += nblk * 64LL) {  // block-uniform
     const long long idx = base + e;
     const int n = (int)(idx / Ktot);
     const int k = (int)(idx - (long long)n * Ktot);
@@ -1309,6 +1308,39 @@ __global__ __launch_bounds__(64 * WR_GROUPS) void wgrad_reduce_kernel(const floa
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(64 * WR_GROUPS) void wgrad_reduce_kernel(const float* __restrict__ slab,
+                                                                     float* __restrict__ dw, int splits, int Npad,
+                                                                     int Kpad, int Cout, int Cin, int Cin_param,
+                                                                     int taps, int accumulate) {
+  wgrad_reduce_body(blockIdx.x, gridDim.x, slab, dw, splits, Npad, Kpad, Cout, Cin, Cin_param, taps, accumulate);
+}
+
+// Several pending slab reductions (the side stream's wgrads of consecutive layers, hip_ops
+// _ReduceBatcher) in one launch: block -> reduction by its first block. Same per-element order
+// as wgrad_reduce_kernel (bitwise equal results).
+struct ReduceDesc {
+  const float* slab;
+  float* dw;
+  int splits, Npad, Kpad, Cout, Cin, Cin_param, taps, accumulate, blk0, nblk;
+};
+static_assert(sizeof(ReduceDesc) == 56, "ReduceDesc layout is mirrored by a ctypes.Structure");
+constexpr int REDUCE_BATCH_MAX = 32;
+struct ReduceBatch {
+  ReduceDesc d[REDUCE_BATCH_MAX];
+  int n;
+};
+
+__global__ __launch_bounds__(64 * WR_GROUPS) void wgrad_reduce_batch_kernel(ReduceBatch b) {
+  int lo = 0, hi = b.n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (b.d[mid].blk0 <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const ReduceDesc& d = b.d[lo];
+  wgrad_reduce_body(blockIdx.x - d.blk0, d.nblk, d.slab, d.dw, d.splits, d.Npad, d.Kpad, d.Cout, d.Cin, d.Cin_param,
+                    d.taps, d.accumulate);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2317,6 +2349,24 @@ int launch_wgrad_reduce(const float* slab, float* dw, int splits, int Npad, int 
   const int grid = (int)((total + 63) / 64 < 16384 ? (total + 63) / 64 : 16384);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid), dim3(64 * WR_GROUPS), 0, stream, slab, dw, splits, Npad, Kpad,
                      Cout, Cin, Cin_param, taps, accumulate);
+  return (int)hipGetLastError();
+}
+
+// descs: host array of n ReduceDesc (blk0 / nblk filled here)
+MILNCE_API int milnce_wgrad_reduce_batch(const void* descs, int n, hipStream_t stream) {
+  if (n < 1 || n > REDUCE_BATCH_MAX) return (int)hipErrorInvalidValue;
+  ReduceBatch b;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    b.d[i] = ((const ReduceDesc*)descs)[i];
+    const long long total = (long long)b.d[i].Cout * b.d[i].taps * b.d[i].Cin;
+    const long long want = (total + 63) / 64;
+    b.d[i].nblk = (int)(want < 2048 ? (want < 1 ? 1 : want) : 2048);
+    b.d[i].blk0 = blk;
+    blk += b.d[i].nblk;
+  }
+  b.n = n;
+  hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(blk), dim3(64 * WR_GROUPS), 0, stream, b);
   return (int)hipGetLastError();
 }
 

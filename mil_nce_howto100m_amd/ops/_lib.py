@@ -29,6 +29,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_halo_wgrad_plan": [I] * 12 + [P, P],
     "milnce_halo_wgrad": [P, I, P, P, P, I] + [I] * 13 + [P],
     "milnce_wgrad_reduce": [P, P] + [I] * 8 + [P],
+    "milnce_wgrad_reduce_batch": [P, I, P],
     "milnce_pack_weights_multi": [P, I, I, P],
     "milnce_bn_finalize": [P, I, I, I, D, P, P, P, P, P, F, F, I, P, P, P],
     "milnce_bn_finalize_group": [P, I, P, I, I, D, I, P],

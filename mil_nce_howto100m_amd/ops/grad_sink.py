@@ -10,6 +10,12 @@ trainer calls before the optimizer step); the first deferral of a backward pass 
 drain as an autograd end-of-pass callback."""
 _SINK = None
 _PENDING = []
+_ON_DRAIN = []  # run (once) by the next drain before it waits: e.g. hip_ops' batched slab reductions
+
+
+def on_drain(fn) -> None:
+    if fn not in _ON_DRAIN:
+        _ON_DRAIN.append(fn)
 
 
 def set_sink(fn) -> None:
@@ -35,6 +41,8 @@ def defer(event) -> None:
 
 
 def drain() -> None:
+    while _ON_DRAIN:
+        _ON_DRAIN.pop(0)()
     if not _PENDING:
         return
     import torch
@@ -45,4 +53,4 @@ def drain() -> None:
 
 
 def pending() -> int:
-    return len(_PENDING)
+    return len(_PENDING) + len(_ON_DRAIN)

@@ -1127,6 +1127,63 @@ def _side_stream(device: torch.device) -> "torch.cuda.Stream":
     return s
 
 
+class _ReduceDesc(ctypes.Structure):
+    """Mirror of csrc/conv.hip ``ReduceDesc`` (56 bytes)."""
+    _fields_ = [("slab", ctypes.c_void_p), ("dw", ctypes.c_void_p)] + \
+        [(f, ctypes.c_int) for f in ("splits", "Npad", "Kpad", "Cout", "Cin", "Cin_param", "taps", "accumulate",
+                                     "blk0", "nblk")]
+
+
+# Batched side-stream slab reductions (MILNCE_REDUCE_BATCH, default on): a side-stream wgrad only
+# fills its split-K slab; the reductions into the parameters' gradients queue here and run as ONE
+# launch (csrc/conv.hip wgrad_reduce_batch_kernel, bitwise equal to one launch each) when 16 are
+# pending or when anything reads the gradients (grad_sink.drain runs the flush first: the bucket
+# all-reduces, the optimizer, the end of the backward pass). ~77 reduce launches per step -> ~6.
+_REDUCE_BATCH = os.environ.get("MILNCE_REDUCE_BATCH", "1") != "0"
+_REDUCE_BATCH_N = 16
+
+
+class _ReduceBatcher:
+    def __init__(self):
+        self.items = []  # (slab address, grad address, splits, npad, kpad, rows, cin, cin_p, taps)
+        self.slabs = []
+        self.targets = set()  # grad addresses of the pending items
+        self.device = None
+
+    def add(self, slab: torch.Tensor, entries, device) -> None:
+        if not self.items and not self.slabs:
+            grad_sink.on_drain(self.flush)
+            try:  # the end of the running backward pass drains (and so flushes)
+                torch.autograd.Variable._execution_engine.queue_callback(grad_sink.drain)
+            except RuntimeError:
+                pass
+        if any(e[1] in self.targets for e in entries):
+            self.flush()  # one launch must not accumulate twice into a gradient (racing read-modify-writes)
+        self.device = device
+        self.slabs.append(slab)
+        self.items.extend(entries)
+        self.targets.update(e[1] for e in entries)
+        if len(self.items) >= _REDUCE_BATCH_N:
+            self.flush()
+
+    def flush(self) -> None:
+        if not self.items:
+            return
+        side = _side_stream(self.device)
+        arr = (_ReduceDesc * len(self.items))()
+        for i, (sptr, gptr, splits, npad, kpad, rows, cin, cin_p, taps) in enumerate(self.items):
+            arr[i] = _ReduceDesc(sptr, gptr, splits, npad, kpad, rows, cin, cin_p, taps, 1, 0, 0)
+        call("milnce_wgrad_reduce_batch", ctypes.addressof(arr), len(self.items), side.cuda_stream)
+        self.items, self.slabs = [], []  # slabs: side-stream allocations, reused in that stream's order
+        self.targets = set()
+        ev = torch.cuda.Event()
+        ev.record(side)
+        grad_sink.defer(ev)
+
+
+_REDUCER = _ReduceBatcher()
+
+
 def _reduce_on_side(slab: torch.Tensor, dw: torch.Tensor, splits: int, npad: int, kpad: int, plan: ConvPlan,
                     accumulate: int) -> None:
     main = torch.cuda.current_stream(slab.device)
@@ -1235,17 +1292,27 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         main = torch.cuda.current_stream(dy.device)
         side = _side_stream(dy.device)
         side.wait_stream(main)
+        batched = _REDUCE_BATCH and plan.w_impl is not None
         with torch.cuda.stream(side):
-            if outs is not None:
+            if batched:  # the slab now, its reduction(s) with the next batch (_ReduceBatcher)
+                slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
+                taps = kt * kh * kw
+                dsts = outs if outs is not None else [(0, plan.Cout, dw)]
+                entries = [(ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows, plan.Cin, plan.Cin_p, taps)
+                           for off, rows, g in dsts]
+            elif outs is not None:
                 launch_split()
             else:
                 launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
         for t in (dy, x, xss):
             if t is not None:
                 t.record_stream(side)
-        ev = torch.cuda.Event()
-        ev.record(side)
-        grad_sink.defer(ev)
+        if batched:
+            _REDUCER.add(slab, entries, dy.device)
+        else:
+            ev = torch.cuda.Event()
+            ev.record(side)
+            grad_sink.defer(ev)
         if outs is not None:
             return None
     elif defer and out is not None and _DEFER_WGRAD:

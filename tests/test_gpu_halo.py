@@ -111,14 +111,17 @@ def test_fused_milnce_speed_report(B):
     print(f"B {B}: fused {res[True]:.3f} ms, materialised {res[False]:.3f} ms")
 
 
+@pytest.mark.parametrize("batch", [True, False])
 @pytest.mark.parametrize("k,halo", [((1, 3, 3), True), ((1, 3, 3), False), ((3, 1, 1), False), ((1, 1, 1), False)])
-def test_deferred_wgrad_reduce_matches_inline(k, halo, monkeypatch):
-    """conv_wgrad(defer=True): the split-K slab reduction runs on a side stream and lands in the
-    accumulated gradient once grad_sink.drain() joined it -- same values as the inline reduce,
-    also when the main stream immediately reuses freed memory for new work."""
+def test_deferred_wgrad_reduce_matches_inline(k, halo, batch, monkeypatch):
+    """conv_wgrad(defer=True): the wgrad runs on the side stream (its slab reductions batched into
+    one launch, or one each) and lands in the accumulated gradient once grad_sink.drain() joined
+    it -- same values as the inline reduce, also when the main stream immediately reuses freed
+    memory for new work."""
     from mil_nce_howto100m_amd.ops import grad_sink
     from mil_nce_howto100m_amd.ops import hip_ops as h
     monkeypatch.setattr(h, "_DEFER_WGRAD", True)
+    monkeypatch.setattr(h, "_REDUCE_BATCH", batch)
     torch.manual_seed(7)
     B, T, H, W, Cin, Cout = 4, 8, 25, 25, 64, 192
     pad = tuple(kk // 2 for kk in k)
@@ -138,6 +141,7 @@ def test_deferred_wgrad_reduce_matches_inline(k, halo, monkeypatch):
         h.conv_wgrad(dy, x, plan, out=out, defer=True)
         junk = [torch.full((1 << 20,), 9.0, device="cuda") for _ in range(8)]
         del junk
+    # batched: each call targets the same gradient, so every add flushes the previous one
     assert grad_sink.pending() == 3
     grad_sink.drain()
     assert grad_sink.pending() == 0
@@ -145,3 +149,13 @@ def test_deferred_wgrad_reduce_matches_inline(k, halo, monkeypatch):
     torch.cuda.synchronize()
     err = ((out - expect).norm() / (expect - 0.25).norm()).item()
     assert err < 1e-6, err
+    # the batched reduction sums each element in the per-launch order: bitwise the same
+    out1 = torch.full((Cout, Cin) + k, 0.25, device="cuda")
+    h.conv_wgrad(dy, x, plan, out=out1, defer=True)
+    grad_sink.drain()
+    monkeypatch.setattr(h, "_REDUCE_BATCH", not batch)
+    out2 = torch.full((Cout, Cin) + k, 0.25, device="cuda")
+    h.conv_wgrad(dy, x, plan, out=out2, defer=True)
+    grad_sink.drain()
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)

@@ -109,7 +109,7 @@ def test_group_launch_merging_matches_per_member(monkeypatch):
     data = SyntheticClips(4, 8, 64, 2, 20, 1000, device=ctx.device)
     res = []
     for merged in (True, False):
-        for flag in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT"):
+        for flag in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT", "_REDUCE_BATCH"):
             monkeypatch.setattr(h, flag, merged)
         seed_everything(1, 0)
         tr = Trainer(args, build_model(args, ctx.device), ctx, 10)
