@@ -50,6 +50,9 @@ def main():
     ap.add_argument("--seq_len", type=int, default=8, help="clips per sequence for the soft-DTW losses")
     ap.add_argument("--grad_cache_chunks", type=int, default=-1,
                     help="GradCache micro-batches per GPU (config 5: 32f, 1024 clips/GPU)")
+    ap.add_argument("--prefetch", type=int, default=0,
+                    help="generate the next step's synthetic batch on a side stream during the current step "
+                         "(same-box A/B: 4592 vs 4677 pairs/s without, profiles/r5_launch_merge.md)")
     ap.add_argument("--save_plan", type=str, default="",
                     help="write this run's kernel-plan decisions as a plan table (ops/tune_sync.py)")
     opts = ap.parse_args()
@@ -86,6 +89,11 @@ def main():
     model = build_model(args, ctx.device)
     trainer = Trainer(args, model, ctx, len(data))
     cuda = ctx.device.type == "cuda"
+    if cuda and opts.prefetch:
+        # the next step's batch is generated on a side stream during the current step
+        # (data/loader.py PrefetchedBatches; each timed step still generates one batch)
+        from mil_nce_howto100m_amd.data.loader import PrefetchedBatches
+        data = PrefetchedBatches(data, ctx.device)
 
     def sync():
         if cuda:

@@ -110,6 +110,42 @@ class DevicePrefetcher:
         return batch, ev
 
 
+class PrefetchedBatches:
+    """``batch(step)`` of an on-device generator (SyntheticClips / SyntheticSequences) with the next
+    step's batch generated on a side stream while the current step runs, as a DataLoader's workers
+    prefetch: every call still generates one batch (the next one), the step only waits for the
+    event of its own. The side stream starts each batch after the work queued so far (the previous
+    step), so it overlaps the current step's forward; the batch tensors are recorded on the
+    consuming stream for the allocator."""
+
+    def __init__(self, data, device: torch.device):
+        self.data, self.device = data, device
+        self.stream = torch.cuda.Stream(device=device)
+        self.next = None
+        self.epoch_len = getattr(data, "epoch_len", 0)
+
+    def __len__(self) -> int:
+        return len(self.data)
+
+    def batch(self, step: int) -> Dict:
+        main = torch.cuda.current_stream(self.device)
+        if self.next is not None and self.next[0] == step:
+            _, b, ev = self.next
+            main.wait_event(ev)
+            for t in b.values():
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(main)
+        else:
+            b = self.data.batch(step)
+        self.stream.wait_stream(main)
+        with torch.cuda.stream(self.stream):
+            nb = self.data.batch(step + 1)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.next = (step + 1, nb, ev)
+        return b
+
+
 class SyntheticFeed:
     def __init__(self, data):
         self.data = data

@@ -1114,6 +1114,8 @@ _DEFER_WGRAD = os.environ.get("MILNCE_DEFER_WGRAD", "0") == "1"
 # dgrad (+2.4 %), high-priority streams for either side (+1-2 %) and CU-masked side streams
 # (-15 %) all measured lower.
 _WGRAD_SIDE = os.environ.get("MILNCE_WGRAD_SIDE", "1") != "0"
+# layers with more output rows than this keep their wgrad on the main stream (A/B knob; 0 = none)
+_WGRAD_SIDE_MAX_M = int(os.environ.get("MILNCE_WGRAD_SIDE_MAX_M", "0"))
 _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 
 
@@ -1283,10 +1285,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             for off, rows, g in outs:
                 call("milnce_wgrad_reduce", ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows,
                      plan.Cin, plan.Cin_p, kt * kh * kw, 1, stream())
-        if not (defer and _WGRAD_SIDE):
-            launch_split()
-            return None
-    if defer and (out is not None or outs is not None) and _WGRAD_SIDE:
+    side_ok = _WGRAD_SIDE and (_WGRAD_SIDE_MAX_M <= 0 or plan.M <= _WGRAD_SIDE_MAX_M)
+    if outs is not None and not (defer and side_ok):
+        launch_split()
+        return None
+    if defer and (out is not None or outs is not None) and side_ok:
         # the whole weight gradient on the side stream, overlapping the rest of the backward
         # pass (its operands are kept alive for that stream; grad_sink joins it)
         main = torch.cuda.current_stream(dy.device)
