@@ -187,6 +187,7 @@ def main():
                        "grad_cache_chunks": trainer.grad_cache_chunks()},
             "final_loss": round(final_loss, 4),
             "peak_mem_gib": round(peak, 2),
+            "peak_reserved_gib": round(torch.cuda.max_memory_reserved() / 2 ** 30, 2) if cuda else 0.0,
         }
         out["plan_hash"] = hashes[0] if len(set(hashes)) == 1 else hashes
         # where the kernel plan came from: the shipped plan table (ops/plans/gfx950.json, valid for

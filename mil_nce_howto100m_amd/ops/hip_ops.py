@@ -74,6 +74,7 @@ def zero_arena_begin(device: torch.device) -> None:
     if device.type == "cuda":
         _ARENA.begin(device)
         _PACKER.begin(device)
+        _refresh_headroom(device)
 
 
 def zero_arena_end() -> None:
@@ -1116,6 +1117,29 @@ _DEFER_WGRAD = os.environ.get("MILNCE_DEFER_WGRAD", "0") == "1"
 _WGRAD_SIDE = os.environ.get("MILNCE_WGRAD_SIDE", "1") != "0"
 # layers with more output rows than this keep their wgrad on the main stream (A/B knob; 0 = none)
 _WGRAD_SIDE_MAX_M = int(os.environ.get("MILNCE_WGRAD_SIDE_MAX_M", "0"))
+# Memory headroom rule: a side-stream wgrad keeps its operands (dy, x) alive until the side stream
+# passes it, and the cross-stream frees inflate the caching allocator's reserved pool (bs 256:
+# 153 GiB reserved for 27 GiB allocated, 36.5 GiB inline). Near capacity the allocator then keeps
+# missing, frees its cache and retries (BASELINE config 5, 1024 clips x 32 frames, 209 GiB peak:
+# 2537 ms/step with side-stream wgrads vs 491 inline). So wgrads go to the side stream only while
+# the step's peak ALLOCATED memory (not the inflated reserved pool) is below this fraction of the
+# device; checked once per step (max_memory_allocated builds the allocator's stats dict).
+_WGRAD_SIDE_MEM_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_MEM_FRAC", "0.4"))
+_HEADROOM: Dict[int, bool] = {}  # per device, refreshed at each training-step start (zero_arena_begin)
+_DEV_TOTAL: Dict[int, int] = {}
+
+
+def _refresh_headroom(device: torch.device) -> None:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    total = _DEV_TOTAL.get(idx)
+    if total is None:
+        total = _DEV_TOTAL[idx] = torch.cuda.get_device_properties(idx).total_memory
+    _HEADROOM[idx] = torch.cuda.max_memory_allocated(idx) < _WGRAD_SIDE_MEM_FRAC * total
+
+
+def _side_headroom(device: torch.device) -> bool:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _HEADROOM.get(idx, True)
 _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 
 
@@ -1285,7 +1309,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
             for off, rows, g in outs:
                 call("milnce_wgrad_reduce", ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows,
                      plan.Cin, plan.Cin_p, kt * kh * kw, 1, stream())
-    side_ok = _WGRAD_SIDE and (_WGRAD_SIDE_MAX_M <= 0 or plan.M <= _WGRAD_SIDE_MAX_M)
+    side_ok = (_WGRAD_SIDE and (_WGRAD_SIDE_MAX_M <= 0 or plan.M <= _WGRAD_SIDE_MAX_M)
+               and _side_headroom(dy.device))
     if outs is not None and not (defer and side_ok):
         launch_split()
         return None
