@@ -1739,7 +1739,7 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ws = (bf16_t*)smem;                      // [64][STF_LDW]
   bf16_t* X = Ws + 64 * STF_LDW;                   // [HALO][8]
-  float* red = (float*)(X + HALO * 8);             // [2][64] stats reduction
+  float* red = (float*)(X + HALO * 8);             // [NPG][128] stats: one row per position group
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1762,8 +1762,6 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
     }
     *(uint4*)(Ws + n * STF_LDW + k8 * 8) = wv;
   }
-  if (tid < 128) red[tid] = 0.f;
-
   using HReg = typename std::conditional<U8, uint2, uint4>::type;
   HReg hreg[HREG];
   // uint8 clip: converted (integer-valued bf16) part-way through the current item's K loop, where
@@ -1916,7 +1914,8 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
     if (it + 2 * (int)gridDim.x < p.nitems) load(it + 2 * gridDim.x);
     lds_barrier();  // LDS only: the register prefetch of item it + 2 * grid stays in flight
   }
-  // statistics: reduce over the 16 lanes of a channel group, then over the position-half waves
+  // statistics: reduce over the 16 lanes of a channel group, then over the position groups in a
+  // fixed order (each group's partials in its own LDS row: deterministic, no LDS atomics)
 #pragma unroll
   for (int nf = 0; nf < CW; ++nf)
 #pragma unroll
@@ -1926,18 +1925,23 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
       for (int o = 1; o < 16; o <<= 1) { a += __shfl_xor(a, o, 64); b2 += __shfl_xor(b2, o, 64); }
       if (l16 == 0) {
         const int c = cbase + nf * 16 + lg * 4 + r;
-        atomicAdd(&red[c], a);
-        atomicAdd(&red[64 + c], b2);
+        red[ph * 128 + c] = a;
+        red[ph * 128 + 64 + c] = b2;
       }
     }
   __syncthreads();
-  if (tid < 128) p.stats[(long long)blockIdx.x * 128 + tid] = red[tid];
+  if (tid < 128) {
+    float v = red[tid];
+#pragma unroll
+    for (int g = 1; g < NPG; ++g) v += red[g * 128 + tid];
+    p.stats[(long long)blockIdx.x * 128 + tid] = v;
+  }
 }
 
 template <int W2, bool U8, int HR, int NPG, int CW = 2>
 static int launch_stem_fwd_t(StemFwdParams& p, int grid, hipStream_t stream) {
   constexpr int HALO = 3 * (2 * HR + 5) * (W2 + 4);
-  constexpr size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + 128 * 4;
+  constexpr size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + (size_t)NPG * 128 * 4;
   static_assert(lds <= 160 * 1024, "stem forward LDS");
   static bool attr_set = false;
   if (!attr_set) {

@@ -13,9 +13,17 @@ _PENDING = []
 _ON_DRAIN = []  # run (once) by the next drain before it waits: e.g. hip_ops' batched slab reductions
 
 
+_AFTER_DRAIN = []  # run by every drain after the current stream waits (persistent registrations)
+
+
 def on_drain(fn) -> None:
     if fn not in _ON_DRAIN:
         _ON_DRAIN.append(fn)
+
+
+def after_drain(fn) -> None:
+    if fn not in _AFTER_DRAIN:
+        _AFTER_DRAIN.append(fn)
 
 
 def set_sink(fn) -> None:
@@ -43,13 +51,14 @@ def defer(event) -> None:
 def drain() -> None:
     while _ON_DRAIN:
         _ON_DRAIN.pop(0)()
-    if not _PENDING:
-        return
-    import torch
-    s = torch.cuda.current_stream()
-    for e in _PENDING:
-        s.wait_event(e)
-    _PENDING.clear()
+    if _PENDING:
+        import torch
+        s = torch.cuda.current_stream()
+        for e in _PENDING:
+            s.wait_event(e)
+        _PENDING.clear()
+    for fn in _AFTER_DRAIN:
+        fn()
 
 
 def pending() -> int:

@@ -7,6 +7,7 @@ the stem) which go to hipBLASLt through ``torch.mm``. Shapes are planned once pe
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import math
@@ -1210,6 +1211,37 @@ class _ReduceBatcher:
 _REDUCER = _ReduceBatcher()
 
 
+class _SideKeep:
+    """Operands (dy, x, ...) of the side-stream wgrads, kept referenced until the side stream is
+    known to be past them -- their event completed, or a grad_sink.drain made the current stream
+    wait for it -- instead of ``record_stream`` (MILNCE_SIDE_KEEP=1 / 2). With record_stream (the
+    default) a tensor freed under a cross-stream record stays unusable for the caching allocator
+    until its next event scan, so the reserved pool grows (bs 256: 93 GiB after 8 steps, 171 after
+    43, for 27 GiB allocated); kept references bound it (41 GiB reserved, 31.8 GiB allocated) but
+    measured ~0.8 % slower (same box, 40 steps: 4651 / 4630 and 4651 / 4659 vs 4694 / 4675)."""
+
+    def __init__(self):
+        self.q = collections.deque()
+        self.hooked = False
+
+    def add(self, event, tensors) -> None:
+        if not self.hooked:
+            grad_sink.after_drain(self.release)
+            self.hooked = True
+        self.q.append((event, tensors))
+        while self.q and self.q[0][0] is not None and self.q[0][0].query():
+            self.q.popleft()
+
+    def release(self) -> None:
+        self.q.clear()
+
+
+_SIDE_KEEP = _SideKeep()
+# 0 (default): record_stream; 1: operands released when their event completed or at the drain;
+# 2: only at the drain (no per-wgrad events)
+_KEEP_REFS = int(os.environ.get("MILNCE_SIDE_KEEP", "0"))
+
+
 def _reduce_on_side(slab: torch.Tensor, dw: torch.Tensor, splits: int, npad: int, kpad: int, plan: ConvPlan,
                     accumulate: int) -> None:
     main = torch.cuda.current_stream(slab.device)
@@ -1332,9 +1364,16 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 launch_split()
             else:
                 launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
-        for t in (dy, x, xss):
-            if t is not None:
-                t.record_stream(side)
+        if _KEEP_REFS:
+            kev = None
+            if _KEEP_REFS == 1:
+                kev = torch.cuda.Event()
+                kev.record(side)
+            _SIDE_KEEP.add(kev, (dy, x, xss))
+        else:
+            for t in (dy, x, xss):
+                if t is not None:
+                    t.record_stream(side)
         if batched:
             _REDUCER.add(slab, entries, dy.device)
         else:

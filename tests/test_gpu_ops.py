@@ -383,6 +383,56 @@ def test_conv1x1_group_matches_separate_units(widths):
         assert torch.allclose(bn.running_var, r.running_var, rtol=2e-2, atol=2e-3)
 
 
+@pytest.mark.parametrize("widths,cin", [((64, 96, 16), 192), ((112, 144, 32), 512)])
+def test_group_launch_merging_bitwise(widths, cin, monkeypatch):
+    """The fused 1x1 group's merged launches -- weights pre-packed from the member parameters,
+    one BN finalize per group in forward and backward, the wgrad on the side stream reduced into
+    each member's flat gradient, batched slab reductions -- are bitwise the per-member launches:
+    outputs, dX, weight / BN gradients accumulated in place over two steps, running stats."""
+    from mil_nce_howto100m_amd.ops import grad_sink
+    h = hip()
+    torch.manual_seed(17)
+    B, T, H, W = 4, 4, 9, 9
+    x = torch.randn(B, T, H, W, cin, device=DEV).to(torch.bfloat16)
+    convs0 = [nn.Conv3d(cin, c, 1, bias=False).to(DEV) for c in widths]
+    bns0 = [nn.BatchNorm3d(c).to(DEV) for c in widths]
+    with torch.no_grad():
+        for bn in bns0:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    dzs = [torch.randn(B, T, H, W, c, device=DEV).to(torch.bfloat16) for c in widths]
+    res = []
+    for merged in (True, False):
+        for flag in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT", "_REDUCE_BATCH"):
+            monkeypatch.setattr(h, flag, merged)
+        convs, bns = copy.deepcopy(convs0), copy.deepcopy(bns0)
+        params = [c.weight for c in convs] + [p for bn in bns for p in (bn.weight, bn.bias)]
+        for p in params:
+            p.grad = torch.zeros_like(p)
+            p._milnce_flat_grad = True  # direct in-place gradient writes, as under the bucketer
+        h._PACKER.entries.clear()
+        h._PACKER.descs = None
+        outs = []
+        for step in range(2):
+            h.zero_arena_begin(x.device)
+            try:
+                xh = x.clone().requires_grad_(True)
+                zs = h.conv1x1_group_bn_relu(xh, [c.weight for c in convs], bns, True, False)
+                zs = [h._materialize(z) if h._is_lazy(z) else z for z in zs]
+                torch.autograd.backward(list(zs), dzs)
+                grad_sink.drain()
+            finally:
+                h.zero_arena_end()
+            outs += [z.float() for z in zs] + [xh.grad.float()]
+        torch.cuda.synchronize()
+        res.append(outs + [p.grad.clone() for p in params] +
+                   [t.clone() for bn in bns for t in (bn.running_mean, bn.running_var)])
+    h._PACKER.entries.clear()
+    h._PACKER.descs = None
+    for a, b in zip(*res):
+        assert torch.equal(a, b), (a - b).abs().max().item()
+
+
 @pytest.mark.parametrize("kernel,stride,tf", [((1, 3, 3), (1, 2, 2), True), ((3, 3, 3), (2, 2, 2), True),
                                               ((2, 2, 2), (2, 2, 2), True), ((3, 3, 3), (1, 1, 1), False)])
 def test_maxpool(kernel, stride, tf):
