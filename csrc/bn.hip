@@ -146,7 +146,7 @@ __global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_group_kernel(FinG
 template <bool WRITE>
 __device__ __forceinline__ void bn_relu_apply_body(
     const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
-    int C, int rows_per_b, int rows_per_block, float* __restrict__ gsum) {
+    int C, int rows_per_b, int rows_per_block, float* __restrict__ part, float* __restrict__ gsum) {
   __shared__ float red[256 * 8];
   const int cpr = C >> 3;
   const int rpi = 256 / cpr;  // rows per iteration
@@ -192,27 +192,40 @@ __device__ __forceinline__ void bn_relu_apply_body(
 #pragma unroll
   for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
   __syncthreads();
-  // first row-group sums the others for its channel chunk
+  // first row-group sums the others for its channel chunk; one partial row per (split, clip) in
+  // part ([splits][B][C] scratch; bn_gsum_sum_kernel adds the splits in order), or -- inside a
+  // HIP graph capture, part == null -- float atomics into gsum
   if (rr == 0 && active) {
+    float* __restrict__ pr = part + ((long long)blockIdx.x * gridDim.y + b) * C + c0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float s = acc[k];
       for (int j = 1; j < rpi; ++j) s += red[k * 256 + j * cpr + cc];
-      atomicAdd(gsum + (long long)b * C + c0 + k, s);
+      if (part != nullptr) pr[k] = s;
+      else atomicAdd(gsum + (long long)b * C + c0 + k, s);
     }
+  }
+}
+
+// gsum[i] += sum over s < nsplit of part[s * n + i], in split order (deterministic gating sums)
+__global__ void bn_gsum_sum_kernel(float* __restrict__ gsum, const float* __restrict__ part, int nsplit, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = part[i];
+    for (int sp = 1; sp < nsplit; ++sp) v += part[(long long)sp * n + i];
+    gsum[i] += v;
   }
 }
 
 __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
     const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
-    int C, int rows_per_b, int rows_per_block, float* __restrict__ gsum) {
-  bn_relu_apply_body<true>(y, ldy, z, ldz, ss, C, rows_per_b, rows_per_block, gsum);
+    int C, int rows_per_b, int rows_per_block, float* __restrict__ part, float* __restrict__ gsum) {
+  bn_relu_apply_body<true>(y, ldy, z, ldz, ss, C, rows_per_b, rows_per_block, part, gsum);
 }
 
 __global__ __launch_bounds__(256) void bn_relu_gsum_kernel(
     const bf16_t* __restrict__ y, int ldy, const float* __restrict__ ss, int C, int rows_per_b,
-    int rows_per_block, float* __restrict__ gsum) {
-  bn_relu_apply_body<false>(y, ldy, nullptr, 0, ss, C, rows_per_b, rows_per_block, gsum);
+    int rows_per_block, float* __restrict__ part, float* __restrict__ gsum) {
+  bn_relu_apply_body<false>(y, ldy, nullptr, 0, ss, C, rows_per_b, rows_per_block, part, gsum);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -421,13 +434,22 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
   // enough blocks to fill 256 CUs instead of a couple of long serial blocks per CU.
   const int splits = pick_splits(rows_per_b, 4 * BN_U * (256 / (C / 8)));
   const int rpb = (rows_per_b + splits - 1) / splits;
+  // gating sums: per-(split, clip) partial rows in scratch, then added to gsum in split order
+  const long long n = (long long)B * C;
+  float* part = nullptr;  // stays null inside a graph capture: atomics into gsum
+  if (gsum != nullptr) part = stream_scratch((size_t)splits * n, stream, SCRATCH_BN_GSUM);
   if (z == nullptr) {  // gating sums only
     if (gsum == nullptr) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_relu_gsum_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy, ss, C,
-                       rows_per_b, rpb, gsum);
+                       rows_per_b, rpb, part, gsum);
   } else {
     hipLaunchKernelGGL(bn_relu_apply_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy,
-                       (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, gsum);
+                       (bf16_t*)z, ldz, ss, C, rows_per_b, rpb, part, gsum);
+  }
+  if (part != nullptr) {
+    const long long g = (n + 255) / 256;
+    hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, gsum, part,
+                       splits, n);
   }
   return (int)hipGetLastError();
 }
@@ -474,38 +496,6 @@ __global__ __launch_bounds__(256) void bn_part_prereduce_kernel(const float* __r
   }
 }
 
-// Scratch for the pre-reduced slabs, one growing buffer per stream (the BN backward runs on the
-// compute stream; a buffer is only reused in its stream's order).
-struct PreBuf {
-  hipStream_t stream;
-  int device;
-  float* buf;
-  size_t cap;
-};
-static PreBuf g_pre[16];
-static int g_npre = 0;
-
-static float* pre_scratch(size_t floats, hipStream_t stream) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  PreBuf* e = nullptr;
-  for (int i = 0; i < g_npre; ++i)
-    if (g_pre[i].stream == stream && g_pre[i].device == dev) e = &g_pre[i];
-  if (e == nullptr) {
-    if (g_npre == 16) return nullptr;
-    e = &g_pre[g_npre++];
-    *e = PreBuf{stream, dev, nullptr, 0};
-  }
-  if (e->cap < floats) {
-    if (e->buf != nullptr && (hipStreamSynchronize(stream) != hipSuccess || hipFree(e->buf) != hipSuccess)) return nullptr;
-    e->buf = nullptr;
-    e->cap = 0;
-    if (hipMalloc(&e->buf, floats * sizeof(float)) != hipSuccess) return nullptr;
-    e->cap = floats;
-  }
-  return e->buf;
-}
-
 // Pre-reduces one slab into dst (PRE_PARTS x 2 x ps floats) when it is large; updates part /
 // nparts to what the finalize should read.
 static void prereduce(const float*& part, int& nparts, int ps, int C, float* dst, hipStream_t stream) {
@@ -517,7 +507,7 @@ static void prereduce(const float*& part, int& nparts, int ps, int C, float* dst
 
 static void prereduce1(const float*& part, int& nparts, int ps, int C, hipStream_t stream) {
   if (nparts < PRE_MIN_PARTS) return;
-  prereduce(part, nparts, ps, C, pre_scratch((size_t)PRE_PARTS * 2 * ps, stream), stream);
+  prereduce(part, nparts, ps, C, stream_scratch((size_t)PRE_PARTS * 2 * ps, stream, SCRATCH_BN_PRE), stream);
 }
 
 MILNCE_API int milnce_bn_bwd(const void* dz, int ldz, const void* y, int ldy, const float* ss, int C, long long M,
@@ -572,7 +562,7 @@ MILNCE_API int milnce_bn_bwd_finalize_group(const void* members, int n, double c
   }
   g.n = n;
   if (need > 0) {  // each large member slab pre-reduced into its own region of the scratch
-    float* dst = pre_scratch(need, stream);
+    float* dst = stream_scratch(need, stream, SCRATCH_BN_PRE);
     for (int i = 0; i < n && dst != nullptr; ++i) {
       if (g.m[i].nparts < PRE_MIN_PARTS) continue;
       prereduce(g.m[i].part, g.m[i].nparts, g.m[i].ps, g.m[i].C, dst, stream);

@@ -137,6 +137,46 @@ __device__ __forceinline__ int xcd_remap(int id, int nblocks) {
 // outstanding global loads (vmcnt), so register prefetches stay in flight across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Host: device scratch (floats) for kernels that stage partial results between launches of ONE
+// API call -- one growing buffer per (purpose slot, stream, device), so reuse is ordered by the
+// stream. Growth synchronises that stream before freeing the old buffer. Per translation unit.
+// Returns null while the stream is being captured into a HIP graph (callers then fall back).
+enum ScratchSlot { SCRATCH_BN_PRE = 0, SCRATCH_BN_GSUM = 1, SCRATCH_GATE_GSUM = 2, SCRATCH_GATE_DG = 3,
+                   SCRATCH_GATE_DOT = 4, SCRATCH_SLOTS = 5 };
+static inline float* stream_scratch(size_t floats, hipStream_t stream, int slot) {
+  struct Buf {
+    hipStream_t stream;
+    int device, slot;
+    float* buf;
+    size_t cap;
+  };
+  static Buf bufs[64];
+  static int nbuf = 0;
+  // never inside a HIP graph capture: no allocation is allowed there, and a later growth would
+  // free memory a captured graph still references -- the callers fall back to atomics
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  Buf* e = nullptr;
+  for (int i = 0; i < nbuf; ++i)
+    if (bufs[i].stream == stream && bufs[i].device == dev && bufs[i].slot == slot) e = &bufs[i];
+  if (e == nullptr) {
+    if (nbuf == 64) return nullptr;
+    e = &bufs[nbuf++];
+    *e = Buf{stream, dev, slot, nullptr, 0};
+  }
+  if (e->cap < floats) {
+    if (e->buf != nullptr && (hipStreamSynchronize(stream) != hipSuccess || hipFree(e->buf) != hipSuccess))
+      return nullptr;
+    e->buf = nullptr;
+    e->cap = 0;
+    if (hipMalloc(&e->buf, floats * sizeof(float)) != hipSuccess) return nullptr;
+    e->cap = floats;
+  }
+  return e->buf;
+}
+
 #define HIP_RET(expr)                           \
   do {                                          \
     hipError_t _e = (expr);                     \

@@ -1739,7 +1739,7 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ws = (bf16_t*)smem;                      // [64][STF_LDW]
   bf16_t* X = Ws + 64 * STF_LDW;                   // [HALO][8]
-  float* red = (float*)(X + HALO * 8);             // [NPG][128] stats: one row per position group
+  float* red = (float*)X;  // [NPG][128] stats, one row per position group: reuses the halo after the last item
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1916,6 +1916,7 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
   }
   // statistics: reduce over the 16 lanes of a channel group, then over the position groups in a
   // fixed order (each group's partials in its own LDS row: deterministic, no LDS atomics)
+  __syncthreads();  // every wave is done reading the halo the rows overwrite
 #pragma unroll
   for (int nf = 0; nf < CW; ++nf)
 #pragma unroll
@@ -1941,7 +1942,8 @@ __global__ __launch_bounds__(64 * (4 / CW) * NPG, 1) void stem_fwd_kernel(StemFw
 template <int W2, bool U8, int HR, int NPG, int CW = 2>
 static int launch_stem_fwd_t(StemFwdParams& p, int grid, hipStream_t stream) {
   constexpr int HALO = 3 * (2 * HR + 5) * (W2 + 4);
-  constexpr size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16 + (size_t)NPG * 128 * 4;
+  constexpr size_t lds = (size_t)64 * STF_LDW * 2 + (size_t)HALO * 16;
+  static_assert((size_t)HALO * 16 >= (size_t)NPG * 128 * 4, "statistics rows reuse the halo");
   static_assert(lds <= 160 * 1024, "stem forward LDS");
   static bool attr_set = false;
   if (!attr_set) {

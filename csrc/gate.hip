@@ -35,16 +35,27 @@ __device__ __forceinline__ int seg_of(const SegTable& t, int c) {
 }
 
 // gsum/g/mean are [B, Ctot] fp32 (branch i at columns off[i]..off[i+1]).
-__global__ void gate_fc_kernel(SegTable t, const float* __restrict__ gsum, float inv_thw, int Ctot,
-                               float* __restrict__ mean, float* __restrict__ g) {
+// part != null: gsum[b, c] is first summed (in split order) from gate_gsum_kernel's nsplit partial
+// rows [nsplit][B][Ctot] and stored.
+__global__ void gate_fc_kernel(SegTable t, float* __restrict__ gsum, const float* __restrict__ part, int nsplit,
+                               int B, float inv_thw, int Ctot, float* __restrict__ mean, float* __restrict__ g) {
   const int b = blockIdx.x, s = blockIdx.y;
   if (s >= t.nseg) return;
   const int c0 = t.off[s], C = t.off[s + 1] - c0;
   extern __shared__ float m[];
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float v = gsum[(long long)b * Ctot + c0 + c] * inv_thw;
+    const long long o = (long long)b * Ctot + c0 + c;
+    float sum;
+    if (part != nullptr) {
+      sum = part[o];
+      for (int sp = 1; sp < nsplit; ++sp) sum += part[(long long)sp * B * Ctot + o];
+      gsum[o] = sum;
+    } else {
+      sum = gsum[o];
+    }
+    const float v = sum * inv_thw;
     m[c] = v;
-    mean[(long long)b * Ctot + c0 + c] = v;
+    mean[o] = v;
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -109,7 +120,7 @@ __global__ __launch_bounds__(256) void gate_scale_kernel(SegTable t, const float
 #endif
 constexpr int GS_U = MILNCE_GS_U;
 __global__ __launch_bounds__(256) void gate_gsum_kernel(SegTable t, int Ctot, int thw, int rows_per_block,
-                                                        float* __restrict__ gsum) {
+                                                        float* __restrict__ part, float* __restrict__ gsum) {
   __shared__ float red[256 * 8];
   const int cpr = Ctot >> 3, rpi = 256 / cpr, tid = threadIdx.x;
   const int cc = tid % cpr, rr = tid / cpr;
@@ -147,19 +158,25 @@ __global__ __launch_bounds__(256) void gate_gsum_kernel(SegTable t, int Ctot, in
   for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
   __syncthreads();
   if (rr == 0 && active) {
+    // one partial row per (split, clip): gate_fc_kernel sums the splits in a fixed order
+    // (float atomics made the sums -- and the whole step -- differ run to run; they remain the
+    // fallback inside a HIP graph capture, part == null)
+    float* __restrict__ pr = part + ((size_t)blockIdx.x * gridDim.y + b) * Ctot + c;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = acc[k];
       for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
-      atomicAdd(gsum + (size_t)b * Ctot + c + k, v);
+      if (part != nullptr) pr[k] = v;
+      else atomicAdd(gsum + (size_t)b * Ctot + c + k, v);
     }
   }
 }
 
-// dg[b, c] += sum over this block's rows of dout[r, c] * z[r, c]   (grid: splits x B)
+// part[split][b][c] = sum over this block's rows of dout[r, c] * z[r, c]   (grid: splits x B); the
+// caller's next kernel sums the splits in a fixed order (deterministic, unlike float atomics)
 __global__ __launch_bounds__(256) void gate_bwd_reduce_kernel(SegTable t, const bf16_t* __restrict__ dout,
                                                               int Ctot, int thw, int rows_per_block,
-                                                              float* __restrict__ dg) {
+                                                              float* __restrict__ part, float* __restrict__ dg) {
   __shared__ float red[256 * 8];
   const int cpr = Ctot >> 3;
   const int tid = threadIdx.x;
@@ -191,20 +208,35 @@ __global__ __launch_bounds__(256) void gate_bwd_reduce_kernel(SegTable t, const 
   for (int k = 0; k < 8; ++k) red[k * 256 + tid] = acc[k];
   __syncthreads();
   if (active && rr == 0) {
+    float* __restrict__ pr = part + ((long long)blockIdx.x * gridDim.y + b) * Ctot + c;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       float v = acc[k];
       for (int j = 1; j < groups; ++j) v += red[k * 256 + j * cpr + cc];
-      atomicAdd(dg + (long long)b * Ctot + c + k, v);
+      if (part != nullptr) pr[k] = v;
+      else atomicAdd(dg + (long long)b * Ctot + c + k, v);  // graph-capture fallback
     }
   }
 }
 
-// dpre = dg * g * (1 - g), in place (all segments at once: [B, Ctot])
-__global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict__ g, long long n) {
+// dst[i] += sum over s < nsplit of part[s * n + i], in split order
+__global__ void split_sum_kernel(float* __restrict__ dst, const float* __restrict__ part, int nsplit, long long n) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = part[i];
+    for (int sp = 1; sp < nsplit; ++sp) v += part[(long long)sp * n + i];
+    dst[i] += v;
+  }
+}
+
+// dpre = (dg + sum of the reduce's split rows, in split order) * g * (1 - g), in place (all segments
+// at once: [B, Ctot])
+__global__ void gate_dpre_kernel(float* __restrict__ dg, const float* __restrict__ part, int nsplit,
+                                 const float* __restrict__ g, long long n) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;  // nsplit 0: the reduce added into dg itself
+    for (int sp = 0; sp < nsplit; ++sp) v += part[(long long)sp * n + i];
     const float gg = g[i];
-    dg[i] = dg[i] * gg * (1.f - gg);
+    dg[i] = (dg[i] + v) * gg * (1.f - gg);
   }
 }
 
@@ -499,7 +531,7 @@ static int grid_for(long long n) {
 
 // lazy (may be null): per-branch flag; a lazy branch's z is read as relu(bn_y * scale + shift)
 // from (bn_y[i], bn_ld[i], bn_ss[i]) instead of z[i].
-// gsum_pass != 0: gsum (zeroed by the caller) is first filled by ONE gate_gsum_kernel pass over
+// gsum_pass != 0: gsum (zeroed by the caller) is first computed by ONE gate_gsum_kernel pass over
 // every branch's raw conv output (all branches must be lazy).
 MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z, const float* const* w,
                                const float* const* bias, float* gsum, int B, int thw, float* mean, float* g,
@@ -515,6 +547,8 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
     }
   }
   const int Ctot = t.off[nseg];
+  float* gpart = nullptr;  // gsum_pass: the gsum kernel's partial rows
+  int nsplit = 0;
   if (gsum_pass) {
     for (int i = 0; i < nseg; ++i)
       if (lazy == nullptr || !lazy[i]) return (int)hipErrorInvalidValue;
@@ -526,12 +560,14 @@ MILNCE_API int milnce_gate_fwd(int nseg, const int* widths, const void* const* z
     if (splits > smax) splits = smax;
     if (splits < 1) splits = 1;
     const int rpb = (thw + splits - 1) / splits;
-    hipLaunchKernelGGL(gate_gsum_kernel, dim3(splits, B), dim3(256), 0, stream, t, Ctot, thw, rpb, gsum);
+    gpart = stream_scratch((size_t)splits * B * Ctot, stream, SCRATCH_GATE_GSUM);  // null: atomics into gsum
+    nsplit = gpart != nullptr ? splits : 0;
+    hipLaunchKernelGGL(gate_gsum_kernel, dim3(splits, B), dim3(256), 0, stream, t, Ctot, thw, rpb, gpart, gsum);
   }
   int cmax = 0;
   for (int i = 0; i < nseg; ++i) cmax = widths[i] > cmax ? widths[i] : cmax;
-  hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum,
-                     1.f / thw, Ctot, mean, g);
+  hipLaunchKernelGGL(gate_fc_kernel, dim3(B, nseg), dim3(256), cmax * sizeof(float), stream, t, gsum, gpart,
+                     nsplit, B, 1.f / thw, Ctot, mean, g);
   if (out == nullptr) return (int)hipGetLastError();  // gate values only: a fused consumer applies them
   if (Ctot % 8 || Ctot > 2048) return (int)hipErrorInvalidValue;
   const int rpi = 256 / (Ctot / 8);
@@ -550,10 +586,12 @@ MILNCE_API int milnce_gate_bwd_reduce(int nseg, const int* widths, const void* c
   const int Ctot = t.off[nseg];
   const int splits = (thw + 511) / 512;
   const int rpb = (thw + splits - 1) / splits;
-  hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, Ctot,
-                     thw, rpb, dpre);
   const long long n = (long long)B * Ctot;
-  hipLaunchKernelGGL(gate_dpre_kernel, dim3(grid_for(n)), dim3(256), 0, stream, dpre, g, n);
+  float* part = stream_scratch((size_t)splits * n, stream, SCRATCH_GATE_DG);  // null: atomics into dpre
+  hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)dout, Ctot,
+                     thw, rpb, part, dpre);
+  hipLaunchKernelGGL(gate_dpre_kernel, dim3(grid_for(n)), dim3(256), 0, stream, dpre, part,
+                     part != nullptr ? splits : 0, g, n);
   return (int)hipGetLastError();
 }
 
@@ -615,8 +653,12 @@ MILNCE_API int milnce_gate_dot(const void* a, const void* v, int B, int rows_per
   SegTable t = make_table(1, widths, zs, nullptr, nullptr, nullptr, nullptr, nullptr);
   const int splits = (rows_per_b + 511) / 512;
   const int rpb = (rows_per_b + splits - 1) / splits;
+  const long long n = (long long)B * C;
+  float* part = stream_scratch((size_t)splits * n, stream, SCRATCH_GATE_DOT);  // null: atomics into gs
   hipLaunchKernelGGL(gate_bwd_reduce_kernel, dim3(splits, B), dim3(256), 0, stream, t, (const bf16_t*)a, C,
-                     rows_per_b, rpb, gs);
+                     rows_per_b, rpb, part, gs);
+  if (part != nullptr)
+    hipLaunchKernelGGL(split_sum_kernel, dim3(grid_for(n)), dim3(256), 0, stream, gs, part, splits, n);
   return (int)hipGetLastError();
 }
 

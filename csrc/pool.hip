@@ -1185,15 +1185,24 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
     acur = anext;
   }
   if (gs == nullptr) return;
+  // the gate reduction over the plane's rows: a fixed-order LDS tree (LDS float atomics summed the
+  // rows in arrival order, so the sums differed from run to run)
   __syncthreads();
-  float* red = (float*)s1_lds;  // G*8 floats
-  for (int i = threadIdx.x; i < G * 8; i += blockDim.x) red[i] = 0.f;
-  __syncthreads();
-  if (s.active) {
+  float* red = (float*)s1_lds;  // [rows][G][8] (fits: the sweep staged more than this per row)
+  if (s.r < s.rows) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(&red[s.g * 8 + k], sacc[k]);
+    for (int k = 0; k < 8; ++k) red[(s.r * G + s.g) * 8 + k] = s.active ? sacc[k] : 0.f;
   }
   __syncthreads();
+  int half = 1;
+  while (half < s.rows) half <<= 1;
+  for (half >>= 1; half >= 1; half >>= 1) {
+    if (s.r < half && s.r + half < s.rows) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[(s.r * G + s.g) * 8 + k] += red[((s.r + half) * G + s.g) * 8 + k];
+    }
+    __syncthreads();
+  }
   for (int i = threadIdx.x; i < G * 8; i += blockDim.x) {
     const int c = s.chunk * G * 8 + i;
     if (c < p.C) gs[(size_t)s.b * p.C + c] = red[i];

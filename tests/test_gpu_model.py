@@ -92,6 +92,66 @@ def test_direct_gradient_writes_match_autograd_accumulation():
     assert torch.allclose(flats[0], flats[1], rtol=1e-5, atol=1e-6)
 
 
+def _two_train_steps(args, ctx, data, monkeypatch, flags):
+    from mil_nce_howto100m_amd.ops import grad_sink
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+    for flag, val in flags.items():
+        monkeypatch.setattr(h, flag, val)
+    seed_everything(1, 0)
+    tr = Trainer(args, build_model(args, ctx.device), ctx, 10)
+    for p in tr.bucketer.params:
+        p._milnce_flat_grad = True
+    tr.model.train()
+    for step in range(2):
+        tr.bucketer.zero()
+        h.zero_arena_begin(ctx.device)
+        try:
+            tr.forward_loss(data.batch(step)).backward()
+        finally:
+            h.zero_arena_end()
+        grad_sink.drain()
+    torch.cuda.synchronize()
+    out = {n: p.grad.clone() for n, p in tr.model.named_parameters() if p.grad is not None}
+    out.update({"buffer:" + n: t.clone().float() for n, t in tr.model.named_buffers()})
+    return out
+
+
+def _assert_same(a, b):
+    """Bitwise, except the SelfGating fc gradients of a block followed by a max pool: the pool's
+    gather backward takes that gate's reduction with float atomics per clip (~1e-8 apart)."""
+    assert a.keys() == b.keys()
+    for n in a:
+        if ".gating" in n and torch.allclose(a[n], b[n], rtol=1e-5, atol=1e-7):
+            continue
+        assert torch.equal(a[n], b[n]), (n, (a[n] - b[n]).abs().max().item())
+
+
+@pytest.mark.parametrize("merged", [True, False])
+def test_train_step_bitwise_reproducible(merged, monkeypatch):
+    """Two identical train-mode runs of the gated model (stem, 3 Inception blocks, text tower,
+    MIL-NCE) give bitwise the same parameter gradients and BN running statistics: the
+    cross-workgroup sums are taken in a fixed order (SelfGating sums, gate-backward dots, the
+    stride-1 pool's gate reductions, stem BN statistics: partial rows summed in order, no float
+    atomics); only the gate fc gradients of a block feeding a stride-2 max pool keep a float-atomic
+    reduction (see _assert_same). With that, the fused 1x1 group's merged launches (member
+    pre-pack, one finalize per group, side-stream wgrad into each member's flat gradient, batched
+    slab reductions) must equal the per-member launches bitwise, too."""
+    from mil_nce_howto100m_amd.config import get_args
+    from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
+    from mil_nce_howto100m_amd.parallel import dist as pdist
+    args = get_args(argv=["--batch_size", "4", "--num_frames", "8", "--video_size", "64", "--num_candidates", "2",
+                          "--blocks", "mixed_3b,mixed_3c,mixed_4b", "--word2vec_path", "", "--vocab_size", "1000"])
+    ctx = pdist.DistContext(device=torch.device("cuda", 0))
+    data = SyntheticClips(4, 8, 64, 2, 20, 1000, device=ctx.device)
+    flags = {f: merged for f in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT", "_REDUCE_BATCH")}
+    a = _two_train_steps(args, ctx, data, monkeypatch, flags)
+    b = _two_train_steps(args, ctx, data, monkeypatch, flags)
+    _assert_same(a, b)
+    if merged:
+        _assert_same(a, _two_train_steps(args, ctx, data, monkeypatch, {f: False for f in flags}))
+
+
 def test_hip_graph_eval_forward_matches_eager():
     """Eval forward replayed from a captured HIP graph == eager, across replays with new inputs."""
     import time
