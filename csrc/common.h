@@ -142,7 +142,7 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // stream. Growth synchronises that stream before freeing the old buffer. Per translation unit.
 // Returns null while the stream is being captured into a HIP graph (callers then fall back).
 enum ScratchSlot { SCRATCH_BN_PRE = 0, SCRATCH_BN_GSUM = 1, SCRATCH_GATE_GSUM = 2, SCRATCH_GATE_DG = 3,
-                   SCRATCH_GATE_DOT = 4, SCRATCH_SLOTS = 5 };
+                   SCRATCH_GATE_DOT = 4, SCRATCH_POOL_GS = 5, SCRATCH_SLOTS = 6 };
 static inline float* stream_scratch(size_t floats, hipStream_t stream, int slot) {
   struct Buf {
     hipStream_t stream;

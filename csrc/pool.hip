@@ -586,7 +586,8 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
                                                      float* __restrict__ gs = nullptr,
                                                      const float* __restrict__ gate_g = nullptr,
                                                      const float* __restrict__ gate_dm = nullptr,
-                                                     float inv_thw = 0.f, const float* __restrict__ coef = nullptr) {
+                                                     float inv_thw = 0.f, const float* __restrict__ coef = nullptr,
+                                                     float* __restrict__ gpart = nullptr) {
   __shared__ float red[16 * 256];
   const int cpr = p.C >> 3, rpi = 256 / cpr;
   const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
@@ -599,16 +600,27 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
   if (bn && active) acc_bn.load(bn_ss, p.C, c0);
   const uint32_t pos_begin = blockIdx.x * pos_per_block;
   const uint32_t pos_end = min(npos, pos_begin + pos_per_block);
-  // gate reduction of the pool input's producer (SelfGating): gs[b, c] += sum dx * gx, flushed
-  // with one atomic per channel whenever the thread's clip changes
-  float sacc[8];
-  uint32_t cur_b = 0xffffffffu;
+  // gate reduction of the pool input's producer (SelfGating): gs[b, c] += sum dx * gx. With gpart
+  // (a block's items span at most two clips): the thread keeps its first clip's sum aside at the
+  // clip change and the block writes one partial row per clip slot at the end, summed over the
+  // blocks in order by pool_gs_sum_kernel (deterministic); without: one atomic per channel
+  // whenever the thread's clip changes.
+  float sacc[8], sprev[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sprev[k] = 0.f;
+  uint32_t cur_b = 0xffffffffu, prev_b = 0xffffffffu;
   auto gs_add = [&](uint32_t ps, const uint4& v, const uint4& xg) {
     const uint32_t bb = fdiv(ps, d.fplane);
     if (bb != cur_b) {
       if (cur_b != 0xffffffffu) {
+        if (gpart != nullptr && prev_b == 0xffffffffu) {
+          prev_b = cur_b;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
+          for (int k = 0; k < 8; ++k) sprev[k] = sacc[k];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) sacc[k] = 0.f;
@@ -756,11 +768,60 @@ __global__ __launch_bounds__(256) void maxpool_bwd_t(PoolParams p, PoolDivs d, c
       if (two) *(uint4*)(dx + (size_t)pos2 * p.C + c0) = v1;
     }
   }
-  if (MODE == POOL_BWD_PLAIN && gs != nullptr && cur_b != 0xffffffffu) {
+  if (MODE == POOL_BWD_PLAIN && gs != nullptr && gpart == nullptr && cur_b != 0xffffffffu) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) unsafeAtomicAdd(gs + (size_t)cur_b * p.C + c0 + k, sacc[k]);
   }
+  if (MODE == POOL_BWD_PLAIN && gs != nullptr && gpart != nullptr) {
+    __shared__ uint32_t bfirst;
+    if (threadIdx.x == 0) bfirst = 0xffffffffu;
+    __syncthreads();
+    const uint32_t mine = prev_b != 0xffffffffu ? prev_b : cur_b;
+    if (mine != 0xffffffffu) atomicMin(&bfirst, mine);  // integer min: order-independent
+    __syncthreads();
+    const uint32_t b0 = bfirst;
+    const bool some = b0 != 0xffffffffu;
+    const bool p0 = some && prev_b == b0, p1 = some && prev_b != 0xffffffffu && prev_b == b0 + 1;
+    const bool c0v = some && cur_b == b0, c1v = some && cur_b != 0xffffffffu && cur_b == b0 + 1;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[k * 256 + threadIdx.x] = (p0 ? sprev[k] : 0.f) + (c0v ? sacc[k] : 0.f);
+      red[(8 + k) * 256 + threadIdx.x] = (p1 ? sprev[k] : 0.f) + (c1v ? sacc[k] : 0.f);
+    }
+    __syncthreads();
+    if (active && rr == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float s0 = 0.f, s1 = 0.f;
+        for (int j = 0; j < rpi; ++j) { s0 += red[k * 256 + j * cpr + cc]; s1 += red[(8 + k) * 256 + j * cpr + cc]; }
+        gpart[((size_t)blockIdx.x * 2) * p.C + c0 + k] = s0;
+        gpart[((size_t)blockIdx.x * 2 + 1) * p.C + c0 + k] = s1;
+      }
+    }
+    if (threadIdx.x == 0) gpart[(size_t)gridDim.x * 2 * p.C + blockIdx.x] = b0 == 0xffffffffu ? -1.f : (float)b0;
+    __syncthreads();  // red is reused by the BN partial commit
+  }
   if (bn) acc_bn.commit(red, part, p.C, cpr, rpi, cc, rr, active);
+}
+
+// gs[b, c] += the pool blocks' partial rows of clip b (slot b - first clip of the block), in block
+// order. gpart: [nblk][2][C] rows, then nblk first-clip indices (as float, -1: empty block).
+__global__ void pool_gs_sum_kernel(float* __restrict__ gs, const float* __restrict__ gpart, int nblk, int B, int C,
+                                   long long ipc, long long ipb) {
+  const long long n = (long long)B * C;
+  const float* __restrict__ bfirst = gpart + (size_t)nblk * 2 * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / C, c = i - b * C;
+    const long long lo = b * ipc / ipb, hi = min((long long)nblk - 1, ((b + 1) * ipc - 1) / ipb);
+    float v = 0.f;
+    for (long long blk = lo; blk <= hi; ++blk) {
+      const float f = bfirst[blk];
+      if (f < 0.f) continue;
+      const long long slot = b - (long long)f;
+      if (slot == 0 || slot == 1) v += gpart[((size_t)blk * 2 + slot) * C + c];
+    }
+    gs[i] += v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1416,6 +1477,27 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   if (mode == POOL_BWD_APPLY && part == nullptr) nparts = pool_apply_grid();  // grid only: no partial rows
   const uint32_t npos = (uint32_t)(n / (p.C / 8));
   const uint32_t ppb = (npos + nparts - 1) / nparts;
+  // deterministic gate reduction (gs): per-block partial rows when a block's items span at most two
+  // clips (items per block <= items per clip), summed in block order after the pass
+  const long long nclip = (long long)npos / ((long long)p.T * p.H * p.W);
+  float* gpart = nullptr;
+  long long g_ipc = 0, g_ipb = 0;
+  auto gs_prep = [&](long long items, long long ipb) {
+    gpart = nullptr;
+    if (gs == nullptr || mode != POOL_BWD_PLAIN || nclip < 1) return;
+    const long long ipc = items / nclip;
+    if (ipb > ipc) return;  // atomics
+    g_ipc = ipc;
+    g_ipb = ipb;
+    gpart = stream_scratch((size_t)nparts * 2 * p.C + nparts, s, SCRATCH_POOL_GS);
+  };
+  auto gs_post = [&]() {
+    if (gpart == nullptr) return;
+    const long long nn = nclip * p.C;
+    const long long g = (nn + 255) / 256;
+    hipLaunchKernelGGL(pool_gs_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, s, gs, gpart, nparts,
+                       (int)nclip, p.C, g_ipc, g_ipb);
+  };
   const bool blk133 = p.kt == 1 && p.kh == 3 && p.kw == 3 && p.st == 1 && p.sh == 2 && p.sw == 2 && p.pt == 0 &&
                       p.To == p.T && p.ph <= 1 && p.pw <= 1;
   const bool blk333 = p.kt == 3 && p.kh == 3 && p.kw == 3 && p.st == 2 && p.sh == 2 && p.sw == 2 && p.pt <= 1 &&
@@ -1425,18 +1507,21 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
     const uint32_t nq = nb * d.fmt.d * d.fmh.d * d.fmw.d, qpb = (nq + nparts - 1) / nparts;
     // an even H, W plane without leading padding takes the leaner quad indexing (pool_bwd_quad)
     const bool even = blk133 && p.ph == 0 && p.pw == 0 && p.H == 2 * p.Ho && p.W == 2 * p.Wo;
+    gs_prep(nq, qpb);
 #define XQ(a, m)                                                                                                 \
     if (mode == m && even) {                                                                                     \
       hipLaunchKernelGGL((maxpool_bwd_t<1, 3, 3, 1, 2, 2, m, 1>), dim3(nparts), dim3(256), 0, s, p, d,           \
                          (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, nq, qpb, (const bf16_t*)bn_y,     \
-                         bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef);             \
+                         bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef, gpart);      \
+      gs_post();                                                                                                 \
       return true;                                                                                               \
     }                                                                                                            \
     if (mode == m) {                                                                                             \
       hipLaunchKernelGGL((maxpool_bwd_t<a, 3, 3, a == 3 ? 2 : 1, 2, 2, m, 2>), dim3(nparts), dim3(256), 0, s,    \
                          p, d, (const bf16_t*)dy, (const uint8_t*)arg, (bf16_t*)dx, nq, qpb,                     \
                          (const bf16_t*)bn_y, bn_ld, bn_ss, part, (const bf16_t*)gx, gs, gate_g, gate_dm,        \
-                         inv_thw, coef);                                                                         \
+                         inv_thw, coef, gpart);                                                                  \
+      gs_post();                                                                                                 \
       return true;                                                                                               \
     }
     if (blk133) {
@@ -1446,11 +1531,13 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
     }
 #undef XQ
   }
+  gs_prep(npos, ppb);
 #define XM(a, b, c, e, f, h, m)                                                                                  \
   if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h && mode == m) {                 \
     hipLaunchKernelGGL((maxpool_bwd_t<a, b, c, e, f, h, m>), dim3(nparts), dim3(256), 0, s, p, d, (const bf16_t*)dy, \
                        (const uint8_t*)arg, (bf16_t*)dx, npos, ppb, (const bf16_t*)bn_y, bn_ld, bn_ss, part,     \
-                       (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef);                                                                    \
+                       (const bf16_t*)gx, gs, gate_g, gate_dm, inv_thw, coef, gpart);                            \
+    gs_post();                                                                                                   \
     return true;                                                                                                 \
   }
 #define X(a, b, c, e, f, h) XM(a, b, c, e, f, h, POOL_BWD_PLAIN) XM(a, b, c, e, f, h, POOL_BWD_GATED) \
