@@ -87,3 +87,70 @@ def test_forward_tuner_pairs_variants_with_grid_sizes(monkeypatch):
     seen.clear()
     impl, grid = h._tune_fwd(lambda i, g: seen.append((i, g)), (3, 4), M, npad, bn, max_rows=2 * h._NUM_CU)
     assert {g for _, g in seen} == {2 * h._NUM_CU} and grid == 2 * h._NUM_CU
+
+
+class _FakeEvent:
+    def __init__(self, *a, **k):
+        self.recorded = None
+
+    def record(self, stream=None):
+        self.recorded = stream
+
+    def query(self):
+        return True
+
+
+class _FakeStream:
+    cuda_stream = 0
+
+
+def test_reduce_batcher_one_launch_per_batch_and_no_double_target(monkeypatch):
+    """The side stream's split-K reductions queue up and go out as one launch (flushed by the next
+    drain, or when 16 are pending), never with two accumulations into the same gradient in one
+    launch (those would race), and every flush registers its completion event with grad_sink."""
+    calls = []
+    monkeypatch.setattr(h, "call", lambda name, *a: calls.append((name, a[1])))
+    monkeypatch.setattr(h, "_side_stream", lambda dev: _FakeStream())
+    monkeypatch.setattr(h.torch.cuda, "Event", _FakeEvent)
+    monkeypatch.setattr(grad_sink, "_PENDING", [])
+    monkeypatch.setattr(grad_sink, "_ON_DRAIN", [])
+    waited = []
+    monkeypatch.setattr(grad_sink, "drain", lambda: (list(map(lambda f: f(), list(grad_sink._ON_DRAIN))),
+                                                     waited.append(len(grad_sink._PENDING))))
+    rb = h._ReduceBatcher()
+    item = lambda grad: (1000, grad, 4, 64, 576, 64, 64, 64, 9)  # noqa: E731
+    rb.add(object(), [item(1), item(2)], "cuda:0")
+    rb.add(object(), [item(3)], "cuda:0")
+    assert calls == [] and len(rb.items) == 3
+    rb.add(object(), [item(2)], "cuda:0")  # gradient 2 again: the pending batch goes out first
+    assert calls == [("milnce_wgrad_reduce_batch", 3)] and len(rb.items) == 1
+    assert len(grad_sink._PENDING) == 1
+    for g in range(10, 25):  # 1 + 15 = 16 pending -> flush without a drain
+        rb.add(object(), [item(g)], "cuda:0")
+    assert calls[-1] == ("milnce_wgrad_reduce_batch", 16) and rb.items == []
+    rb.add(object(), [item(99)], "cuda:0")
+    rb.flush()
+    assert calls[-1] == ("milnce_wgrad_reduce_batch", 1) and rb.items == [] and rb.slabs == []
+
+
+def test_side_keep_releases_after_completion_or_drain(monkeypatch):
+    monkeypatch.setattr(grad_sink, "_AFTER_DRAIN", [])
+    monkeypatch.setattr(grad_sink, "_ON_DRAIN", [])
+    monkeypatch.setattr(grad_sink, "_PENDING", [])
+
+    class Ev:
+        def __init__(self, done):
+            self.done = done
+
+        def query(self):
+            return self.done
+
+    keep = h._SideKeep()
+    keep.add(Ev(False), ("a",))
+    keep.add(Ev(True), ("b",))
+    assert len(keep.q) == 2  # the head is still running: nothing behind it is released either
+    keep.q[0] = (Ev(True), ("a",))
+    keep.add(None, ("c",))  # drain-only entry (no event)
+    assert [t for _, t in keep.q] == [("c",)]
+    grad_sink.drain()  # after the wait: everything goes
+    assert len(keep.q) == 0
