@@ -61,5 +61,15 @@ def drain() -> None:
         fn()
 
 
+def join(stream) -> None:
+    """Make ``stream`` (not the current one) wait for every deferred gradient write so far: a
+    bucket all-reduce issued from it sees complete gradients while the compute stream keeps going.
+    The writes stay pending for the next ``drain``."""
+    while _ON_DRAIN:
+        _ON_DRAIN.pop(0)()
+    for e in _PENDING:
+        stream.wait_event(e)
+
+
 def pending() -> int:
     return len(_PENDING) + len(_ON_DRAIN)

@@ -84,6 +84,7 @@ class GradBucketer:
         self._ready: set = set()
         self._handles: List[Optional[object]] = [None] * len(self.buckets)
         self.sync_enabled = True  # False: accumulate only (micro-batches before the last)
+        self._issue = None  # stream the bucket all-reduces are issued from (GPU)
         self._hooks = []
         if world_size > 1:
             for p in self.params:
@@ -104,6 +105,22 @@ class GradBucketer:
         self._handles = [None] * len(self.buckets)
 
     def _launch(self, b: int) -> None:
+        if self.flat.is_cuda:
+            # issued from a stream that waits for the compute stream's work so far AND for the
+            # side stream's deferred gradient writes (grad_sink.join), so the compute stream is not
+            # made to wait for the side stream at every bucket
+            from ..ops import grad_sink
+            main = torch.cuda.current_stream(self.flat.device)
+            if self._issue is None:
+                self._issue = torch.cuda.Stream(device=self.flat.device)
+            self._issue.wait_stream(main)
+            grad_sink.join(self._issue)
+            with torch.cuda.stream(self._issue):
+                self._launch_on_current(b)
+        else:
+            self._launch_on_current(b)
+
+    def _launch_on_current(self, b: int) -> None:
         s, e = self.buckets[b]
         buf = self.flat[s:e]
         if self.verify:  # reduce a private copy; keep another to check the slice against later
@@ -127,9 +144,7 @@ class GradBucketer:
         b = self.bucket_of[id(p)]
         self._pending[b] -= 1
         if self._pending[b] == 0 and self._handles[b] is None:
-            from ..ops import grad_sink
-            grad_sink.drain()  # gradients still being reduced on a side stream land first
-            self._launch(b)
+            self._launch(b)  # after the side stream's pending gradient writes (see _launch)
 
     def set_sync(self, enabled: bool) -> None:
         """Gradient accumulation: with sync off, backward passes only accumulate into the flat
@@ -152,6 +167,10 @@ class GradBucketer:
                 self._launch(b)
         for h in self._handles:
             h.wait()
+        if self.flat.is_cuda:  # wire / verify copies made on the issue stream, read here on this one
+            cur = torch.cuda.current_stream(self.flat.device)
+            for t in list(self._comm.values()) + list(self._snap.values()):
+                t.record_stream(cur)
         if self.comm_dtype != torch.float32 and not self.verify:
             for b, (s, e) in enumerate(self.buckets):
                 self.flat[s:e].copy_(self._comm[b])

@@ -22,7 +22,18 @@ class BucketRecorder:
         def launch(i):
             s, e = self.b.buckets[i]
             assert i not in self.snaps, f"bucket {i} issued twice"
-            self.snaps[i] = self.b.flat[s:e].clone()
+            if self.b.flat.is_cuda:
+                # what the bucket's all-reduce reads: the bucketer issues it from a stream that
+                # waits for the compute stream and the side stream's deferred writes (grad_sink.join)
+                from mil_nce_howto100m_amd.ops import grad_sink
+                st = torch.cuda.Stream(device=self.b.flat.device)
+                st.wait_stream(torch.cuda.current_stream(self.b.flat.device))
+                grad_sink.join(st)
+                with torch.cuda.stream(st):
+                    self.snaps[i] = self.b.flat[s:e].clone()
+                torch.cuda.current_stream(self.b.flat.device).wait_stream(st)
+            else:
+                self.snaps[i] = self.b.flat[s:e].clone()
             if self._in_finish:
                 self.issued_in_finish.append(i)
             orig_launch(i)
