@@ -190,17 +190,48 @@ class GradBucketer:
 
 
 class BufferBroadcaster:
-    """Broadcast module buffers (BN running stats, counters) from rank 0 each step."""
+    """Broadcast module buffers (BN running stats, counters) from rank 0 each step.
+
+    At N > 1 the buffers are re-pointed once into one flat tensor per dtype (views, like the
+    optimizer's flat parameters; the BN kernels update them in place and checkpoint loads copy
+    into them), so each step's broadcast is one collective per dtype with no pack / unpack: a
+    coalesced broadcast of the ~300 separate S3D-G buffers re-copies every one of them (one small
+    copy launch each) on every step."""
 
     def __init__(self, module: torch.nn.Module, world_size: int, bucket_bytes: int = 32 << 20):
-        self.bufs = [b for b in module.buffers()]
         self.world_size = world_size
         self.bucket_bytes = bucket_bytes
+        self.bufs = [b for b in module.buffers()]
+        self.flats: List[torch.Tensor] = []
+        if world_size > 1 and self.bufs:
+            self._flatten(module)
+
+    def _flatten(self, module: torch.nn.Module) -> None:
+        owners = [(m, name, b) for m in module.modules() for name, b in m._buffers.items() if b is not None]
+        by_dtype: Dict[torch.dtype, list] = {}
+        for m, name, b in owners:
+            by_dtype.setdefault((b.dtype, b.device), []).append((m, name, b))
+        for (dtype, device), items in by_dtype.items():
+            total = sum(b.numel() for _, _, b in items)
+            flat = torch.empty(total, dtype=dtype, device=device)
+            off = 0
+            for m, name, b in items:
+                n = b.numel()
+                view = flat[off:off + n].view_as(b)
+                view.copy_(b)
+                m._buffers[name] = view
+                off += n
+            self.flats.append(flat)
+        self.bufs = [b for b in module.buffers()]
 
     def __call__(self) -> None:
         if self.world_size <= 1 or not self.bufs:
             return
-        dist._broadcast_coalesced(dist.group.WORLD, self.bufs, self.bucket_bytes, 0)
+        if self.flats:
+            for f in self.flats:
+                dist.broadcast(f, 0)
+        else:
+            dist._broadcast_coalesced(dist.group.WORLD, self.bufs, self.bucket_bytes, 0)
 
 
 def broadcast_parameters(module: torch.nn.Module, world_size: int) -> None:
