@@ -1145,13 +1145,34 @@ _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 
 
 
-def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+# wgrads round-robin over this many side streams (A/B knob; the batched reductions run on the
+# first, after it waited for the others)
+_N_SIDE = max(1, int(os.environ.get("MILNCE_SIDE_STREAMS", "1")))
+_SIDE_RR: Dict[int, int] = {}
+
+
+def _side_streams(device: torch.device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _SIDE_STREAMS.get(idx)
-    if s is None:
-        s = torch.cuda.Stream(device=idx)
-        _SIDE_STREAMS[idx] = s
-    return s
+    ss = _SIDE_STREAMS.get(idx)
+    if ss is None:
+        ss = _SIDE_STREAMS[idx] = [torch.cuda.Stream(device=idx) for _ in range(_N_SIDE)]
+    return ss
+
+
+def _side_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The (first) side stream: reductions, joins."""
+    return _side_streams(device)[0]
+
+
+def _wgrad_stream(device: torch.device) -> "torch.cuda.Stream":
+    """The side stream of the next weight gradient (round-robin when MILNCE_SIDE_STREAMS > 1)."""
+    ss = _side_streams(device)
+    if len(ss) == 1:
+        return ss[0]
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    k = _SIDE_RR.get(idx, 0)
+    _SIDE_RR[idx] = k + 1
+    return ss[k % len(ss)]
 
 
 class _ReduceDesc(ctypes.Structure):
@@ -1196,11 +1217,17 @@ class _ReduceBatcher:
     def flush(self) -> None:
         if not self.items:
             return
-        side = _side_stream(self.device)
+        ss = _side_streams(self.device)
+        side = ss[0]
+        for other in ss[1:]:  # slabs written on any side stream
+            side.wait_stream(other)
         arr = (_ReduceDesc * len(self.items))()
         for i, (sptr, gptr, splits, npad, kpad, rows, cin, cin_p, taps) in enumerate(self.items):
             arr[i] = _ReduceDesc(sptr, gptr, splits, npad, kpad, rows, cin, cin_p, taps, 1, 0, 0)
         call("milnce_wgrad_reduce_batch", ctypes.addressof(arr), len(self.items), side.cuda_stream)
+        if len(ss) > 1:  # slabs of the other side streams were read here, on the first
+            for slab in self.slabs:
+                slab.record_stream(side)
         self.items, self.slabs = [], []  # slabs: side-stream allocations, reused in that stream's order
         self.targets = set()
         ev = torch.cuda.Event()
@@ -1350,7 +1377,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         # the whole weight gradient on the side stream, overlapping the rest of the backward
         # pass (its operands are kept alive for that stream; grad_sink joins it)
         main = torch.cuda.current_stream(dy.device)
-        side = _side_stream(dy.device)
+        side = _wgrad_stream(dy.device)
         side.wait_stream(main)
         batched = _REDUCE_BATCH and plan.w_impl is not None
         with torch.cuda.stream(side):

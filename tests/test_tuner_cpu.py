@@ -110,7 +110,7 @@ def test_reduce_batcher_one_launch_per_batch_and_no_double_target(monkeypatch):
     launch (those would race), and every flush registers its completion event with grad_sink."""
     calls = []
     monkeypatch.setattr(h, "call", lambda name, *a: calls.append((name, a[1])))
-    monkeypatch.setattr(h, "_side_stream", lambda dev: _FakeStream())
+    monkeypatch.setattr(h, "_side_streams", lambda dev: [_FakeStream()])
     monkeypatch.setattr(h.torch.cuda, "Event", _FakeEvent)
     monkeypatch.setattr(grad_sink, "_PENDING", [])
     monkeypatch.setattr(grad_sink, "_ON_DRAIN", [])
