@@ -36,8 +36,8 @@ def _native_lib() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch_per_gpu", type=int, default=256)
     ap.add_argument("--num_frames", type=int, default=16)
     ap.add_argument("--size", type=int, default=200)
