@@ -158,6 +158,11 @@ class ConvPlan:
 
 _PLANS: Dict[tuple, ConvPlan] = {}
 _NUM_CU = 256
+# CUs the wgrad split geometry fills (_wgrad_geom / halo / temporal-box plans); a side-stream wgrad
+# may be launched on a fraction of them (MILNCE_SIDE_GRID_FRAC, A/B knob) to leave the rest of the
+# chip to the main chain's kernels
+_GRID_CU = [_NUM_CU]
+_SIDE_GRID_FRAC = float(os.environ.get("MILNCE_SIDE_GRID_FRAC", "1.0"))
 
 
 _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (csrc/conv.hip)
@@ -952,7 +957,7 @@ def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int, occ: int = 4) ->
     npad = _ceil(Cout, tn) * tn
     kpad = _ceil(Ktot, tk) * tk
     tiles = (npad // tn) * (kpad // tk)
-    splits = max(1, min(_ceil(occ * _NUM_CU, tiles), _ceil(M, 32 * 8)))
+    splits = max(1, min(_ceil(occ * _GRID_CU[0], tiles), _ceil(M, 32 * 8)))
     return npad, kpad, splits
 
 
@@ -1038,12 +1043,12 @@ def _halo_wgrad(dy, x, plan: ConvPlan, cc: int, target: Optional[torch.Tensor], 
     """Box-tiled wgrad; with ``target`` None the kernel only fills the split slab and the
     (slab, splits, Npad, Kpad) of the pending reduction is returned."""
     kt, kh, kw = plan.k
-    key = (id(plan), cc, occ)
+    key = (id(plan), cc, occ, _GRID_CU[0])
     geo = _HALO_SPLITS.get(key)
     if geo is None:
         floats, splits = ctypes.c_longlong(0), ctypes.c_int(0)
         rc = lib().milnce_halo_wgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, kt, kh, kw, 64, cc,
-                                          occ * _NUM_CU, ctypes.byref(floats), ctypes.byref(splits))
+                                          occ * _GRID_CU[0], ctypes.byref(floats), ctypes.byref(splits))
         if rc != 0:
             raise RuntimeError(f"halo wgrad plan failed ({rc}) for {plan}")
         geo = _HALO_SPLITS[key] = (int(floats.value), int(splits.value))
@@ -1084,11 +1089,11 @@ def _twgrad(dy, x, plan: ConvPlan, bn: int, target: Optional[torch.Tensor], accu
     only the split slab is filled and (slab, splits, Npad, Kpad) of the pending reduction is returned.
     ``xss`` (register-staged only): x is a BN layer's raw output and the operand relu(x * scale +
     shift) with that layer's constants (see _TW_PRO)."""
-    key = (id(plan), bn, occ)
+    key = (id(plan), bn, occ, _GRID_CU[0])
     geo = _TW_SPLITS.get(key)
     if geo is None:
         floats, splits = ctypes.c_longlong(0), ctypes.c_int(0)
-        rc = lib().milnce_twgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, bn, occ * _NUM_CU,
+        rc = lib().milnce_twgrad_plan(plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, bn, occ * _GRID_CU[0],
                                       ctypes.byref(floats), ctypes.byref(splits))
         if rc != 0:
             raise RuntimeError(f"temporal wgrad plan failed ({rc}) for {plan}")
@@ -1381,6 +1386,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         side.wait_stream(main)
         batched = _REDUCE_BATCH and plan.w_impl is not None
         with torch.cuda.stream(side):
+            if _SIDE_GRID_FRAC < 1.0:
+                _GRID_CU[0] = max(1, int(_NUM_CU * _SIDE_GRID_FRAC))
             if batched:  # the slab now, its reduction(s) with the next batch (_ReduceBatcher)
                 slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
                 taps = kt * kh * kw
@@ -1391,6 +1398,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 launch_split()
             else:
                 launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
+            _GRID_CU[0] = _NUM_CU
         if _KEEP_REFS:
             kev = None
             if _KEEP_REFS == 1:
