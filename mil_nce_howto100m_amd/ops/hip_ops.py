@@ -2005,8 +2005,19 @@ class _InceptionHead(torch.autograd.Function):
         pooled = torch.empty_like(x)
         arg = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
         geo = [B, T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0]
-        call("milnce_maxpool_fwd", ptr(x), ptr(pooled), ptr(arg), *geo, stream())
+        side = None
+        if _HEAD_POOL_SIDE and x.is_cuda:
+            # the branch-3 pool on the (forward-idle) side stream, overlapping the group GEMM and
+            # its BN passes; pooled / arg belong to this stream, which joins before returning them
+            main = torch.cuda.current_stream(x.device)
+            side = _side_stream(x.device)
+            side.wait_stream(main)
+            call("milnce_maxpool_fwd", ptr(x), ptr(pooled), ptr(arg), *geo, side.cuda_stream)
+        else:
+            call("milnce_maxpool_fwd", ptr(x), ptr(pooled), ptr(arg), *geo, stream())
         outs = _group_forward(ctx, x, n, training, want_gsum0, hyper, args, (arg,), lazy_out)
+        if side is not None:
+            main.wait_stream(side)
         ctx.x_gate = bool(getattr(x, "_milnce_gate", False))
         return (*outs, pooled)
 
@@ -2032,6 +2043,7 @@ class _InceptionHead(torch.autograd.Function):
 
 
 _FUSE_HEAD = os.environ.get("MILNCE_FUSE_INCEPTION_HEAD", "1") != "0"
+_HEAD_POOL_SIDE = os.environ.get("MILNCE_HEAD_POOL_SIDE", "0") == "1"
 
 
 def inception_head(x, weights, bns, training: bool, want_gsum0: bool = False, lazy_out=()):
