@@ -627,8 +627,18 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
         zbuf = z_out if z_out is not None else torch.empty(x.shape, dtype=BF16, device=x.device)
         thw_in = plan.T * plan.H * plan.W
 
+        def pro_ok(impl):
+            # a 4-wave variant also needs its 80 KiB with the prologue's [Cin] constants: a plan first
+            # tuned without the prologue (a plain-input call of the same shape) can hold one that
+            # does not fit, which then runs on the materialised z instead
+            if impl not in _BOX_IMPLS or not fusable:
+                return False
+            return impl not in _BOX4_IMPLS or _box4_lds(_box_eff_bn(impl, plan.bn), plan.k, pro=1,
+                                                         epi=1 if stats is not None else 0,
+                                                         cin=plan.Cin) <= 80 * 1024
+
         def launch_pro(impl, grid):
-            if impl in _BOX_IMPLS and fusable:
+            if pro_ok(impl):
                 call("milnce_conv_fwd_pro", ptr(yp), ldp, ptr(wp), ptr(y), ptr(stats), ptr(shift), ptr(ssp),
                      ptr(z_out),
                      plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.p, plan.Kpad, plan.Npad,
@@ -645,7 +655,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
             plan.impl, plan.grid_m = _tune_fwd(launch_pro, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
                                                                       _box_geo(plan)),
                                                plan.M, plan.Npad, plan.bn, rows_p, sig="fwdpro" + _plan_sig(plan))
-        if plan.impl in _BOX_IMPLS and fusable:
+        if pro_ok(plan.impl):
             launch_pro(plan.impl, plan.grid_m)
             return y
         x = _materialize(x, z_out)

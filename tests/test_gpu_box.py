@@ -198,6 +198,48 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k, nw):
         h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
 
 
+def test_prologue_call_on_plan_without_prologue_room():
+    """A plan first tuned on a plain input can hold a 4-wave variant whose 80 KiB has no room for
+    the BN prologue's [Cin] constants (impl 17 on a 192-wide N tile fits without them only). A
+    prologue ("pro" placeholder) input of the same plan then runs that variant on the materialised
+    z, bitwise the unfused path, instead of failing the launch (the two-rank production DP test
+    hit exactly this)."""
+    import copy
+    from mil_nce_howto100m_amd.models.s3dg import STConv3D
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(11)
+    shape, cin, cmid = (2, 4, 11, 13), 64, 192
+    unit = STConv3D(cin, cmid, [3, 3, 3], padding=1, separable=True).cuda().train()
+    x = torch.randn(*shape, cin, device=DEV).to(torch.bfloat16)
+    g = torch.randn(*shape, cmid, device=DEV).to(torch.bfloat16)
+    plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, 3, 1, 1), (1, 1, 1), (1, 0, 0))
+    if plan.bn != 192 or not h._box_ok(plan.bn, cmid, plan.Kpad, 17, h._box_geo(plan)):
+        pytest.skip(f"N tile {plan.bn}: no plain-fit 4-wave 192-wide variant")
+    assert h._box4_lds(192, plan.k, pro=1, epi=1, cin=cmid) > 80 * 1024
+    old = h._PRO_FUSE
+    res = {}
+    try:
+        for fuse in (False, True):  # tune every other plan first
+            h._PRO_FUSE = fuse
+            copy.deepcopy(unit)(x.clone().requires_grad_(True)).backward(g)
+        plan.impl = 17
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, 192, 2)
+        for fuse in (False, True):
+            h._PRO_FUSE = fuse
+            u = copy.deepcopy(unit)
+            xi = x.clone().requires_grad_(True)
+            out = u(xi)
+            out.backward(g)
+            res[fuse] = (out.detach(), xi.grad.clone(), {n: p.grad.clone() for n, p in u.named_parameters()})
+        a, b = res[False], res[True]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+        for n in a[2]:
+            assert torch.equal(a[2][n], b[2][n]), n
+    finally:
+        h._PRO_FUSE = old
+        plan.impl = 0
+
+
 def test_inception_head_prologue_fusion():
     """An Inception block whose head outputs z1a / z2a (channel slices of the fused 1x1 GEMM output,
     row stride = all three branches) are applied by the separable units' box kernels (x_ld != Cin)
