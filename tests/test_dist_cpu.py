@@ -338,3 +338,47 @@ def test_bucket_bf16_wire():
     assert torch.equal(b16, res[1][1]) and torch.equal(f32, res[1][0])
     assert not torch.equal(f32, b16)  # really went through bf16
     assert ((f32 - b16).norm() / f32.norm()).item() < 1e-2
+
+
+def _worker_buffers(rank, world, port, outdir):
+    _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.ddp import BufferBroadcaster
+    torch.manual_seed(rank)  # different buffers per rank
+    m = torch.nn.Sequential(torch.nn.BatchNorm3d(5), torch.nn.Linear(3, 3), torch.nn.BatchNorm3d(7))
+    for b in m.buffers():
+        if b.is_floating_point():
+            b.copy_(torch.randn_like(b))
+        else:
+            b.fill_(rank + 3)
+    keys = list(m.state_dict())
+    bb = BufferBroadcaster(m, world)
+    views = [(b.data_ptr(), b.dtype) for b in m.buffers()]
+    flat_ptrs = [(f.data_ptr(), f.data_ptr() + f.numel() * f.element_size(), f.dtype) for f in bb.flats]
+    # every buffer is a view into its dtype's flat tensor; names / shapes unchanged
+    inside = all(any(lo <= p < hi and fd == d for lo, hi, fd in flat_ptrs) for p, d in views)
+    bb()
+    after = {k: v.clone() for k, v in m.state_dict().items() if "running" in k or "num_batches" in k}
+    # in-place updates (what the BN kernels do) land in the flat tensor; a load copies into the views
+    m[0].running_mean.add_(1.0)
+    m.load_state_dict({k: v.clone() for k, v in m.state_dict().items()})
+    still = all(b.data_ptr() == p for b, (p, _) in zip(m.buffers(), views))
+    _put(outdir, rank, (len(bb.flats), inside, keys == list(m.state_dict()), after, still,
+                        m[0].running_mean.clone(), bb.flats[0].clone()))
+    dist.destroy_process_group()
+
+
+def test_buffer_broadcaster_flat_views():
+    """BufferBroadcaster at N > 1: the BN buffers become views of one flat tensor per dtype (no
+    per-step pack / unpack), the broadcast makes every rank's buffers rank 0's, in-place updates and
+    state-dict loads keep writing through the views."""
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_buffers, args=(world, port, out), nprocs=world)
+        res = _collect(out, world)
+    for nflat, inside, same_keys, _, still, rm, flat in res:
+        assert nflat == 2  # float32 stats, int64 counters
+        assert inside and same_keys and still
+        assert torch.equal(flat[:rm.numel()], rm)  # the first BN's running mean leads the float flat
+    a, b = res[0][3], res[1][3]
+    assert a.keys() == b.keys() and all(torch.equal(a[k], b[k]) for k in a)
+    assert all(int(v.reshape(-1)[0]) == 3 for k, v in a.items() if "num_batches" in k)  # rank 0's
