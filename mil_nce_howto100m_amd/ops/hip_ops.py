@@ -213,6 +213,26 @@ def _tune_fwd(launch, plan_impls: Tuple[int, ...], M: int, npad: int, bn: int,
     return impl, _grid_for(M, npad, _box_eff_bn(impl, bn), w)
 
 
+_BOX4_FALLBACK = True  # (tests that pin a variant turn it off to see the refusal)
+
+
+def _launch_tuned(launch, impl: int, grid: int, bn: int) -> None:
+    """launch(impl, grid) with a plan's tuned variant. A plan is tuned on its first call, and a
+    later call of the same shape can add LDS the timed launches did not have (producer-BN partial
+    rows in a dgrad epilogue, BN statistics in a forward one): a 4-wave box variant that fit 80 KiB
+    then no longer does. It runs as its 8-wave sibling instead (160 KiB; the same MFMA shape and
+    summation order, so the same conv output bitwise; impl 15 for impl 16's 192-wide plans, which
+    14 has no tile for) on the same grid, so the partial-row count matches (slots without a tile
+    write zero rows). Every rank shares the plan (tune_sync) and so takes the same fallback."""
+    try:
+        launch(impl, grid)
+        return
+    except UnsupportedVariant:
+        if impl not in _BOX4_IMPLS or not _BOX4_FALLBACK:
+            raise
+    launch(15 if impl == 17 or bn == 192 else 14, grid)
+
+
 # v4 forward / dgrad (csrc/conv_v4.hip): LDS-DMA ring with scalar per-stage offsets, for convs
 # whose input channel count is a multiple of 64 (every 64-wide K stage inside one tap). 8 / 10:
 # 16x16x32 MFMA, 2 / 3 stages; 9 / 11: 32x32x16 MFMA (N tiles 64 / 128 / 192). MILNCE_V4=0
@@ -679,7 +699,7 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
     if rows is not None and rows < plan.grid_m:
         raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
                          f"(allocate _stats_rows(M, Npad, bn) rows)")
-    launch(plan.impl, plan.grid_m)
+    _launch_tuned(launch, plan.impl, plan.grid_m, plan.bn)
     return y
 
 
@@ -708,7 +728,7 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
                                                                   _box_geo(plan)),
                                                md, plan.d_Npad, plan.d_bn,
                                                sig=("dgradp" if part is not None else "dgrad") + _plan_sig(plan))
-    launch(plan.d_impl, plan.d_grid_m)
+    _launch_tuned(launch, plan.d_impl, plan.d_grid_m, plan.d_bn)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
     return dx

@@ -62,8 +62,9 @@ CASES = [
 
 
 @pytest.mark.parametrize("case", CASES)
-def test_conv_box_matches_reference(case):
+def test_conv_box_matches_reference(case, monkeypatch):
     from mil_nce_howto100m_amd.ops import hip_ops as h
+    monkeypatch.setattr(h, "_BOX4_FALLBACK", False)  # pinned variants: see the 4-wave refusals
     torch.manual_seed(21)
     B, T, H, W, cin, cout, k, p = case
     x = torch.randn(B, T, H, W, cin, device=DEV).to(torch.bfloat16)
@@ -238,6 +239,44 @@ def test_prologue_call_on_plan_without_prologue_room():
     finally:
         h._PRO_FUSE = old
         plan.impl = 0
+
+
+def test_tuned_4wave_dgrad_without_partial_room_runs_8wave_sibling():
+    """A dgrad plan tuned without producer-BN partials (EPI 0) can hold impl 17 on a 192-wide
+    (3,1,1) tile, which fits 80 KiB only without the partial rows; a later call with partials runs
+    the 8-wave sibling (impl 15) on the same grid instead of failing: dX bitwise the 4-wave result,
+    partial sums those of impl 15."""
+    from mil_nce_howto100m_amd.ops import hip_ops as h
+    torch.manual_seed(12)
+    shape, c = (2, 4, 11, 13), 192
+    plan = h.conv_plan(shape + (c,), (c, c, 3, 1, 1), (1, 1, 1), (1, 0, 0))
+    geo = h._box_geo(plan)
+    if plan.d_bn != 192 or not (h._box_ok(192, c, plan.d_Kpad, 17, geo) and h._box_ok(192, c, plan.d_Kpad, 15, geo)):
+        pytest.skip(f"dgrad N tile {plan.d_bn}: no 192-wide 4-wave / 8-wave pair")
+    assert h._box4_lds(192, plan.k, epi=2) > 80 * 1024 >= h._box4_lds(192, plan.k)
+    w = torch.randn(c, c, 3, 1, 1, device=DEV) * 0.05
+    wd = h._pack(w, plan, 1)
+    dy = torch.randn(*shape, c, device=DEV).to(torch.bfloat16)
+    x = torch.randn(*shape, c, device=DEV).to(torch.bfloat16)
+    ss = torch.cat([torch.randn(c, device=DEV) * 0.1, torch.rand(c, device=DEV) + 0.5,
+                    torch.randn(c, device=DEV), torch.randn(c, device=DEV) * 0.2])
+    md = plan.B * plan.T * plan.H * plan.W
+    try:
+        plan.d_grid_m = h._grid_for(md, plan.d_Npad, 192, 2)
+        plan.d_impl = 17
+        dx4 = h.conv_dgrad(dy, wd, plan)  # no partials: the 4-wave kernel itself
+        dx_fb = h.conv_dgrad(dy, wd, plan, (x, ss, c))  # partials: falls back
+        p_fb, n_fb, ps = h.take_bn_partials(dx_fb)
+        plan.d_impl = 15
+        dx8 = h.conv_dgrad(dy, wd, plan, (x, ss, c))
+        p8, n8, _ = h.take_bn_partials(dx8)
+    finally:
+        plan.d_impl = 0
+    assert torch.equal(dx_fb, dx4) and torch.equal(dx_fb, dx8)
+    assert n_fb == n8
+    s_fb = p_fb[:n8 * 2 * ps].view(n8, 2, ps).double().sum(0)
+    s8 = p8[:n8 * 2 * ps].view(n8, 2, ps).double().sum(0)
+    assert torch.allclose(s_fb, s8, rtol=1e-5, atol=1e-3)
 
 
 def test_inception_head_prologue_fusion():
