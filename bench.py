@@ -193,6 +193,12 @@ def main():
         # where the kernel plan came from: the shipped plan table (ops/plans/gfx950.json, valid for
         # these kernel sources) or first-use timing on this box
         out["plan"] = tune_sync.table_info()
+        if cuda:
+            from mil_nce_howto100m_amd.ops import hip_ops
+            # launches whose tuned variant could not run in the call (0: every forward / dgrad call
+            # context was tuned on its own) and the side-stream memory rule's per-step decisions
+            out["plan"].update(hip_ops.plan_events())
+            out["side_stream"] = dict(hip_ops._HEADROOM_STATS)
         if opts.save_plan:
             out["plan"]["saved"] = tune_sync.save_table(opts.save_plan)
         if comm is not None:

@@ -7,6 +7,8 @@
 // the output windows that cover it and sums the gradients whose arg-max points at it
 // (deterministic, no atomics). Ties resolve to the first tap in (t, h, w) order, as in ATen.
 #include "common.h"
+#include <algorithm>
+#include <type_traits>
 
 struct PoolParams {
   int T, H, W, C, To, Ho, Wo;
@@ -1270,6 +1272,324 @@ __global__ __launch_bounds__(512) void maxpool_s1_bwd_sep(PoolParams p, int G, i
   }
 }
 
+// =========================================================================================
+// Row sweeps (stride-1 impl 2, the default). A workgroup owns one clip and a chunk of G 8-channel
+// groups over ALL T x W positions of the plane and sweeps the H rows. An item is (position, group):
+// one 16-B lane access, and the G lanes of a position read G*16 contiguous bytes, so a wave-load
+// covers whole 128-B lines (G = 8) where the plane sweeps above read 32-B row pieces. Every input
+// element is read exactly once: the sweep carries the h neighbours, the tile holds the t / w ones.
+// Separable max in the order w (LDS exchange), t (LDS exchange), h (register ring over the
+// sweep); the h stage breaks value ties by the candidates' absolute frame, then by row, so the
+// arg-max is the first maximum in (t, h, w) order like the reference pool (s3dg.py:20-21,
+// nn.MaxPool3d). Codes per element: cw | ct << 2 | ch << 4 of the element's own cells, stored per
+// (clip, chunk, row) as one contiguous run of n_it * 8 bytes (s1_rows_coff).
+// =========================================================================================
+struct RowItem {
+  uint32_t eoff;  // byte offset of row 0 of this item in the clip (out of range when inactive)
+  int i, t, w;
+  bool act;
+};
+
+__device__ __forceinline__ RowItem row_item(const PoolParams& p, int G, int chunk, int i, int n_it) {
+  RowItem r;
+  r.i = i;
+  r.act = i < n_it;
+  const int pos = r.act ? i / G : 0, g = r.act ? i - pos * G : 0;
+  r.t = pos / p.W;
+  r.w = pos - r.t * p.W;
+  r.eoff = r.act ? (uint32_t)(((r.t * p.H * p.W + r.w) * p.C + (chunk * G + g) * 8) * 2) : 0x40000000u;
+  return r;
+}
+
+// code byte field `sh` (0: cw, 2: ct, 4: ch) of channel k from a lane's 8 code bytes
+__device__ __forceinline__ uint32_t rcode(const uint2& a, int k, int sh) {
+  return (((k < 4 ? a.x : a.y) >> (8 * (k & 3) + sh)) & 3u);
+}
+
+template <int N>
+using ic = std::integral_constant<int, N>;
+
+// D = rows whose loads are in flight ahead of the row being processed (a register ring, the
+// sweep unrolled by D so no pending load is ever copied between registers): one row in flight
+// per wave measured 2.5-3.3 TB/s, latency-bound.
+template <int D>
+__global__ __launch_bounds__(1024) void maxpool_s1_fwd_rows(PoolParams p, int G, int nchunk,
+                                                            const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                            uint8_t* __restrict__ arg) {
+  extern __shared__ uint4 rows_lds[];
+  const int n_it = p.T * p.W * G, WG = p.W * G;
+  uint4* xs = rows_lds;          // [n_it] the current input row
+  uint4* m1s = rows_lds + n_it;  // [n_it] its w maxima
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);  // a clip's chunks share lines when G*16 % 128 != 0
+  const int b = blk / nchunk, chunk = blk - b * nchunk;
+  const int nbytes = p.T * p.H * p.W * p.C * 2;
+  const size_t clip = (size_t)b * p.T * p.H * p.W * p.C;
+  const auto xr = clip_rsrc(x + clip, nbytes);
+  const auto yr = clip_rsrc(y + clip, nbytes);
+  const int cbytes = p.H * n_it * 8;
+  const auto ar = clip_rsrc(arg + (size_t)blk * cbytes, cbytes);
+  const uint32_t rowb = (uint32_t)(p.W * p.C * 2), oob = 0x40000000u;
+  const RowItem it = row_item(p, G, chunk, threadIdx.x, n_it);
+  const int i = it.i, H = p.H;
+  auto xo = [&](int h) { return h < H ? it.eoff + (uint32_t)h * rowb : oob; };
+  uint4 ring[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) ring[d] = bld16(xr, xo(d));
+  // rows h-2 (A), h-1 (B), h (C): t-stage maxima and the cells' own codes (4 bits per channel:
+  // cw | ct << 2)
+  uint4 mA = make_uint4(0, 0, 0, 0), mB = mA;
+  uint32_t cA = 0, cB = 0;
+  const bool wm = it.w > 0, wp = it.w + 1 < p.W, tm = it.t > 0, tp = it.t + 1 < p.T;
+  auto step = [&](auto slot_c, int h) {
+    constexpr int slot = decltype(slot_c)::value;
+    uint4 mC = make_uint4(0, 0, 0, 0);
+    uint32_t cC = 0;
+    if (h < H) {
+      const uint4 xc = ring[slot];
+      if (it.act) xs[i] = xc;
+      ring[slot] = bld16(xr, xo(h + D));
+      lds_barrier();
+      uint32_t cw = 0;
+      uint4 m1 = xc;
+      if (it.act) {
+        float a[8], bb[8], c[8], m[8];
+        uint32_t cd[8];
+        unpack8(xs[wm ? i - G : i], a);
+        unpack8(xc, bb);
+        unpack8(xs[wp ? i + G : i], c);
+        max3(a, wm, bb, true, c, wp, m, cd);
+        m1 = pack8(m);  // exact: maxima of bf16 values
+        m1s[i] = m1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cw |= cd[j] << (4 * j);
+      }
+      lds_barrier();
+      if (it.act) {
+        float a[8], bb[8], c[8], m[8];
+        uint32_t cd[8];
+        unpack8(m1s[tm ? i - WG : i], a);
+        unpack8(m1, bb);
+        unpack8(m1s[tp ? i + WG : i], c);
+        max3(a, tm, bb, true, c, tp, m, cd);
+        mC = pack8(m);
+        cC = cw;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cC |= cd[j] << (4 * j + 2);
+      }
+    }
+    if (h >= 1) {  // output row h-1 from rows h-2 (dh 0), h-1 (dh 1), h (dh 2)
+      const bool va = h >= 2, vc = h < H;
+      float fa[8], fb[8], fc[8], o[8];
+      unpack8(mA, fa);
+      unpack8(mB, fb);
+      unpack8(mC, fc);
+      const int t0 = it.t - 1;
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        // candidates in row order; a later one wins on a larger value or an earlier frame
+        float m = fb[j];
+        int tmx = t0 + (int)((cB >> (4 * j + 2)) & 3u);
+        uint32_t ch = 1;
+        if (va) {
+          const int ta = t0 + (int)((cA >> (4 * j + 2)) & 3u);
+          if (fa[j] > m || (fa[j] == m && ta <= tmx)) { m = fa[j]; tmx = ta; ch = 0; }
+        }
+        if (vc) {
+          const int tc = t0 + (int)((cC >> (4 * j + 2)) & 3u);
+          if (fc[j] > m || (fc[j] == m && tc < tmx)) { m = fc[j]; ch = 2; }
+        }
+        o[j] = m;
+        const uint32_t byte = ((cB >> (4 * j)) & 0xFu) | (ch << 4);
+        if (j < 4) lo |= byte << (8 * j);
+        else hi |= byte << (8 * (j - 4));
+      }
+      bst16(yr, xo(h - 1), pack8(o));
+      bst8(ar, it.act ? (uint32_t)(((h - 1) * n_it + i) * 8) : oob, make_uint2(lo, hi));
+    }
+    mA = mB;
+    cA = cB;
+    mB = mC;
+    cB = cC;
+  };
+  for (int h0 = 0; h0 <= H; h0 += D) {
+    step(ic<0>{}, h0);
+    if constexpr (D > 1) { if (h0 + 1 <= H) step(ic<1 % D>{}, h0 + 1); }
+    if constexpr (D > 2) { if (h0 + 2 <= H) step(ic<2 % D>{}, h0 + 2); }
+    if constexpr (D > 3) { if (h0 + 3 <= H) step(ic<3 % D>{}, h0 + 3); }
+  }
+}
+
+// Backward, input row h' per step (the forward's stages in reverse):
+//   h  dmt(h') = [ch(h'+1) == 0] dy(h'+1) + [ch(h') == 1] dy(h') + [ch(h'-1) == 2] dy(h'-1)   (registers)
+//   t  dm1(t') = sum_dt [ct(t'-dt+1) == dt] dmt(t'-dt+1)                                     (LDS exchange)
+//   w  dx(w')  = sum_dw [cw(w'-dw+1) == dw] dm1(w'-dw+1)                                     (LDS exchange)
+// fp32 sums, dx rounded once. Fused epilogue as maxpool_s1_bwd_sep: dx += acc_in (the Inception
+// head GEMM's dX), gs[b, c] = sum_thw dx * x in a fixed-order workgroup reduction.
+// Register rings: dy / codes of rows h'-1 .. h'+1+D (U = D + 2 slots, row r in slot r % U), the
+// epilogue operands of rows h' .. h'+D-1 (row r in slot r % D); the sweep is unrolled by U (a
+// multiple of D for D = 1, 2).
+template <int D>
+__global__ __launch_bounds__(1024) void maxpool_s1_bwd_rows(PoolParams p, int G, int nchunk,
+                                                            const bf16_t* __restrict__ dy,
+                                                            const uint8_t* __restrict__ arg,
+                                                            const bf16_t* __restrict__ acc_in,
+                                                            const bf16_t* __restrict__ x, float* __restrict__ gs,
+                                                            bf16_t* __restrict__ dx) {
+  static_assert(D == 1 || D == 2, "unroll U = D + 2 must be a multiple of D");
+  constexpr int U = D + 2;
+  extern __shared__ uint4 rows_lds[];
+  const int n_it = p.T * p.W * G, WG = p.W * G;
+  const int na = max(n_it, (int)blockDim.x);  // exchange-area slots (>= threads: the gs reduction)
+  float4* tlo = (float4*)rows_lds;  // t-exchange: dmt channels 0-3 | 4-7, the cells' codes
+  float4* thi = tlo + na;
+  uint2* tcd = (uint2*)(thi + na);
+  float4* wlo = (float4*)(tcd + na);  // w-exchange: dm1, codes (a second area: no WAR barrier)
+  float4* whi = wlo + na;
+  uint2* wcd = (uint2*)(whi + na);
+  const int blk = xcd_remap(blockIdx.x, gridDim.x);
+  const int b = blk / nchunk, chunk = blk - b * nchunk;
+  const int nbytes = p.T * p.H * p.W * p.C * 2;
+  const size_t clip = (size_t)b * p.T * p.H * p.W * p.C;
+  const auto dyr = clip_rsrc(dy + clip, nbytes);
+  const int cbytes = p.H * n_it * 8;
+  const auto agr = clip_rsrc(arg + (size_t)blk * cbytes, cbytes);
+  const auto inr = clip_rsrc(acc_in != nullptr ? acc_in + clip : dy + clip, acc_in != nullptr ? nbytes : 0);
+  const auto xr = clip_rsrc(x != nullptr ? x + clip : dy + clip, gs != nullptr ? nbytes : 0);
+  const auto dxr = clip_rsrc(dx + clip, nbytes);
+  const uint32_t rowb = (uint32_t)(p.W * p.C * 2), oob = 0x40000000u;
+  const RowItem it = row_item(p, G, chunk, threadIdx.x, n_it);
+  const int i = it.i, H = p.H;
+  auto eo = [&](int h) { return (h >= 0 && h < H) ? it.eoff + (uint32_t)h * rowb : oob; };
+  auto co = [&](int h) { return (h >= 0 && h < H && it.act) ? (uint32_t)((h * n_it + i) * 8) : oob; };
+  uint4 g[U], e[D], xv[D];
+  uint2 c[U];
+  // row r in slot r % U; slot U-1 holds row -1 (zeros, invalid)
+  g[U - 1] = make_uint4(0, 0, 0, 0);
+  c[U - 1] = make_uint2(0, 0);
+#pragma unroll
+  for (int r = 0; r <= D; ++r) {
+    g[r] = bld16(dyr, eo(r));
+    c[r] = bld8(agr, co(r));
+  }
+#pragma unroll
+  for (int r = 0; r < D; ++r) {
+    e[r] = bld16(inr, eo(r));
+    xv[r] = bld16(xr, eo(r));
+  }
+  float sacc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) sacc[j] = 0.f;
+  const bool wm = it.w > 0, wp = it.w + 1 < p.W, tm = it.t > 0, tp = it.t + 1 < p.T;
+  auto step = [&](auto sl_c, int h) {
+    constexpr int s = decltype(sl_c)::value;                       // h % U
+    constexpr int sa = (s + U - 1) % U, sc = (s + 1) % U, se = s % D;  // rows h-1, h+1; epilogue slot
+    const bool va = h >= 1, vc = h + 1 < H;
+    {
+      float ga[8], gb[8], gc[8], d1[8];
+      unpack8(g[sa], ga);
+      unpack8(g[s], gb);
+      unpack8(g[sc], gc);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = (vc && rcode(c[sc], j, 4) == 0u) ? gc[j] : 0.f;
+        v += rcode(c[s], j, 4) == 1u ? gb[j] : 0.f;
+        v += (va && rcode(c[sa], j, 4) == 2u) ? ga[j] : 0.f;
+        d1[j] = v;
+      }
+      if (it.act) {
+        tlo[i] = make_float4(d1[0], d1[1], d1[2], d1[3]);
+        thi[i] = make_float4(d1[4], d1[5], d1[6], d1[7]);
+        tcd[i] = c[s];
+      }
+    }
+    // row h-1 is used up: its slot takes row h+D+1
+    g[sa] = bld16(dyr, eo(h + D + 1));
+    c[sa] = bld8(agr, co(h + D + 1));
+    lds_barrier();
+    if (it.act) {  // (a cell's own partial sums are re-read here, not held across the barriers)
+      const int im = tm ? i - WG : i, ip = tp ? i + WG : i;
+      const uint2 c0 = tcd[ip], c2 = tcd[im];
+      const float4 p0a = tlo[ip], p0b = thi[ip], p2a = tlo[im], p2b = thi[im], p1a = tlo[i], p1b = thi[i];
+      const float q0[8] = {p0a.x, p0a.y, p0a.z, p0a.w, p0b.x, p0b.y, p0b.z, p0b.w};
+      const float q1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
+      const float q2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
+      float d1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = (tp && rcode(c0, j, 2) == 0u) ? q0[j] : 0.f;
+        v += rcode(c[s], j, 2) == 1u ? q1[j] : 0.f;
+        v += (tm && rcode(c2, j, 2) == 2u) ? q2[j] : 0.f;
+        d1[j] = v;
+      }
+      wlo[i] = make_float4(d1[0], d1[1], d1[2], d1[3]);
+      whi[i] = make_float4(d1[4], d1[5], d1[6], d1[7]);
+      wcd[i] = c[s];
+    }
+    lds_barrier();
+    if (it.act) {
+      const int im = wm ? i - G : i, ip = wp ? i + G : i;
+      const uint2 c0 = wcd[ip], c2 = wcd[im];
+      const float4 p0a = wlo[ip], p0b = whi[ip], p2a = wlo[im], p2b = whi[im], p1a = wlo[i], p1b = whi[i];
+      const float q0[8] = {p0a.x, p0a.y, p0a.z, p0a.w, p0b.x, p0b.y, p0b.z, p0b.w};
+      const float q1[8] = {p1a.x, p1a.y, p1a.z, p1a.w, p1b.x, p1b.y, p1b.z, p1b.w};
+      const float q2[8] = {p2a.x, p2a.y, p2a.z, p2a.w, p2b.x, p2b.y, p2b.z, p2b.w};
+      float ev[8], d[8], q[8], xf[8];
+      unpack8(e[se], ev);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float v = ev[j];
+        v += (wp && rcode(c0, j, 0) == 0u) ? q0[j] : 0.f;
+        v += rcode(c[s], j, 0) == 1u ? q1[j] : 0.f;
+        v += (wm && rcode(c2, j, 0) == 2u) ? q2[j] : 0.f;
+        d[j] = v;
+      }
+      const uint4 vout = pack8(d);
+      bst16(dxr, eo(h), vout);
+      unpack8(vout, q);
+      unpack8(xv[se], xf);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sacc[j] = fmaf(q[j], xf[j], sacc[j]);
+    }
+    e[se] = bld16(inr, eo(h + D));
+    xv[se] = bld16(xr, eo(h + D));
+  };
+  for (int h0 = 0; h0 < H; h0 += U) {
+    step(ic<0>{}, h0);
+    if (h0 + 1 < H) step(ic<1>{}, h0 + 1);
+    if (h0 + 2 < H) step(ic<2>{}, h0 + 2);
+    if constexpr (U > 3) { if (h0 + 3 < H) step(ic<3 % U>{}, h0 + 3); }
+  }
+  if (gs == nullptr) return;
+  // gs over the plane's positions per (group, channel): per-thread sums -> LDS, then a fixed-order
+  // two-level reduction (P strided partial sums per output, summed in order). Thread r's sums
+  // belong to group r % G.
+  __syncthreads();
+  float* red = (float*)rows_lds;  // [nthr][8] (the t-exchange area holds 40 B per slot)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x * 8 + j] = sacc[j];
+  __syncthreads();
+  const int nthr = blockDim.x, nout = G * 8, rows = (nthr + G - 1) / G;
+  const int P = max(1, min(nthr / nout, rows));
+  float* part = (float*)wlo;  // [P][nout] (the w-exchange area)
+  const int o = threadIdx.x % nout, q = threadIdx.x / nout;
+  if (q < P) {
+    float s = 0.f;
+    for (int r = q; r < rows; r += P) {
+      const int src = r * G + o / 8;
+      if (src < nthr) s += red[src * 8 + (o & 7)];
+    }
+    part[q * nout + o] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < nout) {
+    float s = 0.f;
+    for (int r = 0; r < P; ++r) s += part[r * nout + threadIdx.x];
+    gs[(size_t)b * p.C + chunk * nout + threadIdx.x] = s;
+  }
+}
+
+
 // G (8-channel groups per workgroup) for the plane sweeps: as many as fit `maxthr` threads
 // (all rows of the plane are always in one workgroup), at least 1.
 static int s1_groups(int rows, int C, int maxthr = 256, long long B = 0) {
@@ -1298,14 +1618,102 @@ static size_t s1_bwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 80; 
 // kernels (A/B benchmarks only; milnce_set_pool_s1_impl). A tiled forward (band + halo rows in
 // LDS, one barrier, all loads in flight) measured 1.6-2.4 TB/s against the sweep's 2.6-3.4: its
 // h stage is recomputed per t and the VALU work, not memory, bound it (tools/ew_bench.py).
-static int g_s1_impl = 1;
+// 2 = row sweeps (default; a shape they cannot tile takes the plane sweeps).
+static int g_s1_impl = 2;
+static bool is_s1_333(const PoolParams& p);
+#define HIP_RET_E(expr)                   \
+  do {                                    \
+    hipError_t _e = (expr);               \
+    if (_e != hipSuccess) return _e;      \
+  } while (0)
 static int g_s1_maxthr = 512;  // workgroup size cap of the plane sweeps (G = cap / rows groups)
 MILNCE_API int milnce_set_pool_s1_maxthr(int n) {
   const int old = g_s1_maxthr;
   if (n >= 64 && n <= 1024) g_s1_maxthr = n;
   return old;
 }
-static bool s1_use_lds(const PoolParams& p) { return g_s1_impl == 1 && p.T * p.H <= 512; }
+
+// Row sweeps: G = the largest divisor of C/8 up to MILNCE_S1_G (default 4: the flagship 25x25
+// planes then take 800-item tiles, one item per thread, two workgroups per CU) that keeps the
+// tile at <= 1024 items. A divisor, so the per-(clip, chunk) code runs tile the arg buffer
+// exactly. Depends on the shape only: the forward and the backward must agree. Prefetch depths
+// MILNCE_S1_DF (forward rows in flight, 1-4, default 3) / MILNCE_S1_DB (backward, 1-2, default 2).
+static int env_int(const char* name, int def, int lo, int hi) {
+  const char* e = getenv(name);
+  int v = e ? atoi(e) : def;
+  return (v < lo || v > hi) ? def : v;
+}
+static int s1_rows_gmax() {
+  static int g = -1;
+  if (g < 0) g = env_int("MILNCE_S1_G", 4, 1, 8);
+  return g;
+}
+static int s1_rows_G(const PoolParams& p) {
+  const int cpr = p.C / 8;
+  for (int g = std::min(s1_rows_gmax(), cpr); g >= 1; --g)
+    if (cpr % g == 0 && p.T * p.W * g <= 1024) return g;
+  return 0;
+}
+static bool s1_use_rows(const PoolParams& p) {
+  return g_s1_impl == 2 && is_s1_333(p) && s1_rows_G(p) > 0 && (long long)p.T * p.H * p.W * p.C * 2 < (1ll << 30);
+}
+static bool s1_use_lds(const PoolParams& p) {
+  return (g_s1_impl == 1 || (g_s1_impl == 2 && !s1_use_rows(p))) && p.T * p.H <= 512;
+}
+// either sweep: arg-max codes in a sweep layout, read by the matching sweep backward only
+static bool s1_sweep(const PoolParams& p) { return is_s1_333(p) && (s1_use_rows(p) || s1_use_lds(p)); }
+
+template <typename K>
+static hipError_t lds_attr(K kernel) {
+  return hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+static hipError_t launch_s1_rows_fwd(const PoolParams& p, long long B, const void* x, void* y, void* arg,
+                                     hipStream_t s) {
+  const int G = s1_rows_G(p), nchunk = p.C / 8 / G, n_it = p.T * p.W * G;
+  const int nthr = (n_it + 63) / 64 * 64;
+  const size_t lds = (size_t)n_it * 32;
+  static int df = -1;
+  if (df < 0) {
+    HIP_RET_E(lds_attr(maxpool_s1_fwd_rows<1>));
+    HIP_RET_E(lds_attr(maxpool_s1_fwd_rows<2>));
+    HIP_RET_E(lds_attr(maxpool_s1_fwd_rows<3>));
+    HIP_RET_E(lds_attr(maxpool_s1_fwd_rows<4>));
+    df = env_int("MILNCE_S1_DF", 3, 1, 4);
+  }
+  const dim3 grid((unsigned)(B * nchunk)), block(nthr);
+#define XF(n)                                                                                                  \
+  hipLaunchKernelGGL((maxpool_s1_fwd_rows<n>), grid, block, lds, s, p, G, nchunk, (const bf16_t*)x, (bf16_t*)y, \
+                     (uint8_t*)arg);
+  switch (df) {
+    case 1: XF(1) break;
+    case 2: XF(2) break;
+    case 4: XF(4) break;
+    default: XF(3)
+  }
+#undef XF
+  return hipSuccess;
+}
+
+static hipError_t launch_s1_rows_bwd(const PoolParams& p, long long B, const void* dy, const void* arg,
+                                     const void* acc_in, const void* x, float* gs, void* dx, hipStream_t s) {
+  const int G = s1_rows_G(p), nchunk = p.C / 8 / G, n_it = p.T * p.W * G;
+  const int nthr = (n_it + 63) / 64 * 64;
+  const size_t lds = (size_t)std::max(n_it, nthr) * 80;
+  static int db = -1;
+  if (db < 0) {
+    HIP_RET_E(lds_attr(maxpool_s1_bwd_rows<1>));
+    HIP_RET_E(lds_attr(maxpool_s1_bwd_rows<2>));
+    db = env_int("MILNCE_S1_DB", 2, 1, 2);
+  }
+  const dim3 grid((unsigned)(B * nchunk)), block(nthr);
+#define XR(n)                                                                                                  \
+  hipLaunchKernelGGL((maxpool_s1_bwd_rows<n>), grid, block, lds, s, p, G, nchunk, (const bf16_t*)dy,         \
+                     (const uint8_t*)arg, (const bf16_t*)acc_in, (const bf16_t*)x, gs, (bf16_t*)dx);
+  if (db == 1) { XR(1) } else { XR(2) }
+#undef XR
+  return hipSuccess;
+}
 MILNCE_API int milnce_set_pool_s1_impl(int impl) {
   const int old = g_s1_impl;
   g_s1_impl = impl;
@@ -1396,7 +1804,7 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
     return true;
   }
   if (bn_ss != nullptr) {
-    if (is_s1_333(p) && s1_use_lds(p)) return false;  // its backward reads sweep-layout codes (S1Geo)
+    if (s1_sweep(p)) return false;  // its backward reads sweep-layout codes
     long long g = (n + 255) / 256;
     const int grid = (int)(g > 65536 ? 65536 : g);
 #define X(a, b, c, e, f, h)                                                                                      \
@@ -1413,6 +1821,11 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
     MILNCE_POOL_SHAPES(X)
 #undef X
     return false;
+  }
+  if (s1_use_rows(p)) {
+    const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
+    (void)launch_s1_rows_fwd(p, B, x, y, arg, s);  // a failed launch shows in hipGetLastError
+    return true;
   }
   if (is_s1_333(p) && s1_use_lds(p)) {
     const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
@@ -1455,8 +1868,13 @@ static bool pool_bwd_special(const PoolParams& p, const void* dy, const void* ar
   if (n >= (1ll << 31)) return false;
   // codes in the sweep layout (the plane-sweep forward wrote them) are read by the sweep backward
   // only, which has no BN-partials / gate / apply epilogues
-  if (is_s1_333(p) && s1_use_lds(p) && (bn_y != nullptr || gate_g != nullptr || coef != nullptr)) return false;
+  if (s1_sweep(p) && (bn_y != nullptr || gate_g != nullptr || coef != nullptr)) return false;
   const PoolDivs d = make_divs(p);
+  if (s1_use_rows(p) && bn_y == nullptr) {
+    const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
+    (void)launch_s1_rows_bwd(p, B, dy, arg, nullptr, nullptr, nullptr, dx, s);
+    return true;
+  }
   if (is_s1_333(p) && bn_y == nullptr && s1_use_lds(p)) {
     const long long B = n / ((long long)p.T * p.H * p.W * (p.C / 8));
     const int rows = p.T * p.H, G = s1_groups(rows, p.C, g_s1_maxthr, B), nchunk = (p.C / 8 + G - 1) / G;
@@ -1609,7 +2027,7 @@ MILNCE_API int milnce_maxpool_bwd(const void* dy, const void* arg, void* dx, int
   const long long n = (long long)B * T * H * W * (C / 8);
   if (pool_bwd_special(p, dy, arg, dx, n, bn_y, bn_ld, bn_ss, part, nparts, stream)) return (int)hipGetLastError();
   if (dx == nullptr) return (int)hipErrorInvalidValue;  // partials-only passes: specialised shapes
-  if (is_s1_333(p) && s1_use_lds(p)) return (int)hipErrorInvalidValue;  // sweep-layout codes (S1Geo)
+  if (s1_sweep(p)) return (int)hipErrorInvalidValue;  // sweep-layout codes
   if (bn_y != nullptr && (256 % (C / 8) != 0 || bn_ld != C)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(nparts), dim3(256), 0, stream, p, (const bf16_t*)dy,
                      (const uint8_t*)arg, (bf16_t*)dx, n, (const bf16_t*)bn_y, bn_ss, part);
@@ -1625,7 +2043,12 @@ MILNCE_API int milnce_maxpool_s1_bwd_fused(const void* dy, const void* arg, cons
   PoolParams p = make_pool(T, H, W, C, T, H, W, 3, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, 1, 0);
   const int rows = T * H;
   // the separable code layout must match the forward that produced arg (milnce_maxpool_fwd)
-  if (!s1_use_lds(p) || (gs != nullptr && x == nullptr)) return (int)hipErrorInvalidValue;
+  if (gs != nullptr && x == nullptr) return (int)hipErrorInvalidValue;
+  if (s1_use_rows(p)) {
+    HIP_RET(launch_s1_rows_bwd(p, B, dy, arg, acc_in, x, gs, dx, stream));
+    return (int)hipGetLastError();
+  }
+  if (!s1_use_lds(p)) return (int)hipErrorInvalidValue;
   const int G = s1_groups(rows, C, g_s1_maxthr, B), nchunk = (C / 8 + G - 1) / G;
   launch_s1_bwd(W, dim3((unsigned)((long long)B * nchunk)), dim3(s1_threads(rows, G)), s1_bwd_lds(rows, G), stream,
                 p, G, nchunk, (const bf16_t*)dy, (const uint8_t*)arg, (const bf16_t*)acc_in, (const bf16_t*)x, gs,

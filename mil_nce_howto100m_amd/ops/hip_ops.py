@@ -11,7 +11,7 @@ import collections
 import ctypes
 import os
 import math
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -103,9 +103,41 @@ def _tune_log(line: str) -> None:
 
 
 def _plan_sig(plan) -> str:
-    """Problem identity of a conv plan for rank-consistent tuning (tune_sync)."""
+    """Problem identity of a conv plan for rank-consistent tuning (tune_sync). Callers prefix the
+    call context (direction, prologue, statistics / partial-row epilogue: ``_ctx_key``), so a
+    variant is always timed for exactly the call that launches it."""
     return (f"|B{plan.B}T{plan.T}H{plan.H}W{plan.W}|{plan.Cin}>{plan.Cout}|k{plan.k}s{plan.s}p{plan.p}"
             f"|wo{plan.wo_override}")
+
+
+# Plan hygiene counters (bench.py reports them under "plan"): ``fallbacks`` = launches whose tuned
+# variant could not run in the call and ran as another, untimed variant. Every forward / dgrad
+# call context is tuned on its own (ConvPlan.ctx), so this stays 0 unless a plan table entry
+# disagrees with the running kernels.
+_PLAN_EVENTS = {"fallbacks": 0, "contexts": 0}
+
+
+def plan_events() -> dict:
+    return dict(_PLAN_EVENTS)
+
+
+def _decision(plan: "ConvPlan", ck: str, dgrad: bool, tune) -> Tuple[int, int]:
+    """(variant, grid) of ``plan`` for call context ``ck``: the pinned variant, else the context's
+    tuned decision (``tune()`` on its first call)."""
+    pin = plan.pin_d if dgrad else plan.pin_f
+    if pin:
+        return pin, (plan.d_grid_m if dgrad else plan.grid_m)
+    if ck not in plan.ctx:
+        plan.ctx[ck] = tune()
+        _PLAN_EVENTS["contexts"] += 1
+    return plan.ctx[ck]
+
+
+def _ctx_key(kind: str, *flags: str) -> str:
+    """Call-context key of a tuned decision: kind (fwd / fwdpro / dgrad / dgradbn) plus flags
+    (st: BN-statistics epilogue, p: producer-BN partial rows, fz / nf: the prologue input can /
+    cannot be staged by the fused kernel)."""
+    return kind + "".join("|" + f for f in flags if f)
 
 
 # =========================================================================================
@@ -150,6 +182,12 @@ class ConvPlan:
     d_impl: int = 0       # dgrad kernel variant
     w_impl: int = 0       # wgrad kernel variant (2: register-staged, 3/4: LDS-DMA ring, 3/2 stages)
     w_occ: int = 4        # wgrad split-K target: workgroups per CU (fewer splits = smaller slab to reduce)
+    # forward / dgrad decisions per call context (_ctx_key -> (variant, persistent grid)); impl /
+    # grid_m and d_impl / d_grid_m hold the ones of the latest call
+    ctx: Dict[str, Tuple[int, int]] = field(default_factory=dict)
+    # tests / tools pin a variant for every context (the grid is then grid_m / d_grid_m as set)
+    pin_f: int = 0
+    pin_d: int = 0
 
     @property
     def taps(self) -> int:
@@ -230,6 +268,7 @@ def _launch_tuned(launch, impl: int, grid: int, bn: int) -> None:
     except UnsupportedVariant:
         if impl not in _BOX4_IMPLS or not _BOX4_FALLBACK:
             raise
+    _PLAN_EVENTS["fallbacks"] += 1
     launch(15 if impl == 17 or bn == 192 else 14, grid)
 
 
@@ -670,15 +709,20 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
                      plan.B, plan.T, plan.H, plan.W, plan.Cin, plan.Cout, *plan.k, *plan.s, *plan.p,
                      plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
 
-        if plan.impl == 0:  # tuned on what each variant costs here (fused prologue vs apply pass + conv)
-            rows_p = stats.numel() // (2 * plan.Npad) if stats is not None else None
-            plan.impl, plan.grid_m = _tune_fwd(launch_pro, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
-                                                                      _box_geo(plan)),
-                                               plan.M, plan.Npad, plan.bn, rows_p, sig="fwdpro" + _plan_sig(plan))
+        ck = _ctx_key("fwdpro", "st" if stats is not None else "", "fz" if fusable else "nf")
+        rows_p = stats.numel() // (2 * plan.Npad) if stats is not None else None
+        # tuned on what each variant costs here (fused prologue vs apply pass + conv)
+        plan.impl, plan.grid_m = _decision(plan, ck, False, lambda: _tune_fwd(
+            launch_pro, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps, _box_geo(plan)), plan.M, plan.Npad,
+            plan.bn, rows_p, sig=ck + _plan_sig(plan)))
         if pro_ok(plan.impl):
             launch_pro(plan.impl, plan.grid_m)
             return y
+        # the tuned choice for this context is the apply pass + a plain variant (timed as such)
         x = _materialize(x, z_out)
+        _materialized = True
+    else:
+        _materialized = False
     kt, kh, kw = plan.k
     st, sh, sw = plan.s
     pt, ph, pw = plan.p
@@ -689,13 +733,14 @@ def conv_forward_raw(x: torch.Tensor, wp: torch.Tensor, plan: ConvPlan, stats: O
              plan.Kpad, plan.Npad, plan.Cout, plan.bn, plan.bk, grid, plan.wo_override, impl, stream())
 
     rows = stats.numel() // (2 * plan.Npad) if stats is not None else None
-    if plan.impl == 0:
+    if not _materialized:
+        ck = _ctx_key("fwd", "st" if stats is not None else "")
         if x.dtype == torch.uint8:
-            plan.impl = 2
+            plan.impl = plan.pin_f or 2
         else:
-            plan.impl, plan.grid_m = _tune_fwd(launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps,
-                                                                  _box_geo(plan)),
-                                               plan.M, plan.Npad, plan.bn, rows, sig="fwd" + _plan_sig(plan))
+            plan.impl, plan.grid_m = _decision(plan, ck, False, lambda: _tune_fwd(
+                launch, _fwd_impls(plan.bn, plan.Kpad, plan.Cin, plan.taps, _box_geo(plan)), plan.M, plan.Npad,
+                plan.bn, rows, sig=ck + _plan_sig(plan)))
     if rows is not None and rows < plan.grid_m:
         raise ValueError(f"stats holds {rows} partial rows, the tuned grid writes {plan.grid_m} "
                          f"(allocate _stats_rows(M, Npad, bn) rows)")
@@ -723,11 +768,10 @@ def conv_dgrad(dy: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, producer_bn=N
              plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
 
-    if plan.d_impl == 0:
-        plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
-                                                                  _box_geo(plan)),
-                                               md, plan.d_Npad, plan.d_bn,
-                                               sig=("dgradp" if part is not None else "dgrad") + _plan_sig(plan))
+    ck = _ctx_key("dgrad", "p" if part is not None else "")
+    plan.d_impl, plan.d_grid_m = _decision(plan, ck, True, lambda: _tune_fwd(
+        launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps, _box_geo(plan)), md, plan.d_Npad,
+        plan.d_bn, sig=ck + _plan_sig(plan)))
     _launch_tuned(launch, plan.d_impl, plan.d_grid_m, plan.d_bn)
     if part is not None:
         attach_bn_partials(dx, part, plan.d_grid_m, plan.d_Npad)
@@ -741,12 +785,14 @@ def conv_dgrad_bnbwd(dz: torch.Tensor, wd: torch.Tensor, plan: ConvPlan, produce
     the box-tiled dgrad stages that BN's backward dy = k0 * (dz * mask - k1 - xhat * k2) itself
     (y / ss: the BN's raw conv output and constants, coef: milnce_bn_bwd_finalize output) and writes
     dy to ``dy_out`` for the wgrad, so the separate bn_bwd_apply pass (read dz and y, write dy) and
-    the dgrad's read of dy become its reads of dz and y. Requires a box-tiled ``plan.d_impl``."""
+    the dgrad's read of dy become its reads of dz and y. Requires a box-tiled variant: ``impl`` /
+    ``grid``, else the plan's tuned decision for this call context."""
     kt, kh, kw = plan.k
     if dx is None:
         dx = torch.empty((plan.B, plan.T, plan.H, plan.W, plan.Cin_p), dtype=BF16, device=dz.device)
     pt, ph, pw = kt - 1 - plan.p[0], kh - 1 - plan.p[1], kw - 1 - plan.p[2]
-    impl, grid = impl or plan.d_impl, grid or plan.d_grid_m
+    if not impl:
+        impl, grid = _decision(plan, _ctx_key("dgradbn", "p" if producer_bn is not None else ""), True, None)
     part = None
     if producer_bn is not None:
         md = plan.B * plan.T * plan.H * plan.W
@@ -791,10 +837,13 @@ def _tune_dgrad_bnbwd(plan: ConvPlan, dz, weight, y, ss, gamma, part, nparts, ps
              plan.B, plan.To, plan.Ho, plan.Wo, plan.Cout, plan.Cin_p, kt, kh, kw, 1, 1, 1, pt, ph, pw,
              plan.d_Kpad, plan.d_Npad, plan.Cin_p, plan.d_bn, plan.d_bk, grid, 0, impl, stream())
 
-    plan.d_impl, plan.d_grid_m = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps,
-                                                              _box_geo(plan)),
-                                           md, plan.d_Npad, plan.d_bn,
-                                           sig=("dgradbnp" if x_bn is not None else "dgradbn") + _plan_sig(plan))
+    ck = _ctx_key("dgradbn", "p" if x_bn is not None else "")
+    plan.ctx[ck] = _tune_fwd(launch, _fwd_impls(plan.d_bn, plan.d_Kpad, plan.Cout, plan.taps, _box_geo(plan)),
+                             md, plan.d_Npad, plan.d_bn, sig=ck + _plan_sig(plan))
+    _PLAN_EVENTS["contexts"] += 1
+    if not _box_pro3_ok(plan.ctx[ck][0], plan):
+        # the winner is the apply pass + a plain dgrad: that is what the plain dgrad call will run
+        plan.ctx.setdefault(_ctx_key("dgrad", "p" if x_bn is not None else ""), plan.ctx[ck])
 
 
 # MILNCE_BNBWD_FUSE=0 disables. First version measured slower in the step (conv_2c spatial dgrad
@@ -815,9 +864,11 @@ def _box_pro3_ok(impl: int, plan: ConvPlan) -> bool:
     return True
 
 
-def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor) -> bool:
-    """The dgrad can take over this layer's BN-backward apply (``conv_dgrad_bnbwd``)."""
-    return (_BNBWD_FUSE and _PRO_FUSE and _box_pro3_ok(plan.d_impl, plan) and _box_geo(plan) is not None
+def _bnbwd_fusable(plan: ConvPlan, dz: torch.Tensor, ck: str) -> bool:
+    """The dgrad tuned for context ``ck`` takes over this layer's BN-backward apply
+    (``conv_dgrad_bnbwd``)."""
+    impl = plan.pin_d or plan.ctx.get(ck, (0, 0))[0]
+    return (_BNBWD_FUSE and _PRO_FUSE and _box_pro3_ok(impl, plan) and _box_geo(plan) is not None
             and dz.dtype == BF16 and dz.shape[-1] == plan.Cout and plan.Cout % 8 == 0)
 
 
@@ -1160,22 +1211,38 @@ _WGRAD_SIDE_MAX_M = int(os.environ.get("MILNCE_WGRAD_SIDE_MAX_M", "0"))
 # 2537 ms/step with side-stream wgrads vs 491 inline). So wgrads go to the side stream only while
 # the step's peak ALLOCATED memory (not the inflated reserved pool) is below this fraction of the
 # device; checked once per step (max_memory_allocated builds the allocator's stats dict).
+# The peak is the PREVIOUS step's: each step start reads it and resets the counter, so one early
+# spike (the tuning step's flush buffer) does not switch the side stream off for the whole run.
+# Before any step was measured the wgrads run inline (step 0 of a near-capacity config must not
+# take the side-stream regime). The reserved pool is bounded too: above
+# MILNCE_WGRAD_SIDE_RESERVED_FRAC of the device (default 0.85) the cached blocks are released.
 _WGRAD_SIDE_MEM_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_MEM_FRAC", "0.4"))
+_WGRAD_SIDE_RESERVED_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_RESERVED_FRAC", "0.85"))
 _HEADROOM: Dict[int, bool] = {}  # per device, refreshed at each training-step start (zero_arena_begin)
 _DEV_TOTAL: Dict[int, int] = {}
+_HEADROOM_STATS = {"inline_steps": 0, "side_steps": 0, "cache_releases": 0}
 
 
 def _refresh_headroom(device: torch.device) -> None:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     total = _DEV_TOTAL.get(idx)
-    if total is None:
+    first = total is None
+    if first:
         total = _DEV_TOTAL[idx] = torch.cuda.get_device_properties(idx).total_memory
-    _HEADROOM[idx] = torch.cuda.max_memory_allocated(idx) < _WGRAD_SIDE_MEM_FRAC * total
+        # the counter covers whatever ran before the first step (model build, tuning): not a step
+        _HEADROOM[idx] = False
+    else:
+        _HEADROOM[idx] = torch.cuda.max_memory_allocated(idx) < _WGRAD_SIDE_MEM_FRAC * total
+        if torch.cuda.memory_reserved(idx) > _WGRAD_SIDE_RESERVED_FRAC * total:
+            torch.cuda.empty_cache()  # cross-stream frees left the pool inflated (see _SideKeep)
+            _HEADROOM_STATS["cache_releases"] += 1
+    torch.cuda.reset_peak_memory_stats(idx)
+    _HEADROOM_STATS["side_steps" if _HEADROOM[idx] else "inline_steps"] += 1
 
 
 def _side_headroom(device: torch.device) -> bool:
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    return _HEADROOM.get(idx, True)
+    return _HEADROOM.get(idx, False)
 _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 
 
@@ -1418,17 +1485,19 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         with torch.cuda.stream(side):
             if _SIDE_GRID_FRAC < 1.0:
                 _GRID_CU[0] = max(1, int(_NUM_CU * _SIDE_GRID_FRAC))
-            if batched:  # the slab now, its reduction(s) with the next batch (_ReduceBatcher)
-                slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
-                taps = kt * kh * kw
-                dsts = outs if outs is not None else [(0, plan.Cout, dw)]
-                entries = [(ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows, plan.Cin, plan.Cin_p, taps)
-                           for off, rows, g in dsts]
-            elif outs is not None:
-                launch_split()
-            else:
-                launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
-            _GRID_CU[0] = _NUM_CU
+            try:
+                if batched:  # the slab now, its reduction(s) with the next batch (_ReduceBatcher)
+                    slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
+                    taps = kt * kh * kw
+                    dsts = outs if outs is not None else [(0, plan.Cout, dw)]
+                    entries = [(ptr(slab) + off * kpad * 4, ptr(g), splits, npad, kpad, rows, plan.Cin, plan.Cin_p,
+                                taps) for off, rows, g in dsts]
+                elif outs is not None:
+                    launch_split()
+                else:
+                    launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
+            finally:  # later plans key their split geometry on _GRID_CU: never leave it reduced
+                _GRID_CU[0] = _NUM_CU
         if _KEEP_REFS:
             kev = None
             if _KEEP_REFS == 1:
@@ -1598,10 +1667,12 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
         return None, dw, dgamma, dbeta
     dy = torch.empty_like(y)
     dx = None
-    if (lazy is None and fused is not None and ctx.needs_input_grad[0] and plan.d_impl == 0 and _BNBWD_FUSE
-            and _PRO_FUSE and _box_geo(plan) is not None and dz.dtype == BF16 and plan.Cout % 8 == 0):
+    ck = _ctx_key("dgradbn", "p" if ctx.x_bn is not None else "")
+    if (lazy is None and fused is not None and ctx.needs_input_grad[0] and not plan.pin_d and ck not in plan.ctx
+            and _BNBWD_FUSE and _PRO_FUSE and _box_geo(plan) is not None and dz.dtype == BF16
+            and plan.Cout % 8 == 0):
         _tune_dgrad_bnbwd(plan, dz, weight, y, ss, gamma, part, nparts, ps, ctx.x_bn, ctx.training)
-    if lazy is None and fused is not None and ctx.needs_input_grad[0] and _bnbwd_fusable(plan, dz):
+    if lazy is None and fused is not None and ctx.needs_input_grad[0] and _bnbwd_fusable(plan, dz, ck):
         # BN-backward apply inside the dgrad's staging (dy written there for the wgrad)
         call("milnce_bn_bwd_finalize", ptr(part), nparts, ps, C, float(plan.M), ptr(gamma), ptr(ss), ptr(dgamma),
              ptr(dbeta), ptr(coef), int(direct_bn), int(ctx.training), stream())

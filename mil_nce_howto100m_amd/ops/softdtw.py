@@ -52,10 +52,30 @@ def dist_matrix(x: torch.Tensor, y: torch.Tensor, kind: Optional[str]) -> torch.
     yy = (y * y).sum(-1, keepdim=True).transpose(-1, -2)
     sq = torch.clamp(xx + yy - 2.0 * _bmm_t(x, y), min=0.0)
     if kind == "euclidean":
-        return torch.exp(torch.sqrt(sq + 1e-12))
+        return torch.exp(torch.sqrt(_exact_near(sq, x, y, xx + yy) + 1e-12))
     if kind is None or kind == "sqeuclidean":
         return sq
     raise ValueError(f"unknown dist_func {kind}")
+
+
+# the Gram form ||x||^2 + ||y||^2 - 2<x, y> of a squared distance is rounding noise below about
+# this many ulps of the norms' scale (fp32: r = ||x - y|| ~ 3e-3 for unit rows)
+_NEAR_ULPS = 64.0
+
+
+def _exact_near(sq: torch.Tensor, x: torch.Tensor, y: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """``sq`` with the near-duplicate cells (sq at the Gram form's cancellation level) recomputed
+    from the explicit difference sum((x_i - y_j)^2), the reference's form
+    (``soft_dtw_cuda.py:326-335``): there the euclidean exp(||x - y||) has the finite gradient
+    exp(r) (x - y) / r, which a noise-level r would scale arbitrarily. Differentiable (out-of-place
+    index_put); identical rows give sq = 0 and a zero gradient."""
+    near = sq <= _NEAR_ULPS * torch.finfo(sq.dtype).eps * scale
+    if not bool(near.any()):
+        return sq
+    idx = near.nonzero(as_tuple=True)
+    lead, i, j = idx[:-2], idx[-2], idx[-1]
+    diff = x[lead + (i,)] - y[lead + (j,)]
+    return sq.index_put(idx, (diff * diff).sum(-1))
 
 
 # ----------------------------------------------------------------------------------------
@@ -170,8 +190,10 @@ class _SoftDTWHIP(torch.autograd.Function):
         return G, None, None, None
 
 
-# distance functions the HIP kernels apply to the GEMM output in place (csrc/softdtw.hip DistKind)
-_DIST_KIND = {"negative_dot": 1, "cosine": 2, "negative_cosine": 3, None: 4, "sqeuclidean": 4, "euclidean": 5}
+# distance functions the HIP kernels apply to the GEMM output in place (csrc/softdtw.hip DistKind).
+# "euclidean" (DK_EUCLID = 5) is not routed here: its gradient needs the explicit difference at
+# near-duplicate rows (_exact_near), so it runs as dist_matrix + the raw-distance kernels.
+_DIST_KIND = {"negative_dot": 1, "cosine": 2, "negative_cosine": 3, None: 4, "sqeuclidean": 4}
 
 
 class _SoftDTWFusedHIP(torch.autograd.Function):

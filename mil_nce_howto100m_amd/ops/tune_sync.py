@@ -33,7 +33,7 @@ import json
 import os
 from typing import Callable, Dict, Optional
 
-_STATE = {"store": None, "rank": 0, "world": 1, "active": 0, "n": 0, "prefix": "milnce_tune"}
+_STATE = {"store": None, "rank": 0, "world": 1, "active": 0, "n": 0, "prefix": "milnce_tune", "checked": False}
 _HASH = hashlib.sha1()
 _COUNT = [0]
 _ARCH = "gfx950"
@@ -115,7 +115,7 @@ def save_table(path: str = "") -> str:
 
 def configure(store, rank: int, world: int, prefix: str = "milnce_tune") -> None:
     """Use ``store`` (a c10d Store shared by every rank) for decisions inside ``region()``."""
-    _STATE.update(store=store if world > 1 else None, rank=rank, world=world, prefix=prefix)
+    _STATE.update(store=store if world > 1 else None, rank=rank, world=world, prefix=prefix, checked=False)
 
 
 def configure_from_process_group() -> bool:
@@ -145,10 +145,35 @@ def synced() -> bool:
     return _STATE["store"] is not None and _STATE["active"] > 0
 
 
+def _table_digest() -> str:
+    t = _load_table()
+    h = hashlib.sha1(json.dumps(sorted(t.items())).encode()).hexdigest()[:16]
+    return f"{_TABLE['status']}|{h}"
+
+
+def _check_table_consistent() -> None:
+    """Synced tuning numbers its store keys by a counter that only table misses advance, so every
+    rank must see the same table: rank 0 publishes its table status and entry digest, the others
+    compare before their first decision (a different MILNCE_PLAN_TABLE per rank, or a checkout
+    whose csrc/ differs, would otherwise desynchronise the keys: wrong decisions or a hang)."""
+    _STATE["checked"] = True
+    store, key = _STATE["store"], f"{_STATE['prefix']}/table"
+    mine = _table_digest()
+    if _STATE["rank"] == 0:
+        store.set(key, mine)
+        return
+    theirs = store.get(key).decode()
+    if theirs != mine:
+        raise RuntimeError(f"rank {_STATE['rank']}: kernel-plan table {mine!r} differs from rank 0's {theirs!r} "
+                           "(MILNCE_PLAN_TABLE / csrc sources must match on every rank)")
+
+
 def decide(sig: str, tune: Callable[[], int]) -> int:
     """The variant code for problem ``sig``: the plan table's entry, else ``tune()`` here, or rank
     0's choice when synced. A rank-0 ``tune()`` that raises publishes the error, so the other ranks
     raise too instead of waiting for a decision that never comes."""
+    if synced() and not _STATE["checked"]:
+        _check_table_consistent()
     table = _load_table()
     if sig in table:
         value = table[sig]

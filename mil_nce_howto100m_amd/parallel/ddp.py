@@ -196,13 +196,21 @@ class BufferBroadcaster:
     optimizer's flat parameters; the BN kernels update them in place and checkpoint loads copy
     into them), so each step's broadcast is one collective per dtype with no pack / unpack: a
     coalesced broadcast of the ~300 separate S3D-G buffers re-copies every one of them (one small
-    copy launch each) on every step."""
+    copy launch each) on every step.
+
+    Anything that later replaces a buffer tensor (``model.to()``, ``load_state_dict(assign=True)``,
+    a module assigning a new running stat) would detach it from its flat; every call first checks
+    that each buffer still is its view (one pointer compare per buffer) and re-flattens otherwise,
+    so the broadcast never syncs orphaned copies."""
 
     def __init__(self, module: torch.nn.Module, world_size: int, bucket_bytes: int = 32 << 20):
         self.world_size = world_size
         self.bucket_bytes = bucket_bytes
+        self.module = module
         self.bufs = [b for b in module.buffers()]
         self.flats: List[torch.Tensor] = []
+        self.slots: List[tuple] = []  # (owner module, buffer name, expected data_ptr)
+        self.reflattens = 0
         if world_size > 1 and self.bufs:
             self._flatten(module)
 
@@ -211,6 +219,7 @@ class BufferBroadcaster:
         by_dtype: Dict[torch.dtype, list] = {}
         for m, name, b in owners:
             by_dtype.setdefault((b.dtype, b.device), []).append((m, name, b))
+        self.flats, self.slots = [], []
         for (dtype, device), items in by_dtype.items():
             total = sum(b.numel() for _, _, b in items)
             flat = torch.empty(total, dtype=dtype, device=device)
@@ -220,13 +229,20 @@ class BufferBroadcaster:
                 view = flat[off:off + n].view_as(b)
                 view.copy_(b)
                 m._buffers[name] = view
+                self.slots.append((m, name, view.data_ptr()))
                 off += n
             self.flats.append(flat)
         self.bufs = [b for b in module.buffers()]
 
+    def views_intact(self) -> bool:
+        return all(m._buffers.get(name) is not None and m._buffers[name].data_ptr() == p for m, name, p in self.slots)
+
     def __call__(self) -> None:
         if self.world_size <= 1 or not self.bufs:
             return
+        if self.flats and not self.views_intact():
+            self._flatten(self.module)  # a buffer was replaced: its current values move into new flats
+            self.reflattens += 1
         if self.flats:
             for f in self.flats:
                 dist.broadcast(f, 0)

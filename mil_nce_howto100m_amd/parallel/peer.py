@@ -20,24 +20,43 @@ all in flight together, then one completion fence.
   a buffer whose previous contents are still to be read.
 
 ``all_gather_embeddings`` (parallel/dist.py) takes this path with ``--emb_gather peer``; the comm
-probe (parallel/comm_probe.py) times both. Off-node ranks or CPU tensors fall back to
-``dist.all_gather_into_tensor``.
+probe (parallel/comm_probe.py) times both. CPU tensors, and groups whose ranks are not all on
+one node (checked once per group: every rank's host name and boot id, gathered through the
+group), take ``dist.all_gather_into_tensor`` instead: IPC handles cannot be opened across nodes.
 """
 from __future__ import annotations
 
+import socket
 from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
 
 
-def _fence(device: torch.device) -> None:
-    if dist.get_backend() == "nccl":
+def _fence(device: torch.device, group=None) -> None:
+    if dist.get_backend(group) == "nccl":
         t = torch.zeros(1, dtype=torch.float32, device=device)
-        dist.all_reduce(t)  # ordered after this rank's copies on the current stream
+        dist.all_reduce(t, group=group)  # ordered after this rank's copies on the current stream
     else:
         torch.cuda.current_stream(device).synchronize()
-        dist.barrier()
+        dist.barrier(group=group)
+
+
+def _node_id() -> str:
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    return f"{socket.gethostname()}|{boot}"
+
+
+def same_node(group=None) -> bool:
+    """True when every rank of ``group`` runs on this node (collective: call on every rank)."""
+    world = dist.get_world_size(group)
+    ids: List[Optional[str]] = [None] * world
+    dist.all_gather_object(ids, _node_id(), group=group)
+    return len(set(ids)) == 1
 
 
 class PeerAllGather:
@@ -47,6 +66,7 @@ class PeerAllGather:
         self.group = group
         self._bufs: Dict[Tuple, List[List[torch.Tensor]]] = {}  # key -> [parity][rank] buffer views
         self._calls = 0
+        self._local: Optional[bool] = None  # all ranks on one node (decided on the first gather)
 
     def _exchange(self, key, shape, dtype, device) -> List[List[torch.Tensor]]:
         from torch.multiprocessing.reductions import reduce_tensor
@@ -71,7 +91,9 @@ class PeerAllGather:
         world, rank = dist.get_world_size(self.group), dist.get_rank(self.group)
         if world == 1:
             return x.clone()
-        if not x.is_cuda:
+        if self._local is None and x.is_cuda:
+            self._local = same_node(self.group)
+        if not x.is_cuda or not self._local:
             out = x.new_empty((world * x.shape[0],) + tuple(x.shape[1:]))
             dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
             return out
@@ -90,7 +112,7 @@ class PeerAllGather:
         else:
             for r in order:
                 views[p][r][rank].copy_(x, non_blocking=True)
-        _fence(x.device)
+        _fence(x.device, self.group)
         return views[p][rank].reshape((world * x.shape[0],) + tuple(x.shape[1:])).clone()
 
 

@@ -85,7 +85,7 @@ def test_conv_box_matches_reference(case, monkeypatch):
         pytest.skip(f"no box variant for N tiles {plan.bn} / {plan.d_bn} at {geo}")
 
     def run(fi, di, grid_wgs):
-        plan.impl, plan.d_impl = fi, di
+        plan.pin_f, plan.pin_d = fi, di
         plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(fi, plan.bn), grid_wgs)
         plan.d_grid_m = h._grid_for(plan.M, plan.d_Npad, h._box_eff_bn(di, plan.d_bn), grid_wgs)
         y = h.conv_forward_raw(x, wp, plan, stats)
@@ -124,7 +124,7 @@ def test_conv_box_matches_reference(case, monkeypatch):
                     if a is not None and b is not None:
                         assert torch.equal(a, b), (what, i8, i4)
     finally:
-        plan.impl = plan.d_impl = 0
+        plan.pin_f = plan.pin_d = 0
 
 
 def _box_impl(bn, nw=8):
@@ -163,18 +163,18 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k, nw):
             copy.deepcopy(unit)(x.clone().requires_grad_(True)).backward(g)
         # the box-tiled kernel on the temporal conv
         plan = h.conv_plan(tuple(shape) + (cmid,), (cmid, cmid, k[0], 1, 1), (1, 1, 1), (1, 0, 0))
-        plan.impl = _box_impl(plan.bn, nw)
-        if not h._box_ok(plan.bn, cmid, plan.Kpad, plan.impl, h._box_geo(plan)):
+        plan.pin_f = _box_impl(plan.bn, nw)
+        if not h._box_ok(plan.bn, cmid, plan.Kpad, plan.pin_f, h._box_geo(plan)):
             pytest.skip(f"no {nw}-wave box variant for N tile {plan.bn}")
-        plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(plan.impl, plan.bn), 2 if nw == 4 else 1)
+        plan.grid_m = h._grid_for(plan.M, plan.Npad, h._box_eff_bn(plan.pin_f, plan.bn), 2 if nw == 4 else 1)
         # and on the spatial conv's dgrad: its BN backward (dy) is then staged by that dgrad
         # (conv_dgrad_bnbwd, PRO 3) when fused
         plan1 = h.conv_plan(tuple(shape) + (cin,), (cmid, cin, 1, k[1], k[2]), (1, 1, 1), (0, 1, 1))
         if plan1.d_bn <= 128:
-            plan1.d_impl = _box_impl(plan1.d_bn, nw)
-            if not h._box_pro3_ok(plan1.d_impl, plan1):
+            plan1.pin_d = _box_impl(plan1.d_bn, nw)
+            if not h._box_pro3_ok(plan1.pin_d, plan1):
                 pytest.skip(f"the {nw}-wave dgrad of N tile {plan1.d_bn} has no room for the BN prologue")
-            plan1.d_grid_m = h._grid_for(plan1.M, plan1.d_Npad, h._box_eff_bn(plan1.d_impl, plan1.d_bn),
+            plan1.d_grid_m = h._grid_for(plan1.M, plan1.d_Npad, h._box_eff_bn(plan1.pin_d, plan1.d_bn),
                                          2 if nw == 4 else 1)
         for fuse in (False, True, False):
             h._PRO_FUSE = h._BNBWD_FUSE = fuse
@@ -197,6 +197,8 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k, nw):
         assert torch.equal(res[(False, "ng")], res[(True, "ng")])
     finally:
         h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
+        for pl in h._PLANS.values():  # unpin: later tests tune their own contexts
+            pl.pin_f = pl.pin_d = 0
 
 
 def test_prologue_call_on_plan_without_prologue_room():
@@ -223,7 +225,7 @@ def test_prologue_call_on_plan_without_prologue_room():
         for fuse in (False, True):  # tune every other plan first
             h._PRO_FUSE = fuse
             copy.deepcopy(unit)(x.clone().requires_grad_(True)).backward(g)
-        plan.impl = 17
+        plan.pin_f = 17
         plan.grid_m = h._grid_for(plan.M, plan.Npad, 192, 2)
         for fuse in (False, True):
             h._PRO_FUSE = fuse
@@ -238,7 +240,7 @@ def test_prologue_call_on_plan_without_prologue_room():
             assert torch.equal(a[2][n], b[2][n]), n
     finally:
         h._PRO_FUSE = old
-        plan.impl = 0
+        plan.pin_f = 0
 
 
 def test_tuned_4wave_dgrad_without_partial_room_runs_8wave_sibling():
@@ -263,15 +265,15 @@ def test_tuned_4wave_dgrad_without_partial_room_runs_8wave_sibling():
     md = plan.B * plan.T * plan.H * plan.W
     try:
         plan.d_grid_m = h._grid_for(md, plan.d_Npad, 192, 2)
-        plan.d_impl = 17
+        plan.pin_d = 17
         dx4 = h.conv_dgrad(dy, wd, plan)  # no partials: the 4-wave kernel itself
         dx_fb = h.conv_dgrad(dy, wd, plan, (x, ss, c))  # partials: falls back
         p_fb, n_fb, ps = h.take_bn_partials(dx_fb)
-        plan.d_impl = 15
+        plan.pin_d = 15
         dx8 = h.conv_dgrad(dy, wd, plan, (x, ss, c))
         p8, n8, _ = h.take_bn_partials(dx8)
     finally:
-        plan.d_impl = 0
+        plan.pin_d = 0
     assert torch.equal(dx_fb, dx4) and torch.equal(dx_fb, dx8)
     assert n_fb == n8
     s_fb = p_fb[:n8 * 2 * ps].view(n8, 2, ps).double().sum(0)
@@ -308,7 +310,7 @@ def test_inception_head_prologue_fusion():
                 bufs = {n: t.clone() for n, t in b.named_buffers()}
             for cin, cout in ((96, 128), (16, 32)):  # the spatial convs reading z1a / z2a: box-tiled
                 plan = h.conv_plan(tuple(shape) + (cin,), (cout, cin, 1, 3, 3), (1, 1, 1), (0, 1, 1))
-                plan.impl = 15
+                plan.pin_f = 15
             xi.grad = None
             b.zero_grad()
             out = b(xi)

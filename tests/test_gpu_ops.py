@@ -95,7 +95,7 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
     stats = torch.empty((h._stats_rows(plan.M, plan.Npad, plan.bn) * 2 * plan.Npad,), device=DEV)
     outs = {}
     for impl in h._IMPLS:
-        plan.impl = plan.d_impl = impl
+        plan.pin_f = plan.pin_d = impl
         for rep in range(2):
             y = h.conv_forward_raw(x, wp, plan, stats)
             st = stats[:plan.grid_m * 2 * plan.Npad].clone()
@@ -121,7 +121,8 @@ def test_conv_kernel_variants_bitwise_identical(cin, cout, k, p):
             dws.append(h.conv_wgrad(dy, x, plan))
     for d in dws[1:]:
         assert torch.equal(d, dws[0])
-    plan.impl = plan.d_impl = plan.w_impl = 0
+    plan.pin_f = plan.pin_d = plan.w_impl = 0
+    plan.ctx.clear()
 
 
 @pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 192, (3, 1, 1), (1, 0, 0)),
@@ -152,8 +153,8 @@ def test_conv_v4_variants(cin, cout, k, p):
     assert 8 in fw_impls and (cout % 64 != 0 or 8 in dg_impls)
     outs = {}
     for impl in [4] + sorted(set(fw_impls) | set(dg_impls)):
-        plan.impl = impl if (impl == 4 or impl in fw_impls) else 4
-        plan.d_impl = impl if (impl == 4 or impl in dg_impls) else 4
+        plan.pin_f = impl if (impl == 4 or impl in fw_impls) else 4
+        plan.pin_d = impl if (impl == 4 or impl in dg_impls) else 4
         y = h.conv_forward_raw(x, wp, plan, stats)
         st = stats[:plan.grid_m * 2 * plan.Npad].view(plan.grid_m, 2, plan.Npad).double().sum(0)
         dx = h.conv_dgrad(dy, wd, plan, (x, ss, cin))
@@ -171,7 +172,7 @@ def test_conv_v4_variants(cin, cout, k, p):
             assert torch.allclose(pst, ref[3], rtol=1e-4, atol=1e-3), ("partials", impl)
         assert torch.allclose(st, ref[1], rtol=2e-3, atol=1e-1), ("stats", impl)
         assert torch.allclose(pst, ref[3], rtol=2e-2, atol=1.0), ("partials", impl)
-    plan.impl = plan.d_impl = 0
+    plan.pin_f = plan.pin_d = 0
 
 
 @pytest.mark.parametrize("cin,cout,k,p", [(64, 192, (1, 3, 3), (0, 1, 1)), (192, 176, (1, 1, 1), (0, 0, 0)),
@@ -870,10 +871,34 @@ def test_softdtw_vs_cpu_oracle(dist, B, N, M, bw):
     assert rel_err(x.grad.cpu(), xc.grad) < 1e-3 and rel_err(y.grad.cpu(), yc.grad) < 1e-3
 
 
+@pytest.mark.parametrize("r", [1e-3, 3e-4])
+def test_softdtw_euclidean_near_duplicate_rows(r):
+    """Rows at distance r ~ 1e-3 (below the fp32 Gram form's cancellation level): the euclidean
+    exp(||x - y||) gradient exp(r) (x - y) / r comes from the explicit difference there
+    (ops/softdtw.py _exact_near, the reference's form soft_dtw_cuda.py:326-335), so it matches the
+    float64 oracle instead of being a noise-scaled or zeroed subgradient."""
+    from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
+    torch.manual_seed(5)
+    x0 = torch.randn(2, 8, 16) * 0.25
+    u = torch.randn(2, 8, 16)
+    y0 = x0 + r * u / u.norm(dim=-1, keepdim=True)
+    x = x0.to(DEV).requires_grad_(True)
+    y = y0.to(DEV).requires_grad_(True)
+    sd = SoftDTW(True, gamma=0.1, dist_func="euclidean")
+    out = sd(x, y)
+    xc = x0.double().requires_grad_(True)
+    yc = y0.double().requires_grad_(True)
+    outc = sd(xc, yc)
+    assert torch.allclose(out.cpu().double(), outc, rtol=1e-4, atol=1e-4)
+    out.sum().backward()
+    outc.sum().backward()
+    assert rel_err(x.grad.cpu(), xc.grad) < 1e-2 and rel_err(y.grad.cpu(), yc.grad) < 1e-2
+
+
 def test_softdtw_euclidean_normalized_identical_rows():
     """normalize=True puts exactly-zero distances on the xx / yy self cells (and identical rows make
-    x == y cells): the euclidean exp(||x - y||) gradient there is a zero subgradient on the GPU
-    (csrc/softdtw.hip dist_grad), finite and equal to the float64 oracle's."""
+    x == y cells): the explicit difference there is exactly zero, so the euclidean gradient is
+    finite (zero at those cells) and equal to the float64 oracle's."""
     from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
     torch.manual_seed(11)
     base = torch.randn(3, 6, 16) * 0.2

@@ -129,3 +129,25 @@ def test_hard_dtw_runs():
     assert out.shape == (3,) and torch.isfinite(out).all()
     out.mean().backward()
     assert torch.isfinite(x.grad).all()
+
+
+@pytest.mark.parametrize("r", [1e-3, 3e-4])
+def test_softdtw_euclidean_near_duplicate_rows_fp32(r):
+    """Near-duplicate rows (r ~ 1e-3, below the fp32 Gram form's cancellation level): the fp32
+    euclidean soft-DTW value and gradient match float64, because those cells' distances come from
+    the explicit difference (ops/softdtw.py _exact_near; reference soft_dtw_cuda.py:326-335)."""
+    from mil_nce_howto100m_amd.ops.softdtw import SoftDTW
+    torch.manual_seed(5)
+    x0 = torch.randn(2, 8, 16) * 0.25
+    u = torch.randn(2, 8, 16)
+    y0 = x0 + r * u / u.norm(dim=-1, keepdim=True)
+    sd = SoftDTW(False, gamma=0.1, dist_func="euclidean")
+    x, y = x0.clone().requires_grad_(True), y0.clone().requires_grad_(True)
+    out = sd(x, y)
+    out.sum().backward()
+    xc, yc = x0.double().requires_grad_(True), y0.double().requires_grad_(True)
+    outc = sd(xc, yc)
+    outc.sum().backward()
+    assert torch.allclose(out.double(), outc, atol=1e-5)
+    for g, gc in ((x.grad, xc.grad), (y.grad, yc.grad)):
+        assert ((g.double() - gc).norm() / gc.norm()).item() < 1e-4

@@ -90,7 +90,7 @@ def main():
     ss = torch.cat([torch.zeros(o.cin, device="cuda"), torch.ones(o.cin, device="cuda"),
                     torch.ones(o.cin, device="cuda"), torch.zeros(o.cin, device="cuda")])
     prod = (x, ss, o.cin) if o.producer else None
-    plan.impl = plan.d_impl = o.impl
+    plan.pin_f = plan.pin_d = o.impl
     plan.grid_m = h._grid_for(plan.M, plan.Npad, plan.bn, 1)
     plan.d_grid_m = h._grid_for(plan.B * plan.T * plan.H * plan.W, plan.d_Npad, plan.d_bn, 1)
     if o.dir == "fwd":

@@ -54,7 +54,8 @@ def main():
     print(f"{'shape (B,T,H,W,Cin)->Cout k s':58s} {'GFLOP':>7s} {'fwd ms':>7s} {'TF/s':>6s} {'dgr ms':>7s} "
           f"{'TF/s':>6s} {'wgr ms':>7s} {'TF/s':>6s}")
     for key, plan in sorted(hip_ops._PLANS.items(), key=lambda kv: -kv[1].M * kv[1].Cout * kv[1].Ktot):
-        plan.impl = plan.d_impl = plan.w_impl = 0  # re-tune on these operands
+        plan.pin_f = plan.pin_d = plan.w_impl = 0
+    plan.ctx.clear()  # re-tune on these operands
         xs, ws, s, p, _wo = key
         u8 = plan.Cin % 8 != 0
         x = (torch.randint(0, 255, xs, dtype=torch.uint8, device="cuda") if u8

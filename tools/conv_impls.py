@@ -75,7 +75,7 @@ def main():
           f"bk {plan.d_bk}; {fl / 1e9:.0f} GFLOP", flush=True)
     g0, dg0 = plan.grid_m, plan.d_grid_m
     for impl in o.impls:
-        plan.impl = plan.d_impl = impl
+        plan.pin_f = plan.pin_d = impl
         # the 256-row variants hold one workgroup per CU: persistent grid of 1 per CU
         wide = impl in h._V4_WIDE_M
         md = plan.B * plan.T * plan.H * plan.W
