@@ -127,6 +127,27 @@ def test_conv_box_matches_reference(case, monkeypatch):
         plan.pin_f = plan.pin_d = 0
 
 
+def _pin_tuned(h):
+    """Pin every plan to its plain-call decisions (forward with statistics, dgrad with partials
+    first), so two arms that differ only in the fusion flags launch the same variants on the same
+    grids (each call context is tuned on its own, hip_ops._decision). Returns an unpin callable."""
+    for pl in h._PLANS.values():
+        for kinds, dgrad in ((("fwd|st", "fwd", "fwdpro|st|fz", "fwdpro|st|nf"), False),
+                             (("dgrad|p", "dgrad", "dgradbn|p", "dgradbn"), True)):
+            dec = next((pl.ctx[k] for k in kinds if k in pl.ctx), None)
+            if dec is None or (pl.pin_d if dgrad else pl.pin_f):
+                continue
+            if dgrad:
+                pl.pin_d, pl.d_grid_m = dec
+            else:
+                pl.pin_f, pl.grid_m = dec
+
+    def unpin():
+        for pl in h._PLANS.values():
+            pl.pin_f = pl.pin_d = 0
+    return unpin
+
+
 def _box_impl(bn, nw=8):
     if nw == 4:  # (a 192-wide tile with the prologue constants overflows impl 17's 80 KiB: 16 splits it)
         return 17 if bn in (64, 128) else 16
@@ -176,6 +197,7 @@ def test_bn_prologue_fusion_bitwise(shape, cin, cmid, k, nw):
                 pytest.skip(f"the {nw}-wave dgrad of N tile {plan1.d_bn} has no room for the BN prologue")
             plan1.d_grid_m = h._grid_for(plan1.M, plan1.d_Npad, h._box_eff_bn(plan1.pin_d, plan1.d_bn),
                                          2 if nw == 4 else 1)
+        _pin_tuned(h)  # the unit's other kernels: the same variants in every arm
         for fuse in (False, True, False):
             h._PRO_FUSE = h._BNBWD_FUSE = fuse
             u = copy.deepcopy(unit)
@@ -227,6 +249,7 @@ def test_prologue_call_on_plan_without_prologue_room():
             copy.deepcopy(unit)(x.clone().requires_grad_(True)).backward(g)
         plan.pin_f = 17
         plan.grid_m = h._grid_for(plan.M, plan.Npad, 192, 2)
+        unpin = _pin_tuned(h)  # every other kernel the same in both arms
         for fuse in (False, True):
             h._PRO_FUSE = fuse
             u = copy.deepcopy(unit)
@@ -240,7 +263,8 @@ def test_prologue_call_on_plan_without_prologue_room():
             assert torch.equal(a[2][n], b[2][n]), n
     finally:
         h._PRO_FUSE = old
-        plan.pin_f = 0
+        for pl in h._PLANS.values():
+            pl.pin_f = pl.pin_d = 0
 
 
 def test_tuned_4wave_dgrad_without_partial_room_runs_8wave_sibling():
@@ -311,6 +335,7 @@ def test_inception_head_prologue_fusion():
             for cin, cout in ((96, 128), (16, 32)):  # the spatial convs reading z1a / z2a: box-tiled
                 plan = h.conv_plan(tuple(shape) + (cin,), (cout, cin, 1, 3, 3), (1, 1, 1), (0, 1, 1))
                 plan.pin_f = 15
+            _pin_tuned(h)  # the plain-call variants in both arms (each context is tuned on its own)
             xi.grad = None
             b.zero_grad()
             out = b(xi)
@@ -322,6 +347,8 @@ def test_inception_head_prologue_fusion():
             assert _rel(g1[n], g0[n]) < 1e-2, n
     finally:
         h._PRO_FUSE, h._BNBWD_FUSE = old, old_b
+        for pl in h._PLANS.values():
+            pl.pin_f = pl.pin_d = 0
 
 
 @pytest.mark.parametrize("impl", [14, 15, 16, 17])
