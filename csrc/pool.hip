@@ -1309,6 +1309,21 @@ __device__ __forceinline__ uint32_t rcode(const uint2& a, int k, int sh) {
 template <int N>
 using ic = std::integral_constant<int, N>;
 
+// max3 without control flow (bitwise boolean ops: a short-circuit && / || on per-lane values
+// compiles to exec-mask branches)
+__device__ __forceinline__ void max3s(const float* a, bool va, const float* b, const float* c, bool vc, float* out,
+                                      uint32_t* code) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool gb = !va | (b[k] > a[k]);
+    float m = gb ? b[k] : a[k];
+    uint32_t cd = gb ? 1u : 0u;
+    const bool gc = vc & (c[k] > m);
+    out[k] = gc ? c[k] : m;
+    code[k] = gc ? 2u : cd;
+  }
+}
+
 // D = rows whose loads are in flight ahead of the row being processed (a register ring, the
 // sweep unrolled by D so no pending load is ever copied between registers): one row in flight
 // per wave measured 2.5-3.3 TB/s, latency-bound.
@@ -1318,8 +1333,8 @@ __global__ __launch_bounds__(1024) void maxpool_s1_fwd_rows(PoolParams p, int G,
                                                             uint8_t* __restrict__ arg) {
   extern __shared__ uint4 rows_lds[];
   const int n_it = p.T * p.W * G, WG = p.W * G;
-  uint4* xs = rows_lds;          // [n_it] the current input row
-  uint4* m1s = rows_lds + n_it;  // [n_it] its w maxima
+  uint4* xs = rows_lds;              // [n_it + 1] the current input row (slot n_it: idle lanes)
+  uint4* m1s = rows_lds + n_it + 1;  // [n_it + 1] its w maxima
   const int blk = xcd_remap(blockIdx.x, gridDim.x);  // a clip's chunks share lines when G*16 % 128 != 0
   const int b = blk / nchunk, chunk = blk - b * nchunk;
   const int nbytes = p.T * p.H * p.W * p.C * 2;
@@ -1330,7 +1345,13 @@ __global__ __launch_bounds__(1024) void maxpool_s1_fwd_rows(PoolParams p, int G,
   const auto ar = clip_rsrc(arg + (size_t)blk * cbytes, cbytes);
   const uint32_t rowb = (uint32_t)(p.W * p.C * 2), oob = 0x40000000u;
   const RowItem it = row_item(p, G, chunk, threadIdx.x, n_it);
-  const int i = it.i, H = p.H;
+  const int H = p.H;
+  // branch-free: idle lanes work on a dummy slot with no neighbours; their stores go out of range
+  const int i = it.act ? it.i : n_it;
+  const bool wm = it.act && it.w > 0, wp = it.act && it.w + 1 < p.W;
+  const bool tm = it.act && it.t > 0, tp = it.act && it.t + 1 < p.T;
+  const int iwm = wm ? i - G : i, iwp = wp ? i + G : i, itm = tm ? i - WG : i, itp = tp ? i + WG : i;
+  const uint32_t cbase = it.act ? (uint32_t)(i * 8) : oob, crow = (uint32_t)(n_it * 8);
   auto xo = [&](int h) { return h < H ? it.eoff + (uint32_t)h * rowb : oob; };
   uint4 ring[D];
 #pragma unroll
@@ -1339,38 +1360,37 @@ __global__ __launch_bounds__(1024) void maxpool_s1_fwd_rows(PoolParams p, int G,
   // cw | ct << 2)
   uint4 mA = make_uint4(0, 0, 0, 0), mB = mA;
   uint32_t cA = 0, cB = 0;
-  const bool wm = it.w > 0, wp = it.w + 1 < p.W, tm = it.t > 0, tp = it.t + 1 < p.T;
   auto step = [&](auto slot_c, int h) {
     constexpr int slot = decltype(slot_c)::value;
     uint4 mC = make_uint4(0, 0, 0, 0);
     uint32_t cC = 0;
-    if (h < H) {
+    if (h < H) {  // (uniform)
       const uint4 xc = ring[slot];
-      if (it.act) xs[i] = xc;
+      xs[i] = xc;
       ring[slot] = bld16(xr, xo(h + D));
       lds_barrier();
       uint32_t cw = 0;
-      uint4 m1 = xc;
-      if (it.act) {
+      uint4 m1;
+      {
         float a[8], bb[8], c[8], m[8];
         uint32_t cd[8];
-        unpack8(xs[wm ? i - G : i], a);
+        unpack8(xs[iwm], a);
         unpack8(xc, bb);
-        unpack8(xs[wp ? i + G : i], c);
-        max3(a, wm, bb, true, c, wp, m, cd);
+        unpack8(xs[iwp], c);
+        max3s(a, wm, bb, c, wp, m, cd);
         m1 = pack8(m);  // exact: maxima of bf16 values
         m1s[i] = m1;
 #pragma unroll
         for (int j = 0; j < 8; ++j) cw |= cd[j] << (4 * j);
       }
       lds_barrier();
-      if (it.act) {
+      {
         float a[8], bb[8], c[8], m[8];
         uint32_t cd[8];
-        unpack8(m1s[tm ? i - WG : i], a);
+        unpack8(m1s[itm], a);
         unpack8(m1, bb);
-        unpack8(m1s[tp ? i + WG : i], c);
-        max3(a, tm, bb, true, c, tp, m, cd);
+        unpack8(m1s[itp], c);
+        max3s(a, tm, bb, c, tp, m, cd);
         mC = pack8(m);
         cC = cw;
 #pragma unroll
@@ -1383,29 +1403,24 @@ __global__ __launch_bounds__(1024) void maxpool_s1_fwd_rows(PoolParams p, int G,
       unpack8(mA, fa);
       unpack8(mB, fb);
       unpack8(mC, fc);
-      const int t0 = it.t - 1;
       uint32_t lo = 0, hi = 0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        // candidates in row order; a later one wins on a larger value or an earlier frame
-        float m = fb[j];
-        int tmx = t0 + (int)((cB >> (4 * j + 2)) & 3u);
-        uint32_t ch = 1;
-        if (va) {
-          const int ta = t0 + (int)((cA >> (4 * j + 2)) & 3u);
-          if (fa[j] > m || (fa[j] == m && ta <= tmx)) { m = fa[j]; tmx = ta; ch = 0; }
-        }
-        if (vc) {
-          const int tc = t0 + (int)((cC >> (4 * j + 2)) & 3u);
-          if (fc[j] > m || (fc[j] == m && tc < tmx)) { m = fc[j]; ch = 2; }
-        }
-        o[j] = m;
+        // candidates in row order; a later one wins on a larger value or an earlier frame (the
+        // frames compare by their t codes: the three cells share the output's t)
+        const uint32_t ta = (cA >> (4 * j + 2)) & 3u, tb = (cB >> (4 * j + 2)) & 3u, tc = (cC >> (4 * j + 2)) & 3u;
+        const bool pa = va & ((fa[j] > fb[j]) | ((fa[j] == fb[j]) & (ta <= tb)));
+        float m = pa ? fa[j] : fb[j];
+        const uint32_t tm2 = pa ? ta : tb;
+        const bool pc = vc & ((fc[j] > m) | ((fc[j] == m) & (tc < tm2)));
+        o[j] = pc ? fc[j] : m;
+        const uint32_t ch = pc ? 2u : (pa ? 0u : 1u);
         const uint32_t byte = ((cB >> (4 * j)) & 0xFu) | (ch << 4);
         if (j < 4) lo |= byte << (8 * j);
         else hi |= byte << (8 * (j - 4));
       }
       bst16(yr, xo(h - 1), pack8(o));
-      bst8(ar, it.act ? (uint32_t)(((h - 1) * n_it + i) * 8) : oob, make_uint2(lo, hi));
+      bst8(ar, cbase + (uint32_t)(h - 1) * crow, make_uint2(lo, hi));
     }
     mA = mB;
     cA = cB;
@@ -1618,8 +1633,17 @@ static size_t s1_bwd_lds(int rows, int G) { return (size_t)(rows + 1) * G * 80; 
 // kernels (A/B benchmarks only; milnce_set_pool_s1_impl). A tiled forward (band + halo rows in
 // LDS, one barrier, all loads in flight) measured 1.6-2.4 TB/s against the sweep's 2.6-3.4: its
 // h stage is recomputed per t and the VALU work, not memory, bound it (tools/ew_bench.py).
-// 2 = row sweeps (default; a shape they cannot tile takes the plane sweeps).
-static int g_s1_impl = 2;
+// 2 = row sweeps (MILNCE_S1_IMPL=2; a shape they cannot tile takes the plane sweeps). The plane
+// sweeps stay the default: the row sweeps' backward is 9 % faster at the flagship shapes but their
+// forward 23 % slower (tools/pool_bench.py, profiles/r6_pool_rows.md), net +0.1 ms per step.
+static int g_s1_impl = -1;
+static int s1_impl() {
+  if (g_s1_impl < 0) {
+    const char* e = getenv("MILNCE_S1_IMPL");
+    g_s1_impl = e ? atoi(e) : 1;
+  }
+  return g_s1_impl;
+}
 static bool is_s1_333(const PoolParams& p);
 #define HIP_RET_E(expr)                   \
   do {                                    \
@@ -1655,10 +1679,10 @@ static int s1_rows_G(const PoolParams& p) {
   return 0;
 }
 static bool s1_use_rows(const PoolParams& p) {
-  return g_s1_impl == 2 && is_s1_333(p) && s1_rows_G(p) > 0 && (long long)p.T * p.H * p.W * p.C * 2 < (1ll << 30);
+  return s1_impl() == 2 && is_s1_333(p) && s1_rows_G(p) > 0 && (long long)p.T * p.H * p.W * p.C * 2 < (1ll << 30);
 }
 static bool s1_use_lds(const PoolParams& p) {
-  return (g_s1_impl == 1 || (g_s1_impl == 2 && !s1_use_rows(p))) && p.T * p.H <= 512;
+  return (s1_impl() == 1 || (s1_impl() == 2 && !s1_use_rows(p))) && p.T * p.H <= 512;
 }
 // either sweep: arg-max codes in a sweep layout, read by the matching sweep backward only
 static bool s1_sweep(const PoolParams& p) { return is_s1_333(p) && (s1_use_rows(p) || s1_use_lds(p)); }
@@ -1672,7 +1696,7 @@ static hipError_t launch_s1_rows_fwd(const PoolParams& p, long long B, const voi
                                      hipStream_t s) {
   const int G = s1_rows_G(p), nchunk = p.C / 8 / G, n_it = p.T * p.W * G;
   const int nthr = (n_it + 63) / 64 * 64;
-  const size_t lds = (size_t)n_it * 32;
+  const size_t lds = (size_t)(n_it + 1) * 32;
   static int df = -1;
   if (df < 0) {
     HIP_RET_E(lds_attr(maxpool_s1_fwd_rows<1>));
@@ -1715,7 +1739,7 @@ static hipError_t launch_s1_rows_bwd(const PoolParams& p, long long B, const voi
   return hipSuccess;
 }
 MILNCE_API int milnce_set_pool_s1_impl(int impl) {
-  const int old = g_s1_impl;
+  const int old = s1_impl();
   g_s1_impl = impl;
   return old;
 }

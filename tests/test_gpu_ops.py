@@ -466,14 +466,20 @@ def test_maxpool_tf_same_even_plane(shape):
     assert torch.equal(y.float(), yr)
 
 
+@pytest.mark.parametrize("impl", [1, 2])
 @pytest.mark.parametrize("shape", [(2, 16, 25, 9, 16), (3, 4, 13, 13, 56), (2, 2, 7, 7, 832), (1, 3, 1, 5, 8),
-                                   (256, 2, 3, 3, 56), (256, 8, 25, 25, 40)])
-def test_maxpool_s1_lds_shapes(shape):
-    """LDS plane-sweep stride-1 pool: > 256 plane rows (1 group), W=5/H=1, and (batch 256: 2-group
-    workgroups over 7 / 5 channel groups) a partial last channel chunk, whose arg-max codes take a
-    narrower run of the sweep's workgroup-order code layout."""
+                                   (256, 2, 3, 3, 56), (256, 8, 25, 25, 40), (4, 8, 25, 25, 256)])
+def test_maxpool_s1_lds_shapes(shape, impl, request):
+    """Stride-1 pool sweeps (impl 1: LDS plane sweeps, impl 2: row sweeps, csrc/pool.hip): > 256
+    plane rows (1 group), W=5/H=1, and (batch 256: 2-group workgroups over 7 / 5 channel groups) a
+    partial last channel chunk, whose arg-max codes take a narrower run of the sweep's
+    workgroup-order code layout; the flagship Mixed_3c plane. Values bitwise, ties first in
+    (t, h, w) order, gradients to the fp32 reference."""
     torch.manual_seed(12)
     h = hip()
+    from mil_nce_howto100m_amd.ops._lib import lib as _l
+    old = _l().milnce_set_pool_s1_impl(impl)
+    request.addfinalizer(lambda: _l().milnce_set_pool_s1_impl(old))
     x = torch.randn(*shape, device=DEV).to(torch.bfloat16)
     x[0, 0, 0, :2, :8] = 1.0  # ties: first tap in (t, h, w) order wins
     xh = x.clone().requires_grad_(True)

@@ -39,6 +39,7 @@ def rel(a, b):
 
 def main():
     L = lib()
+    old = L.milnce_set_pool_s1_impl(1)
     impls = [2, 1]
     if "--impls" in sys.argv:
         impls = [int(v) for v in sys.argv[sys.argv.index("--impls") + 1].split(",")]
@@ -83,7 +84,7 @@ def main():
             print(f"{str(shp):28s} {names[impl]:6s} {tf * 1e3:8.1f} {tb * 1e3:8.1f} {tu * 1e3:8.1f} "
                   f"{2.5 * nb / tf / 1e6:9.0f} {2.5 * nb / tb / 1e6:9.0f} {4.5 * nb / tu / 1e6:9.0f}  {chk}",
                   flush=True)
-    L.milnce_set_pool_s1_impl(2)
+    L.milnce_set_pool_s1_impl(old)
 
 
 if __name__ == "__main__":
