@@ -72,6 +72,17 @@ def main():
     torch.cuda.synchronize()
     flat_p = torch.cat([p.detach().reshape(-1).float().cpu() for p in tr.model.parameters()])
     torch.save(flat_p, os.path.join(out, f"param_w{W}_r{r}.pt"))
+    # BN buffers through the flat BufferBroadcaster: the train steps (GradCache micro-batches when
+    # CHUNKS > 1) updated them in place through its views; one more broadcast (the next step's
+    # first action) makes every rank hold rank 0's statistics
+    bc = tr.buffers
+    if bc is not None:
+        bc()
+        torch.cuda.synchronize()
+        res["bcast"] = {"flats": len(bc.flats), "intact": bool(bc.views_intact()) if bc.flats else True,
+                        "reflattens": bc.reflattens}
+    bufs = torch.cat([b.detach().reshape(-1).double().cpu() for b in tr.model.buffers()])
+    torch.save(bufs, os.path.join(out, f"bufs_w{W}_r{r}.pt"))
     from mil_nce_howto100m_amd.ops import tune_sync
     res["plan_hash"] = tune_sync.plan_hash()
     res["tune_decisions"] = tune_sync.decisions()

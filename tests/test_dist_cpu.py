@@ -51,7 +51,8 @@ def _worker_gather(rank, world, port, outdir, mode="rccl"):
     from mil_nce_howto100m_amd.parallel.dist import all_gather_embeddings, set_emb_gather
     set_emb_gather(mode)
     if mode == "peer":  # the peer path's host fallback (CPU tensors) keeps the rank-major layout
-        from mil_nce_howto100m_amd.parallel.peer import PeerAllGather
+        from mil_nce_howto100m_amd.parallel.peer import PeerAllGather, same_node
+        assert same_node()  # every rank of this group on one host (the IPC path's precondition)
         got = PeerAllGather().gather(torch.full((3, 2), float(rank)))
         assert torch.equal(got[:, 0], torch.tensor([0.0] * 3 + [1.0] * 3))
     v = torch.full((2, 3), float(rank), requires_grad=True)
@@ -75,6 +76,46 @@ def test_allgather_semantics(mode):
         assert torch.equal(tg, torch.full((4, 3), 3.0))
 
 
+def _worker_negatives(rank, world, port, outdir, mode, b, K):
+    """Each rank's b video rows carry global id rank*b + j, its b*K text rows the id of their clip
+    (candidate k in the fractional part): after the gather, text rows i*K..i*K+K-1 belong to
+    video row i of the global batch (loss.py:12, the MIL-NCE positive block)."""
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.dist import all_gather_embeddings, set_emb_gather
+    set_emb_gather(mode)
+    vid = torch.arange(b, dtype=torch.float32) + rank * b
+    v = vid[:, None].repeat(1, 4).requires_grad_(True)
+    t = (vid[:, None] + torch.arange(K, dtype=torch.float32)[None] / 10).reshape(b * K, 1).repeat(1, 4)
+    t.requires_grad_(True)
+    gv, gt = all_gather_embeddings(v, t, ctx)
+    # a loss that weights every global row by its index: the local-slice backward keeps this
+    # rank's rows only
+    w_v = torch.arange(world * b, dtype=torch.float32)[:, None]
+    w_t = torch.arange(world * b * K, dtype=torch.float32)[:, None]
+    ((gv * w_v).sum() + (gt * w_t).sum()).backward()
+    _put(outdir, rank, (rank, gv.detach(), gt.detach(), v.grad, t.grad))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["rccl", "peer"])
+def test_negatives_rank_major_w8(mode):
+    world, b, K = 8, 3, 4
+    port = _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_negatives, args=(world, port, out, mode, b, K), nprocs=world)
+        res = _collect(out, world)
+    for rank, gv, gt, vg, tg in res:
+        assert gv.shape == (world * b, 4) and gt.shape == (world * b * K, 4)
+        i = torch.arange(world * b, dtype=torch.float32)
+        assert torch.equal(gv[:, 0], i)  # video row i = global clip i, rank-major
+        # text rows i*K .. i*K+K-1 are clip i's K candidates, in order
+        exp_t = (i[:, None] + torch.arange(K, dtype=torch.float32)[None] / 10).reshape(-1)
+        assert torch.allclose(gt[:, 0], exp_t)
+        # local-slice backward: this rank's rows' weights, no cross-rank reduction
+        assert torch.equal(vg[:, 0], torch.arange(rank * b, (rank + 1) * b, dtype=torch.float32))
+        assert torch.equal(tg[:, 0], torch.arange(rank * b * K, (rank + 1) * b * K, dtype=torch.float32))
+
+
 def _worker_grad(rank, world, port, outdir, mode):
     ctx = _init(rank, world, port)
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
@@ -94,7 +135,7 @@ def _worker_grad(rank, world, port, outdir, mode):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode,world", [("reference", 2), ("exact", 2), ("reference", 4)])
+@pytest.mark.parametrize("mode,world", [("reference", 2), ("exact", 2), ("reference", 4), ("reference", 8)])
 def test_dp_gradient_scale(mode, world):
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
     from mil_nce_howto100m_amd.parallel import dist as pdist
@@ -382,3 +423,31 @@ def test_buffer_broadcaster_flat_views():
     a, b = res[0][3], res[1][3]
     assert a.keys() == b.keys() and all(torch.equal(a[k], b[k]) for k in a)
     assert all(int(v.reshape(-1)[0]) == 3 for k, v in a.items() if "num_batches" in k)  # rank 0's
+
+
+def _worker_bcast(rank, world, port, outdir):
+    _init(rank, world, port)
+    from mil_nce_howto100m_amd.parallel.ddp import BufferBroadcaster
+    m = torch.nn.Sequential(torch.nn.BatchNorm1d(3), torch.nn.BatchNorm1d(5))
+    for b in m.buffers():
+        b.fill_(float(rank + 1))
+    bc = BufferBroadcaster(m, world)
+    bc()
+    first = [b.clone() for b in m.buffers()]
+    # replace a buffer tensor (what load_state_dict(assign=True) or .to() does): it leaves the flat
+    m[1].running_mean = torch.full((5,), 10.0 + rank)
+    assert not bc.views_intact()
+    bc()  # re-flattens, then broadcasts rank 0's values into the new buffer too
+    _put(outdir, rank, (first, [b.clone() for b in m.buffers()], bc.reflattens, bc.views_intact()))
+    dist.destroy_process_group()
+
+
+def test_buffer_broadcaster_reflattens_replaced_buffers():
+    world, port = 2, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_bcast, args=(world, port, out), nprocs=world)
+        res = _collect(out, world)
+    for first, after, refl, intact in res:
+        assert all(torch.all(b == 1.0) for b in first)  # rank 0's values everywhere
+        assert refl == 1 and intact
+        assert torch.all(after[3] == 10.0)  # the replaced running_mean: rank 0's new value

@@ -70,6 +70,7 @@ def _run(out, world, chunks, production=False):
 def _load(out, world, r):
     with open(os.path.join(out, f"res_w{world}_r{r}.json")) as f:
         res = json.load(f)
+    res["bufs"] = torch.load(os.path.join(out, f"bufs_w{world}_r{r}.pt"))
     return (res, torch.load(os.path.join(out, f"grad_w{world}_r{r}.pt")),
             torch.load(os.path.join(out, f"param_w{world}_r{r}.pt")))
 
@@ -92,6 +93,11 @@ def test_two_ranks_on_gpu_match_single_process(chunks):
     assert cos > 0.999, cos
     # identical updates on both ranks after real train steps (bucket verifier on)
     assert torch.equal(p20, p21)
+    # the flat BN-buffer broadcast (parallel/ddp.py BufferBroadcaster) through one-shot and GradCache
+    # train steps: the buffers stayed views of its flats and every rank holds rank 0's statistics
+    assert torch.equal(r0["bufs"], r1["bufs"])
+    assert r0["bcast"]["flats"] >= 1 and r0["bcast"]["intact"] and r0["bcast"]["reflattens"] == 0
+    assert r1["bcast"] == r0["bcast"]
     for k in ("train_loss1", "train_loss2"):
         assert r0[k] == r1[k]
     c = r0["comm"]

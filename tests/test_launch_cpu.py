@@ -6,7 +6,7 @@
 * GPU counting for the launcher never initialises HIP (env lists / KFD topology);
 * ``GradBucketer``: every trainable parameter reports ready each step, every bucket
   is issued exactly once, and no gradient lands in a bucket after it was issued (the
-  all-reduce would have read an incomplete slice), at W=2 and W=4, one-shot and GradCache.
+  all-reduce would have read an incomplete slice), at W=2, 4 and 8, one-shot and GradCache.
 """
 import json
 import os
@@ -41,21 +41,24 @@ def _clean_env():
     return env
 
 
-def test_bench_self_launches_n_ranks():
-    cmd = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "1", *TINY]
-    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=_clean_env())
+@pytest.mark.parametrize("world", [2, 8])
+def test_bench_self_launches_n_ranks(world):
+    """bench.py --gpus N as its own launcher: N ranks, one JSON line, the world size observed by
+    torch.distributed; W = 8 is the driver's scaling-run shape (rehearsed on gloo here)."""
+    cmd = [sys.executable, "bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "1", *TINY]
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=900, env=_clean_env())
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, out.stdout  # rank 0 only
     r = json.loads(lines[0])
-    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2"
-    assert r["config"]["backend"] == "gloo" and r["config"]["global_batch"] == 4
+    assert r["n_gpus"] == world and r["config"]["parallelism"] == f"dp{world}"
+    assert r["config"]["backend"] == "gloo" and r["config"]["global_batch"] == 2 * world
     # the step's collectives timed after the timed region (parallel/comm_probe.py)
     c = r["comm"]
-    assert c["world_size"] == 2 and c["buckets"] >= 1 and c["grad_mib"] > 0
+    assert c["world_size"] == world and c["buckets"] >= 1 and c["grad_mib"] > 0
     assert c["allreduce_ms"] > 0 and c["bucketed_allreduce_ms"] > 0 and c["allgather_ms"] > 0
     assert c["allreduce_bf16_ms"] > 0
-    assert c["allgather_kib"] == 2 * 2 * (1 + 4) * 512 * 4 / 1024  # W * b(1+K) rows * 512 fp32
+    assert c["allgather_kib"] == world * 2 * (1 + 4) * 512 * 4 / 1024  # W * b(1+K) rows * 512 fp32
 
 
 def test_bench_world_size_mismatch_fails():
@@ -125,7 +128,7 @@ def _worker_buckets(rank, world, port, outdir, chunks):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,chunks", [(2, 0), (4, 0), (2, 2)])
+@pytest.mark.parametrize("world,chunks", [(2, 0), (4, 0), (2, 2), (8, 0)])
 def test_bucket_readiness_multirank(world, chunks):
     with tempfile.TemporaryDirectory() as out:
         mp.spawn(_worker_buckets, args=(world, _port(), out, chunks), nprocs=world)
