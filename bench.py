@@ -99,6 +99,13 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
+    # A/B knob: the whole step on a high-priority stream (the side stream's weight-gradient
+    # workgroups then lose the dispatch arbitration to the main chain's)
+    prio_ctx = None
+    if cuda and os.environ.get("MILNCE_MAIN_PRIO", "0") == "1":
+        prio_ctx = torch.cuda.stream(torch.cuda.Stream(device=ctx.device, priority=-1))
+        prio_ctx.__enter__()
+
     step = 0
     if opts.warmup == 0 and cuda:
         # setup, not a training step: one forward/backward so per-shape conv autotuning

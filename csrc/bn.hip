@@ -13,13 +13,18 @@
 
 // ---------------------------------------------------------------------------------------
 // Partial-slab reductions ([nparts][2][stride] fp32 -> per-channel fp64 sums). They are
-// latency-bound (a few MB over few channels), so a block is 8 channels x 128 row groups of
-// 1024 threads: each thread sums ~nparts/128 rows with two chains in flight, then a fixed-order
-// LDS tree reduces the 128 groups (deterministic).
+// latency-bound (a few MB over few channels) and sit on the main chain of the backward pass,
+// where the side stream's weight-gradient workgroups hold most of every CU (wave slots, VGPRs,
+// LDS: two 80-KiB temporal-wgrad workgroups fill a CU's LDS). A finalize workgroup that needs
+// 16 waves and 16 KiB (the round-5 shape) waited up to 0.67 ms for a CU to drain; this one is
+// 4 waves with 512 B of LDS: 8 channels x 32 row groups, each thread summing its rows with four
+// loads in flight, a fixed-order butterfly over the wave's row groups, then the 4 waves in order
+// (deterministic).
 #ifndef MILNCE_FIN_RG
-#define MILNCE_FIN_RG 128  // (256-thread finalize workgroups, FIN_RG 32, measured the same: r5)
+#define MILNCE_FIN_RG 32
 #endif
 constexpr int FIN_CH = 8, FIN_RG = MILNCE_FIN_RG;
+static_assert(FIN_RG % 8 == 0 && FIN_RG <= 128, "row groups: whole waves");
 #ifndef MILNCE_BN_U
 #define MILNCE_BN_U 4
 #endif
@@ -27,37 +32,52 @@ constexpr int BN_U = MILNCE_BN_U;  // rows in flight per thread in the streaming
 
 __device__ __forceinline__ void fin_reduce(const float* __restrict__ part, int nparts, int stride, int c, bool ok,
                                            double& s1, double& s2) {
-  __shared__ double red[2][FIN_RG][FIN_CH];
+  constexpr int NWV = FIN_RG / 8;  // waves
+  __shared__ double red[2][NWV][FIN_CH];
   const int cl = threadIdx.x % FIN_CH, rg = threadIdx.x / FIN_CH;
-  double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+  double a[4] = {0.0, 0.0, 0.0, 0.0}, b[4] = {0.0, 0.0, 0.0, 0.0};
   if (ok) {
     int i = rg;
-    for (; i + FIN_RG < nparts; i += 2 * FIN_RG) {
-      const float* p0 = part + (long long)i * 2 * stride + c;
-      const float* p1 = p0 + (long long)FIN_RG * 2 * stride;
-      a1 += (double)p0[0];
-      a2 += (double)p0[stride];
-      b1 += (double)p1[0];
-      b2 += (double)p1[stride];
+    for (; i + 3 * FIN_RG < nparts; i += 4 * FIN_RG) {
+      float u[4], v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float* p0 = part + (long long)(i + k * FIN_RG) * 2 * stride + c;
+        u[k] = p0[0];
+        v[k] = p0[stride];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a[k] += (double)u[k];
+        b[k] += (double)v[k];
+      }
     }
     for (; i < nparts; i += FIN_RG) {
-      a1 += (double)part[(long long)i * 2 * stride + c];
-      a2 += (double)part[(long long)i * 2 * stride + stride + c];
+      a[0] += (double)part[(long long)i * 2 * stride + c];
+      b[0] += (double)part[(long long)i * 2 * stride + stride + c];
     }
   }
-  red[0][rg][cl] = a1 + b1;
-  red[1][rg][cl] = a2 + b2;
-  __syncthreads();
+  double x1 = (a[0] + a[1]) + (a[2] + a[3]), x2 = (b[0] + b[1]) + (b[2] + b[3]);
+  // the wave's 8 row groups (lane bits 3..5): every lane ends with the same fixed-order sum
 #pragma unroll
-  for (int h = FIN_RG / 2; h >= 1; h >>= 1) {
-    if (rg < h) {
-      red[0][rg][cl] += red[0][rg + h][cl];
-      red[1][rg][cl] += red[1][rg + h][cl];
-    }
-    __syncthreads();
+  for (int o = 8; o < 64; o <<= 1) {
+    x1 += __shfl_xor(x1, o, 64);
+    x2 += __shfl_xor(x2, o, 64);
   }
-  s1 = red[0][0][cl];
-  s2 = red[1][0][cl];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) < FIN_CH) {
+    red[0][wv][cl] = x1;
+    red[1][wv][cl] = x2;
+  }
+  __syncthreads();
+  double t1 = 0.0, t2 = 0.0;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) {
+    t1 += red[0][w][cl];
+    t2 += red[1][w][cl];
+  }
+  s1 = t1;
+  s2 = t2;
 }
 
 __device__ __forceinline__ void bn_finalize_body(

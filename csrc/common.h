@@ -177,6 +177,26 @@ static inline float* stream_scratch(size_t floats, hipStream_t stream, int slot)
   return e->buf;
 }
 
+// Minimum LDS bytes per workgroup of the weight-gradient launches (milnce_set_lds_floor; 0 = off):
+// the side-stream wgrads are launched with extra dynamic LDS so that fewer of their workgroups share
+// a CU, leaving LDS for the main chain's kernels (a CU whose LDS the wgrads filled cannot start any
+// workgroup that needs LDS, e.g. a BN finalize or a pool backward: it waits for a wgrad workgroup
+// to retire). Defined in conv.hip.
+extern int g_milnce_lds_floor;
+template <typename K>
+static inline size_t lds_floor(K kernel, size_t dyn) {
+  if (g_milnce_lds_floor <= 0) return dyn;
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, (const void*)kernel) != hipSuccess) return dyn;
+  const size_t total = a.sharedSizeBytes + dyn, floor = (size_t)g_milnce_lds_floor;
+  if (total >= floor || floor > 160 * 1024) return dyn;
+  const size_t want = dyn + (floor - total);
+  if (want > 64 * 1024 &&
+      hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(160 * 1024 - a.sharedSizeBytes)) != hipSuccess)
+    return dyn;
+  return want;
+}
+
 #define HIP_RET(expr)                           \
   do {                                          \
     hipError_t _e = (expr);                     \

@@ -2046,6 +2046,13 @@ __global__ __launch_bounds__(256) void pack_weight_multi_kernel(const PackDesc* 
   }
 }
 
+int g_milnce_lds_floor = 0;
+MILNCE_API int milnce_set_lds_floor(int bytes) {
+  const int old = g_milnce_lds_floor;
+  g_milnce_lds_floor = bytes < 0 ? 0 : bytes;
+  return old;
+}
+
 MILNCE_API int milnce_pack_weights_multi(const void* descs, int n, int total_blocks, hipStream_t stream) {
   if (n <= 0 || total_blocks <= 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pack_weight_multi_kernel, dim3(total_blocks), dim3(256), 0, stream, (const PackDesc*)descs, n);
@@ -2254,7 +2261,8 @@ static int launch_wgrad(WgradParams& p, hipStream_t stream) {
     attr_set = true;
   }
   const int nblocks = p.n_tiles * p.k_tiles * p.splits;
-  hipLaunchKernelGGL((conv_wgrad_kernel<TN_, TK_, U8, DEEP>), dim3(nblocks), dim3(256), lds, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_kernel<TN_, TK_, U8, DEEP>), dim3(nblocks), dim3(256),
+                     lds_floor(conv_wgrad_kernel<TN_, TK_, U8, DEEP>, lds), stream, p);
   return (int)hipGetLastError();
 }
 
@@ -2262,7 +2270,8 @@ template <int TN_, int TK_, int STAGES>
 static int launch_wgrad_v3(WgradParams& p, hipStream_t stream) {
   static_assert((size_t)STAGES * WG_R * (TN_ + TK_) * 2 <= 160 * 1024, "static LDS ring");
   const int nblocks = p.n_tiles * p.k_tiles * p.splits;
-  hipLaunchKernelGGL((conv_wgrad_v3_kernel<TN_, TK_, STAGES>), dim3(nblocks), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL((conv_wgrad_v3_kernel<TN_, TK_, STAGES>), dim3(nblocks), dim3(256),
+                     lds_floor(conv_wgrad_v3_kernel<TN_, TK_, STAGES>, 0), stream, p);
   return (int)hipGetLastError();
 }
 

@@ -370,7 +370,8 @@ int launch_tw(TwParams& p, hipStream_t stream) {
                                 lds));
     attr_set = true;
   }
-  hipLaunchKernelGGL((twgrad_kernel<BN, REG>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT), lds, stream,
+  hipLaunchKernelGGL((twgrad_kernel<BN, REG>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT),
+                     lds_floor(twgrad_kernel<BN, REG>, lds), stream,
                      p);
   return (int)hipGetLastError();
 }

@@ -50,6 +50,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_bn_relu_maxpool_fwd": [P, P, P, P] + [I] * 21 + [P, P],
     "milnce_maxpool_s1_bwd_fused": [P, P, P, P, P, P] + [I] * 5 + [P],
     "milnce_set_pool_s1_impl": [I],
+    "milnce_set_lds_floor": [I],
     "milnce_set_pool_s1_maxthr": [I],
     "milnce_set_pool_s1_codes": [I],
     "milnce_stem_wgrad": [P, P, I, P, L, P, I, I, I, I, I, P],

@@ -201,6 +201,9 @@ _NUM_CU = 256
 # chip to the main chain's kernels
 _GRID_CU = [_NUM_CU]
 _SIDE_GRID_FRAC = float(os.environ.get("MILNCE_SIDE_GRID_FRAC", "1.0"))
+# LDS floor (KiB) per workgroup of the side-stream wgrads (csrc/common.h lds_floor): fewer wgrad
+# workgroups per CU, LDS left for the main chain's kernels. 0 = off.
+_SIDE_LDS_FLOOR = int(float(os.environ.get("MILNCE_SIDE_LDS_FLOOR", "0")) * 1024)
 
 
 _WIDE_BN = (96, 160, 192)  # N tiles served by the LDS-DMA ring kernels only (csrc/conv.hip)
@@ -1204,45 +1207,72 @@ _DEFER_WGRAD = os.environ.get("MILNCE_DEFER_WGRAD", "0") == "1"
 _WGRAD_SIDE = os.environ.get("MILNCE_WGRAD_SIDE", "1") != "0"
 # layers with more output rows than this keep their wgrad on the main stream (A/B knob; 0 = none)
 _WGRAD_SIDE_MAX_M = int(os.environ.get("MILNCE_WGRAD_SIDE_MAX_M", "0"))
-# Memory headroom rule: a side-stream wgrad keeps its operands (dy, x) alive until the side stream
-# passes it, and the cross-stream frees inflate the caching allocator's reserved pool (bs 256:
-# 153 GiB reserved for 27 GiB allocated, 36.5 GiB inline). Near capacity the allocator then keeps
-# missing, frees its cache and retries (BASELINE config 5, 1024 clips x 32 frames, 209 GiB peak:
-# 2537 ms/step with side-stream wgrads vs 491 inline). So wgrads go to the side stream only while
-# the step's peak ALLOCATED memory (not the inflated reserved pool) is below this fraction of the
-# device; checked once per step (max_memory_allocated builds the allocator's stats dict).
-# The peak is the PREVIOUS step's: each step start reads it and resets the counter, so one early
-# spike (the tuning step's flush buffer) does not switch the side stream off for the whole run.
-# Before any step was measured the wgrads run inline (step 0 of a near-capacity config must not
-# take the side-stream regime). The reserved pool is bounded too: above
-# MILNCE_WGRAD_SIDE_RESERVED_FRAC of the device (default 0.85) the cached blocks are released.
+# Side-stream memory policy, decided per training step from the PREVIOUS step's peak allocated
+# memory (each step start reads it and resets the counter; before any step was measured the wgrads
+# run inline: step 0 of a near-capacity config must not take the side-stream regime). A side-stream
+# wgrad's operands (dy, x: main-stream allocations) must stay alive until the side stream passed
+# them, in one of two ways:
+#   "record": Tensor.record_stream -- the caching allocator defers their reuse to an event; its
+#             reserved pool then grows to ~6x the allocated peak (bs 256: 160 GiB reserved for
+#             23 GiB allocated), and near capacity it thrashes (BASELINE config 5 at 2537-6960
+#             ms/step instead of 488 inline);
+#   "keep":   the references are held until the wgrad's event completed (or the backward pass's
+#             drain made the current stream wait for it), _SideKeep: reserved ~= allocated (bs 256:
+#             37.5 GiB reserved for 31.8 allocated; config 5: 2142 pairs/s vs 2098 inline at 248 GiB
+#             peak), at ~0.5-1 % of the bs-256 step (same-box A/Bs, profiles/r6_side_memory.md).
+# Below MILNCE_WGRAD_SIDE_MEM_FRAC (0.4) of the device the step uses "record" (fastest), below
+# MILNCE_WGRAD_SIDE_KEEP_FRAC (0.93) "keep", above it inline; a "keep" step that went above the
+# limit turns the side stream off for the rest of the run (no oscillation near capacity).
+# MILNCE_SIDE_KEEP=1 forces "keep" wherever the side stream is used, =2 releases only at the drain.
+# In "record" mode the reserved pool is bounded too: a step that left more than
+# MILNCE_WGRAD_SIDE_RESERVED_FRAC (0.85) of the device reserved with a quarter of the device cached
+# but unallocated releases the cache.
 _WGRAD_SIDE_MEM_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_MEM_FRAC", "0.4"))
+_WGRAD_SIDE_KEEP_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_KEEP_FRAC", "0.93"))
 _WGRAD_SIDE_RESERVED_FRAC = float(os.environ.get("MILNCE_WGRAD_SIDE_RESERVED_FRAC", "0.85"))
-_HEADROOM: Dict[int, bool] = {}  # per device, refreshed at each training-step start (zero_arena_begin)
+_KEEP_ENV = int(os.environ.get("MILNCE_SIDE_KEEP", "0"))
+_SIDE_MODE: Dict[int, str] = {}  # per device: "inline" | "record" | "keep" (training-step start)
+_KEEP_TRIPPED: Dict[int, bool] = {}
 _DEV_TOTAL: Dict[int, int] = {}
-_HEADROOM_STATS = {"inline_steps": 0, "side_steps": 0, "cache_releases": 0}
+_HEADROOM_STATS = {"inline_steps": 0, "record_steps": 0, "keep_steps": 0, "cache_releases": 0}
 
 
 def _refresh_headroom(device: torch.device) -> None:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     total = _DEV_TOTAL.get(idx)
-    first = total is None
-    if first:
+    if total is None:
         total = _DEV_TOTAL[idx] = torch.cuda.get_device_properties(idx).total_memory
         # the counter covers whatever ran before the first step (model build, tuning): not a step
-        _HEADROOM[idx] = False
+        mode = "inline"
     else:
-        _HEADROOM[idx] = torch.cuda.max_memory_allocated(idx) < _WGRAD_SIDE_MEM_FRAC * total
-        if torch.cuda.memory_reserved(idx) > _WGRAD_SIDE_RESERVED_FRAC * total:
-            torch.cuda.empty_cache()  # cross-stream frees left the pool inflated (see _SideKeep)
+        prev = _SIDE_MODE.get(idx, "inline")
+        peak = torch.cuda.max_memory_allocated(idx)
+        if prev == "keep" and peak >= _WGRAD_SIDE_KEEP_FRAC * total:
+            _KEEP_TRIPPED[idx] = True
+        if peak < _WGRAD_SIDE_MEM_FRAC * total:
+            mode = "keep" if _KEEP_ENV else "record"
+        elif peak < _WGRAD_SIDE_KEEP_FRAC * total and not _KEEP_TRIPPED.get(idx, False):
+            mode = "keep"
+        else:
+            mode = "inline"
+        reserved = torch.cuda.memory_reserved(idx)
+        if prev == "record" and reserved > _WGRAD_SIDE_RESERVED_FRAC * total and reserved - peak > 0.25 * total:
+            torch.cuda.empty_cache()  # cross-stream frees left the pool inflated
             _HEADROOM_STATS["cache_releases"] += 1
+        if mode == "keep" and prev == "record":
+            torch.cuda.empty_cache()  # record_stream's bloat from the earlier steps: keep tracks allocated
+    _SIDE_MODE[idx] = mode
     torch.cuda.reset_peak_memory_stats(idx)
-    _HEADROOM_STATS["side_steps" if _HEADROOM[idx] else "inline_steps"] += 1
+    _HEADROOM_STATS[mode + "_steps"] += 1
+
+
+def _side_mode(device: torch.device) -> str:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _SIDE_MODE.get(idx, "inline")
 
 
 def _side_headroom(device: torch.device) -> bool:
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    return _HEADROOM.get(idx, False)
+    return _side_mode(device) != "inline"
 _SIDE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 
 
@@ -1366,9 +1396,8 @@ class _SideKeep:
 
 
 _SIDE_KEEP = _SideKeep()
-# 0 (default): record_stream; 1: operands released when their event completed or at the drain;
-# 2: only at the drain (no per-wgrad events)
-_KEEP_REFS = int(os.environ.get("MILNCE_SIDE_KEEP", "0"))
+# (the operand lifetime of a side-stream wgrad: _side_mode "record" -> record_stream, "keep" ->
+# released when its event completed or at the drain; MILNCE_SIDE_KEEP=2: only at the drain)
 
 
 def _reduce_on_side(slab: torch.Tensor, dw: torch.Tensor, splits: int, npad: int, kpad: int, plan: ConvPlan,
@@ -1485,6 +1514,8 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
         with torch.cuda.stream(side):
             if _SIDE_GRID_FRAC < 1.0:
                 _GRID_CU[0] = max(1, int(_NUM_CU * _SIDE_GRID_FRAC))
+            if _SIDE_LDS_FLOOR:
+                lib().milnce_set_lds_floor(_SIDE_LDS_FLOOR)
             try:
                 if batched:  # the slab now, its reduction(s) with the next batch (_ReduceBatcher)
                     slab, splits, npad, kpad = launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, None, 1)
@@ -1498,9 +1529,11 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                     launch_with(plan.w_tn, plan.w_impl, plan.w_occ, plan.w_tk, dw, acc)
             finally:  # later plans key their split geometry on _GRID_CU: never leave it reduced
                 _GRID_CU[0] = _NUM_CU
-        if _KEEP_REFS:
+                if _SIDE_LDS_FLOOR:
+                    lib().milnce_set_lds_floor(0)
+        if _side_mode(dy.device) == "keep":
             kev = None
-            if _KEEP_REFS == 1:
+            if _KEEP_ENV != 2:
                 kev = torch.cuda.Event()
                 kev.record(side)
             _SIDE_KEEP.add(kev, (dy, x, xss))
