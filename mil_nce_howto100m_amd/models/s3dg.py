@@ -118,9 +118,24 @@ class InceptionBlock(nn.Module):
                                                       [u.bn1 for u in units], self.training, want_gsum0=gs,
                                                       lazy_out=(False, True, True))
         b0 = (z0, s0)
-        b1 = self.conv_b1_b(z1, want_gsum=gs)
-        b2 = self.conv_b2_b(z2, want_gsum=gs)
-        b3 = self.conv_b3_b(pooled, want_gsum=gs)
+        if ops.branch_streams_enabled(x):
+            # branches 2 and 3 on a second compute stream next to branch 1 (their backward follows
+            # them there); ops.hip_ops "Branch streams"
+            from ..ops import hip_ops
+            main = torch.cuda.current_stream(x.device)
+            side = hip_ops.branch_stream(x.device)
+            side.wait_stream(main)
+            hip_ops.record_on((z2, pooled), side)
+            with torch.cuda.stream(side):
+                b2 = self.conv_b2_b(z2, want_gsum=gs)
+                b3 = self.conv_b3_b(pooled, want_gsum=gs)
+            b1 = self.conv_b1_b(z1, want_gsum=gs)
+            main.wait_stream(side)
+            hip_ops.record_on([t for t in (*b2, *b3) if isinstance(t, torch.Tensor)], main)
+        else:
+            b1 = self.conv_b1_b(z1, want_gsum=gs)
+            b2 = self.conv_b2_b(z2, want_gsum=gs)
+            b3 = self.conv_b3_b(pooled, want_gsum=gs)
         if not g:
             return torch.cat((z0, b1, b2, b3), dim=-1)
         gates = (self.gating_b0, self.gating_b1, self.gating_b2, self.gating_b3)

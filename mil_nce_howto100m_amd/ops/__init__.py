@@ -56,6 +56,11 @@ class force_aten:
         _KEEP_DTYPE = self._prev_keep
 
 
+def branch_streams_enabled(x: torch.Tensor) -> bool:
+    """Inception branches 2 / 3 on a second compute stream (hip_ops "Branch streams")."""
+    return use_hip(x) and _hip().branch_streams_enabled(x)
+
+
 def _hip():
     from . import hip_ops  # imported lazily: loads (and checks) the native library
     return hip_ops

@@ -14,6 +14,12 @@ _ON_DRAIN = []  # run (once) by the next drain before it waits: e.g. hip_ops' ba
 
 
 _AFTER_DRAIN = []  # run by every drain after the current stream waits (persistent registrations)
+_STREAMS = []  # extra compute streams (hip_ops branch streams): joined by every drain / join
+
+
+def add_stream(stream) -> None:
+    if stream not in _STREAMS:
+        _STREAMS.append(stream)
 
 
 def on_drain(fn) -> None:
@@ -51,12 +57,15 @@ def defer(event) -> None:
 def drain() -> None:
     while _ON_DRAIN:
         _ON_DRAIN.pop(0)()
-    if _PENDING:
+    if _PENDING or _STREAMS:
         import torch
         s = torch.cuda.current_stream()
         for e in _PENDING:
             s.wait_event(e)
         _PENDING.clear()
+        for st in _STREAMS:
+            if st != s:
+                s.wait_stream(st)
     for fn in _AFTER_DRAIN:
         fn()
 
@@ -69,6 +78,9 @@ def join(stream) -> None:
         _ON_DRAIN.pop(0)()
     for e in _PENDING:
         stream.wait_event(e)
+    for st in _STREAMS:
+        if st != stream:
+            stream.wait_stream(st)
 
 
 def pending() -> int:

@@ -1006,6 +1006,68 @@ def take_bn_partials(dz: torch.Tensor):
 
 
 # -----------------------------------------------------------------------------------------
+# Branch streams (MILNCE_BRANCH_STREAMS=1): an Inception block's branches 2 and 3 run on a second
+# compute stream next to branch 1 (models/s3dg.py InceptionBlock), and autograd runs their backward
+# on that stream too (PyTorch runs each backward op on its forward op's stream and syncs the
+# gradients between streams). The small 13x13 / 7x7 layers' kernels do not fill the chip alone.
+# Memory: a tensor allocated on one stream and used on another is recorded on the user stream
+# (the caching allocator then defers its reuse): branch inputs / outputs at the fork and join,
+# incoming gradients, lazy-gradient operands and BN partials at backward entry (``adopt``).
+# grad_sink joins the branch stream wherever it joins the side stream (in-place gradient writes).
+_BRANCH = os.environ.get("MILNCE_BRANCH_STREAMS", "0") == "1"
+_BRANCH_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def branch_streams_enabled(x: torch.Tensor) -> bool:
+    return _BRANCH and x.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
+def branch_stream(device: torch.device) -> "torch.cuda.Stream":
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _BRANCH_STREAMS.get(idx)
+    if st is None:
+        st = _BRANCH_STREAMS[idx] = torch.cuda.Stream(device=idx)
+        grad_sink.add_stream(st)
+    return st
+
+
+def _backing(t):
+    """The device tensors a (possibly placeholder) activation / gradient stands for."""
+    out = []
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        return out
+    out.append(t)
+    for attr in ("_milnce_bn",):
+        info = getattr(t, attr, None)
+        if info is not None:
+            out += [v for v in info if isinstance(v, torch.Tensor)]
+    lz = getattr(t, "_milnce_lazydz", None)
+    if lz is not None:
+        out += [v for v in lz if isinstance(v, torch.Tensor)]
+    part = getattr(t, "_milnce_bnpart", None)
+    if part is not None:
+        out.append(part[0])
+    gs = getattr(t, "_milnce_gs", None)
+    if isinstance(gs, torch.Tensor):
+        out.append(gs)
+    return out
+
+
+def record_on(tensors, stream) -> None:
+    """Record every backing tensor of ``tensors`` as used on ``stream``."""
+    for t in tensors:
+        for b in _backing(t):
+            b.record_stream(stream)
+
+
+def adopt(*tensors) -> None:
+    """Backward entry under branch streams: the incoming tensors (possibly allocated on another
+    stream) are used on the current one."""
+    if _BRANCH_STREAMS:
+        record_on(tensors, torch.cuda.current_stream())
+
+
+# -----------------------------------------------------------------------------------------
 # Direct gradient writes. Parameters whose .grad is a view into the data-parallel flat buffer
 # (parallel/ddp.py marks them ``_milnce_flat_grad``) get their weight / BN gradients written
 # (accumulated) in place by the producing kernel instead of being returned to autograd, which
@@ -1666,6 +1728,7 @@ def _conv_bn_backward(ctx, dz, x, weight, y, ss, gamma):
     """Backward of conv -> BN -> ReLU from dz (grad of the ReLU output): BN backward (fused
     partials when the producer of dz attached them), dgrad, wgrad; BN and weight gradients are
     accumulated in place into flat-buffer grads when possible."""
+    adopt(dz)
     plan: ConvPlan = ctx.plan
     lazy = _lazy_dz_info(dz)
     if lazy is None:
@@ -2020,6 +2083,7 @@ def _group_forward(ctx, x, n, training, want_gsum0, hyper, args, extra_saved, la
 def _group_backward(ctx, grads, saved=None):
     """Backward of the fused 1x1 group: returns (dX of the GEMM, the remaining grads tuple)."""
     n, widths, plan = ctx.n, ctx.widths, ctx.plan
+    adopt(*[g for g in grads if g is not None])
     saved = ctx.saved_tensors if saved is None else saved
     x, y = saved[:2]
     sss = saved[2:2 + n]
@@ -2161,6 +2225,8 @@ class _InceptionHead(torch.autograd.Function):
         arg = saved[-1]
         x = saved[0]
         dpooled = grads[-1]
+        if dpooled is not None:
+            adopt(dpooled)
         dx1, rest = _group_backward(ctx, grads[:-1], saved[:-1])
         rest = (None,) + tuple(rest)  # lazy_out
         B, T, H, W, C = x.shape
