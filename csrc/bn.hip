@@ -678,6 +678,101 @@ MILNCE_API int milnce_bn_bwd_gate(const void* dout, int ldo, const float* g, con
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// The BN backward apply of every member of a fused 1x1 group (hip_ops _group_backward) in ONE pass
+// over whole rows: y (the group GEMM's output, ctot channels) and dY (ditto) are read / written as
+// contiguous rows instead of one c-channel slice per member launch (16-96 of 176-384 channels: 32-192
+// B pieces of each row), and the members' dz come from their own sources -- a plain gradient tensor
+// [M][c], or the SelfGating-lazy bf16(dout * g + dmean / thw) of bn_bwd_apply_gate_kernel (same
+// arithmetic and roundings as the per-member kernels, so bitwise the same dY). Grid (splits, B): a
+// block's rows lie in one clip (the gate constants are per clip).
+struct GroupApplyMember {
+  const bf16_t* dz;    // plain: [M][ldz]; lazy gate: the gate output gradient dout (+ channel offset)
+  const float* g;      // lazy gate: g / dmean rows [B][ldg] (+ offset); null: plain
+  const float* dmean;
+  const float* ss;     // [4][c]: mean, invstd, scale, shift
+  const float* coef;   // [3][c]
+  int ldz, ldg, c0, c; // c0: first channel of the member in the group's rows
+};
+static_assert(sizeof(GroupApplyMember) == 56, "GroupApplyMember layout is mirrored by a ctypes.Structure");
+struct GroupApply {
+  GroupApplyMember m[FIN_MAX_MEMBERS];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void bn_bwd_apply_group_kernel(GroupApply ga, const bf16_t* __restrict__ y, int ctot,
+                                                                 float inv_thw, int thw, int rows_per_block,
+                                                                 bf16_t* __restrict__ dy) {
+  const int cpr = ctot >> 3, rpi = 256 / cpr;
+  const int cc = threadIdx.x % cpr, rr = threadIdx.x / cpr;
+  if (rr >= rpi) return;
+  const int ch0 = cc * 8, b = blockIdx.y;
+  int mi = 0;
+  while (mi + 1 < ga.n && ch0 >= ga.m[mi + 1].c0) ++mi;
+  const GroupApplyMember& m = ga.m[mi];
+  const int lc = ch0 - m.c0;  // channel within the member
+  const bool lazy = m.g != nullptr;
+  BnBwdC q[8];
+  float gg[8], dm[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = lc + k;
+    q[k] = bn_bwd_const(m.ss[c], m.ss[m.c + c], m.ss[2 * m.c + c], m.ss[3 * m.c + c], m.coef[c], m.coef[m.c + c],
+                        m.coef[2 * m.c + c]);
+    gg[k] = lazy ? m.g[(size_t)b * m.ldg + c] : 0.f;
+    dm[k] = lazy ? m.dmean[(size_t)b * m.ldg + c] * inv_thw : 0.f;
+  }
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(thw, r_begin + rows_per_block);
+  const size_t row0 = (size_t)b * thw;
+  if (r_begin + rr >= r_end) return;
+  for (int r0 = r_begin + rr; r0 < r_end; r0 += BN_U * rpi) {
+    uint4 dv[BN_U], yv[BN_U];  // whole batch issued before the first use
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const size_t rc = row0 + min(r0 + u * rpi, r_end - 1);
+      dv[u] = *(const uint4*)(m.dz + rc * m.ldz + lc);
+      yv[u] = *(const uint4*)(y + rc * ctot + ch0);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const int r = r0 + u * rpi;
+      if (r >= r_end) break;
+      const size_t row = row0 + r;
+      float d[8], v[8], o[8];
+      unpack8(dv[u], d);
+      unpack8(yv[u], v);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float dz = lazy ? bf2f(f2bf(fmaf(d[k], gg[k], dm[k]))) : d[k];
+        o[k] = bn_bwd_elem(dz, v[k], q[k]);
+      }
+      *(uint4*)(dy + row * ctot + ch0) = pack8(o);
+    }
+  }
+}
+
+// members: host array of n GroupApplyMember (c0 ascending, covering [0, ctot) in multiples of 8)
+MILNCE_API int milnce_bn_bwd_apply_group(const void* members, int n, const void* y, int ctot, int B, int thw,
+                                         void* dy, hipStream_t stream) {
+  if (n < 1 || n > FIN_MAX_MEMBERS || ctot % 8 || ctot > 2048) return (int)hipErrorInvalidValue;
+  GroupApply ga;
+  int c = 0;
+  for (int i = 0; i < n; ++i) {
+    ga.m[i] = ((const GroupApplyMember*)members)[i];
+    if (ga.m[i].c0 != c || ga.m[i].c % 8) return (int)hipErrorInvalidValue;
+    c += ga.m[i].c;
+  }
+  if (c != ctot) return (int)hipErrorInvalidValue;
+  ga.n = n;
+  const int rpi = 256 / (ctot / 8);
+  int splits = (thw + 16 * rpi - 1) / (16 * rpi);  // >= 16 rows per thread
+  if (splits < 1) splits = 1;
+  const int rpb = (thw + splits - 1) / splits;
+  hipLaunchKernelGGL(bn_bwd_apply_group_kernel, dim3(splits, B), dim3(256), 0, stream, ga, (const bf16_t*)y, ctot,
+                     1.f / thw, thw, rpb, (bf16_t*)dy);
+  return (int)hipGetLastError();
+}
+
 // milnce_bn_bwd_gate's apply pass alone (coef already finalized)
 MILNCE_API int milnce_bn_bwd_gate_apply(const void* dout, int ldo, const float* g, const float* dmean, int ldg, int B,
                                         int thw, const void* y, int ldy, const float* ss, const float* coef, int C,

@@ -51,6 +51,7 @@ SIGNATURES: Dict[str, list] = {
     "milnce_maxpool_s1_bwd_fused": [P, P, P, P, P, P] + [I] * 5 + [P],
     "milnce_set_pool_s1_impl": [I],
     "milnce_set_lds_floor": [I],
+    "milnce_bn_bwd_apply_group": [P, I, P, I, I, I, P, P],
     "milnce_set_pool_s1_maxthr": [I],
     "milnce_set_pool_s1_codes": [I],
     "milnce_stem_wgrad": [P, P, I, P, L, P, I, I, I, I, I, P],

@@ -539,6 +539,18 @@ _GROUP_PREPACK = os.environ.get("MILNCE_GROUP_PREPACK", "1") != "0"
 _GROUP_FIN = os.environ.get("MILNCE_GROUP_FIN", "1") != "0"  # one BN-finalize launch per fused 1x1 group
 
 
+class _GroupApplyMember(ctypes.Structure):
+    """Mirror of csrc/bn.hip ``GroupApplyMember`` (56 bytes)."""
+    _fields_ = [("dz", ctypes.c_void_p), ("g", ctypes.c_void_p), ("dmean", ctypes.c_void_p), ("ss", ctypes.c_void_p),
+                ("coef", ctypes.c_void_p), ("ldz", ctypes.c_int), ("ldg", ctypes.c_int), ("c0", ctypes.c_int),
+                ("c", ctypes.c_int)]
+
+
+# the group's BN-backward apply passes as one launch over whole rows (csrc/bn.hip
+# bn_bwd_apply_group_kernel; MILNCE_GROUP_APPLY=0: one launch per member)
+_GROUP_APPLY = os.environ.get("MILNCE_GROUP_APPLY", "1") != "0"
+
+
 class _BwdFinMember(ctypes.Structure):
     """Mirror of csrc/bn.hip ``BwdFinMember`` (72 bytes)."""
     _fields_ = [(f, ctypes.c_void_p) for f in ("part", "gamma", "ss", "dgamma", "dbeta", "coef")] + \
@@ -2127,9 +2139,26 @@ def _group_backward(ctx, grads, saved=None):
              stream())
     dgs, dbs = [], []
     off = 0
+    one_pass = grouped and _GROUP_APPLY and ctot % 8 == 0 and ctot <= 2048
+    if one_pass:
+        arr = (_GroupApplyMember * n)()
+        o = 0
+        thw = plan.To * plan.Ho * plan.Wo
+        for i, (c, (dz, lazy, _, coef, _, _, _)) in enumerate(zip(widths, mem)):
+            if lazy is not None:
+                _, dout, goff, g, dmean, _ = lazy
+                ld = dout.shape[-1]
+                arr[i] = _GroupApplyMember(ptr(dout) + 2 * goff, ptr(g) + 4 * goff, ptr(dmean) + 4 * goff, ptr(sss[i]),
+                                           ptr(coef), ld, ld, o, c)
+            else:
+                arr[i] = _GroupApplyMember(ptr(dz), None, None, ptr(sss[i]), ptr(coef), c, 0, o, c)
+            o += c
+        call("milnce_bn_bwd_apply_group", ctypes.addressof(arr), n, ptr(y2), ctot, plan.B, thw, ptr(dY), stream())
     for i, (c, (dz, lazy, (part, nparts, ps, have_part), coef, dgamma, dbeta, direct_bn)) in enumerate(zip(widths,
                                                                                                        mem)):
-        if grouped and lazy is not None:
+        if one_pass:
+            pass  # applied above
+        elif grouped and lazy is not None:
             _, dout, goff, g, dmean, thw = lazy
             ld = dout.shape[-1]
             call("milnce_bn_bwd_gate_apply", ptr(dout) + 2 * goff, ld, ptr(g) + 4 * goff, ptr(dmean) + 4 * goff, ld,

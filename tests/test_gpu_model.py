@@ -130,7 +130,8 @@ def test_train_step_bitwise_reproducible(merged, monkeypatch):
     cross-workgroup sums are taken in a fixed order (SelfGating sums, gate-backward dots, the
     pools' gate reductions, stem BN statistics: partial rows summed in order, no float atomics).
     With that, the fused 1x1 group's merged launches (member pre-pack, one finalize per group,
-    side-stream wgrad into each member's flat gradient, batched slab reductions) must equal the
+    side-stream wgrad into each member's flat gradient, batched slab reductions, one BN-backward
+    apply pass over the group's whole rows) must equal the
     per-member launches bitwise, too."""
     from mil_nce_howto100m_amd.config import get_args
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
@@ -139,7 +140,7 @@ def test_train_step_bitwise_reproducible(merged, monkeypatch):
                           "--blocks", "mixed_3b,mixed_3c,mixed_4b", "--word2vec_path", "", "--vocab_size", "1000"])
     ctx = pdist.DistContext(device=torch.device("cuda", 0))
     data = SyntheticClips(4, 8, 64, 2, 20, 1000, device=ctx.device)
-    flags = {f: merged for f in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT", "_REDUCE_BATCH")}
+    flags = {f: merged for f in ("_GROUP_FIN", "_GROUP_PREPACK", "_GROUP_WGRAD_DIRECT", "_REDUCE_BATCH", "_GROUP_APPLY")}
     a = _two_train_steps(args, ctx, data, monkeypatch, flags)
     b = _two_train_steps(args, ctx, data, monkeypatch, flags)
     _assert_same(a, b)

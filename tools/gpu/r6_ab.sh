@@ -9,7 +9,7 @@ shift
 mkdir -p $D
 MILNCE_PLAN_TABLE=0 timeout -k 10 300 python bench.py --steps 5 --warmup 3 --save_plan $D/plan.json > $D/tune.log 2>&1 || { tail -20 $D/tune.log; exit 1; }
 export MILNCE_PLAN_TABLE=$D/plan.json
-for r in 1 2; do
+for r in ${AB_ROUNDS:-1 2}; do
   for e in "$@"; do
     echo "== [$e] round $r"
     if [ "$e" = "-" ]; then timeout -k 10 300 python bench.py --steps 20 --warmup 5 | cut -c1-170
