@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Time the Inception branch-3 stride-1 max pool at the flagship shapes (bs 256, 16x200x200 input):
 forward, plain backward and the fused backward of the model (+ the 1x1 head's dX, + the gate
-reduction sum dx * x), for the row sweeps (csrc/pool.hip maxpool_s1_*_rows, impl 2, the default)
-and the plane sweeps (impl 1, both arg-code layouts). Pooled values must agree bitwise between
+reduction sum dx * x), for the row sweeps (csrc/pool.hip maxpool_s1_*_rows, impl 2)
+and the plane sweeps (impl 1, the default). Pooled values must agree bitwise between
 variants (same arg-max); gradients to fp32 rounding (the sweeps sum the scattered gradient in
 different orders). "GB/s" counts the bytes each op must move once.
 
