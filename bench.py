@@ -210,6 +210,8 @@ def main():
             out["plan"]["saved"] = tune_sync.save_table(opts.save_plan)
         if comm is not None:
             out["comm"] = comm
+            if getattr(trainer, "comm_plan", None) is not None:  # --bucket_mb auto (parallel/bucket_plan.py)
+                out["comm"]["bucket_plan"] = trainer.comm_plan.as_dict()
         if cuda:
             out["kernel_lib"] = _native_lib()
         print(json.dumps(out), flush=True)

@@ -23,6 +23,16 @@ SMALL_PRESET = dict(
 )
 
 
+def _bucket_mb(v):
+    """--bucket_mb: a size in MiB, or "auto" (parallel/bucket_plan.py)."""
+    if str(v).lower() == "auto":
+        return "auto"
+    f = float(v)
+    if f <= 0:
+        raise argparse.ArgumentTypeError("--bucket_mb must be > 0 or auto")
+    return f
+
+
 def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description=description)
     # ---- reference flags (args.py:5-49), same names/defaults/dests ----
@@ -88,7 +98,9 @@ def build_parser(description: str = "MILNCE") -> argparse.ArgumentParser:
     g.add_argument("--grad_scale", type=str, default="reference",
                    help="reference: reproduce the 1/world_size gradient scale (utils.py:19-24 + DDP mean); "
                         "exact: full-batch gradient")
-    g.add_argument("--bucket_mb", type=float, default=8.0, help="gradient all-reduce bucket size (MiB)")
+    g.add_argument("--bucket_mb", type=_bucket_mb, default="auto",
+                   help="gradient all-reduce bucket size (MiB), or auto: sized from the all-reduce cost "
+                        "measured on the process group at start-up (parallel/bucket_plan.py)")
     g.add_argument("--grad_comm_dtype", type=str, default="fp32", choices=("fp32", "bf16"),
                    help="gradient all-reduce wire dtype (bf16 halves the bytes, sums in bf16)")
     g.add_argument("--emb_gather", type=str, default="rccl", choices=("rccl", "peer"),

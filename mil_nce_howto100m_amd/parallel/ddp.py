@@ -9,10 +9,11 @@ sized design:
   the ``ops.grad_sink`` notification) marks parameters ready; when a bucket's last
   gradient lands its all-reduce is issued asynchronously (RCCL runs on its own HIP stream,
   ordered after the compute stream by an event), overlapping with the rest of backward;
-* bucket size defaults to 8 MiB: the 45 MB fp32 gradient becomes ~6 collectives. On
-  8x MI355X (7 xGMI links, ~153 GB/s each) a ring step moves size/8 per link, so 8 MiB
-  buckets are ~1 MiB per hop — large enough to be bandwidth- not latency-bound, small
-  enough that the last bucket (the stem, issued after the final backward kernel) is short;
+* bucket sizes: ``bucket_bytes`` per bucket in backward order, and optionally a smaller last
+  bucket of at most ``tail_bytes`` (the first layers, whose gradients land last, so their
+  all-reduce is the exposed one). The trainer's default (``--bucket_mb auto``) takes both from
+  ``parallel/bucket_plan.py``: the all-reduce cost measured on the run's process group at
+  start-up (or the xGMI link model), buckets at 4x the latency knee, the tail at the knee;
 * ``comm_dtype=torch.bfloat16`` (``--grad_comm_dtype bf16``) puts each bucket on the wire as
   bf16 (half the xGMI bytes; the ring then sums in bf16, ~3 significant digits per hop) and
   writes the reduced values back into the fp32 buffer; the default keeps fp32 on the wire;
@@ -45,7 +46,7 @@ class GradBucketer:
 
     def __init__(self, params: Sequence[torch.nn.Parameter], world_size: int,
                  bucket_bytes: int = 8 << 20, process_group=None, verify: Optional[bool] = None,
-                 comm_dtype: torch.dtype = torch.float32):
+                 comm_dtype: torch.dtype = torch.float32, tail_bytes: Optional[int] = None):
         self.verify = (os.environ.get("MILNCE_VERIFY_BUCKETS", "0") == "1") if verify is None else bool(verify)
         self._snap: Dict[int, torch.Tensor] = {}
         self._comm: Dict[int, torch.Tensor] = {}
@@ -64,11 +65,20 @@ class GradBucketer:
         self.buckets: List[List[int]] = []  # list of [start, end)
         self.bucket_of: Dict[int, int] = {}
         self.bucket_size: List[int] = []
+        # the last bucket: the trailing parameters of the backward order (at least one) that fit
+        # in tail_bytes; None: no separate tail
+        tail_start = len(order)
+        if tail_bytes is not None and len(order) > 1:
+            acc = 0
+            while tail_start > 1 and acc + order[tail_start - 1].numel() * 4 <= tail_bytes:
+                tail_start -= 1
+                acc += order[tail_start].numel() * 4
+            tail_start = min(tail_start, len(order) - 1)
         off = 0
         cur_start, cur_count = 0, 0
-        for p in order:
+        for i, p in enumerate(order):
             n = p.numel()
-            if off > cur_start and (off - cur_start + n) * 4 > bucket_bytes:
+            if off > cur_start and ((off - cur_start + n) * 4 > bucket_bytes or i == tail_start):
                 self.buckets.append([cur_start, off])
                 self.bucket_size.append(cur_count)
                 cur_start, cur_count = off, 0

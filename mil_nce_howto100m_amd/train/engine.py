@@ -26,6 +26,7 @@ import torch
 from .. import ops
 from ..losses import build_loss
 from ..models import S3D
+from ..parallel import bucket_plan
 from ..parallel import dist as pdist
 from ..parallel.ddp import BufferBroadcaster, GradBucketer, broadcast_parameters
 from ..utils import StepTimer, Watchdog
@@ -70,7 +71,16 @@ class Trainer:
             self.optimizer = FlatSGD(params, lr=args.lr, momentum=args.momemtum, grad_scale=scale)
         else:
             raise ValueError(args.optimizer)
-        self.bucketer = GradBucketer(params, ctx.world_size, int(getattr(args, "bucket_mb", 8.0) * (1 << 20)),
+        bucket_mb = getattr(args, "bucket_mb", "auto")
+        tail = None
+        if bucket_mb == "auto":  # link-aware sizes (parallel/bucket_plan.py), measured at N > 1
+            grad_bytes = 4 * sum(p.numel() for p in params if p.requires_grad)
+            self.comm_plan = bucket_plan.auto_plan(grad_bytes, ctx.world_size, self.device)
+            bucket_bytes, tail = self.comm_plan.bucket_bytes, self.comm_plan.tail_bytes
+        else:
+            self.comm_plan = None
+            bucket_bytes = int(float(bucket_mb) * (1 << 20))
+        self.bucketer = GradBucketer(params, ctx.world_size, bucket_bytes, tail_bytes=tail,
                                      verify=bool(getattr(args, "verify_buckets", 0)) or None,
                                      comm_dtype=(torch.bfloat16 if getattr(args, "grad_comm_dtype", "fp32") == "bf16"
                                                  else torch.float32))

@@ -451,3 +451,65 @@ def test_buffer_broadcaster_reflattens_replaced_buffers():
         assert all(torch.all(b == 1.0) for b in first)  # rank 0's values everywhere
         assert refl == 1 and intact
         assert torch.all(after[3] == 10.0)  # the replaced running_mean: rank 0's new value
+
+
+def test_bucket_plan_model():
+    """The link model's plan: buckets at 4x the latency knee within [4, 64] MiB and at most half the
+    gradient, the last bucket at the knee (>= 1 MiB); more ranks -> larger latency term."""
+    from mil_nce_howto100m_amd.parallel import bucket_plan as bp
+    MIB = bp.MIB
+    m2, m8 = bp.xgmi_model(2), bp.xgmi_model(8)
+    assert m8.a_s > m2.a_s and m8.knee_bytes > 0
+    for w in (2, 4, 8):
+        p = bp.plan_buckets(45 * MIB, w)
+        assert 1 * MIB <= p.tail_bytes <= p.bucket_bytes <= max(22.5 * MIB, 4 * MIB)
+        assert p.source == "xgmi-model" and p.busbw_gbps > 0
+    # a measured latency-free link: minimum sizes; a slow-latency link: capped at half the gradient
+    fast = bp.LinkModel(0.0, 1e-11, "measured")
+    p = bp.plan_buckets(45 * MIB, 8, fast)
+    assert p.bucket_bytes == 4 * MIB and p.tail_bytes == 1 * MIB
+    slow = bp.LinkModel(1e-3, 1e-11, "measured")
+    p = bp.plan_buckets(45 * MIB, 8, slow)
+    assert p.bucket_bytes == 45 * MIB // 2 and p.tail_bytes == p.bucket_bytes
+
+
+def test_bucketer_tail_bucket():
+    """tail_bytes: the first-registered parameters (backward's last gradients) form the last
+    bucket, at most tail_bytes (at least one parameter); the rest keep the greedy buckets."""
+    from mil_nce_howto100m_amd.parallel.ddp import GradBucketer
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (10, 20, 30, 40, 50)]
+    bk = GradBucketer(ps, 1, bucket_bytes=4 * 60, tail_bytes=4 * 35)
+    # backward order 50, 40, 30, 20, 10: greedy 60-element buckets [50], [40], then the tail
+    # [20 + 10] split off at its start even though [30] alone would have room for 20 more
+    assert bk.buckets == [[0, 50], [50, 90], [90, 120], [120, 150]]
+    bk1 = GradBucketer(ps, 1, bucket_bytes=4 * 60, tail_bytes=4)  # tail smaller than any param
+    assert bk1.buckets[-1] == [140, 150]  # the first parameter alone
+    bk2 = GradBucketer(ps, 1, bucket_bytes=4 * 60)
+    assert bk2.buckets == [[0, 50], [50, 90], [90, 150]]
+
+
+def _worker_autoplan(rank, world, port, outdir):
+    ctx = _init(rank, world, port)
+    from mil_nce_howto100m_amd.train.engine import Trainer, build_model, seed_everything
+    args = _args()
+    assert args.bucket_mb == "auto"
+    seed_everything(1, rank)
+    model = build_model(args, ctx.device)
+    tr = Trainer(args, model, ctx, 10)
+    _put(outdir, rank, (tr.comm_plan.as_dict(), [list(b) for b in tr.bucketer.buckets]))
+    dist.destroy_process_group()
+
+
+def test_auto_bucket_plan_same_on_every_rank():
+    """--bucket_mb auto at W = 4 on gloo: the all-reduce is timed on the process group, and every
+    rank builds the same buckets (a mismatch would pair different slices in the all-reduce)."""
+    world, port = 4, _port()
+    with tempfile.TemporaryDirectory() as out:
+        mp.spawn(_worker_autoplan, args=(world, port, out), nprocs=world)
+        res = _collect(out, world)
+    plan0, buckets0 = res[0]
+    assert plan0["source"] == "measured" and plan0["world_size"] == world
+    assert plan0["tail_bytes"] <= plan0["bucket_bytes"]
+    for plan, buckets in res[1:]:
+        assert buckets == buckets0
+        assert (plan["bucket_bytes"], plan["tail_bytes"]) == (plan0["bucket_bytes"], plan0["tail_bytes"])
