@@ -1,6 +1,6 @@
 """One rank of the on-GPU data-parallel check (tests/test_gpu_dp.py); not a test module.
 
-    python tests/dp_worker.py OUTDIR CHUNKS   (env: RANK, WORLD_SIZE, MASTER_*, MILNCE_DEVICE_INDEX)
+    python tests/dp_worker.py OUTDIR CHUNKS [BUCKET_MB]   (env: RANK, WORLD_SIZE, MASTER_*, MILNCE_DEVICE_INDEX)
 
 Runs the production Trainer on cuda (HIP kernels, direct flat-buffer gradient writes, the
 GradBucketer's async all-reduces, the embedding all-gather) with the ranks sharing one device
@@ -9,7 +9,8 @@ over a gloo process group, and saves what the test compares:
     the loss and the reduced flat gradient of one forward/backward (GradCache CHUNKS > 1 or not);
   * train mode with --verify_buckets 1: two full train_steps (bucket order verifier, fused Adam),
     then the flat parameters, which must be identical on every rank;
-  * at W > 1 the comm probe (parallel/comm_probe.py) on the step's sizes.
+  * at W > 1 the comm probe (parallel/comm_probe.py) on the step's sizes, and the buckets (with
+    BUCKET_MB auto: the start-up plan measured on the process group, parallel/bucket_plan.py).
 World size 1 gets the concatenation of the W=2 shards as its batch (the reference run).
 """
 import json
@@ -24,6 +25,7 @@ import torch  # noqa: E402
 
 def main():
     out, chunks = sys.argv[1], int(sys.argv[2])
+    bucket_mb = sys.argv[3] if len(sys.argv) > 3 else "1"
     from mil_nce_howto100m_amd.config import get_args
     from mil_nce_howto100m_amd.data.synthetic import SyntheticClips
     from mil_nce_howto100m_amd.ops import _lib, hip_ops
@@ -35,7 +37,7 @@ def main():
     b_local = 4
     args = get_args(argv=["--batch_size", str(b_local * W), "--num_frames", "8", "--video_size", "64",
                           "--num_candidates", "2", "--word2vec_path", "", "--warmup_steps", "1",
-                          "--grad_cache_chunks", str(chunks), "--verify_buckets", "1", "--bucket_mb", "1"])
+                          "--grad_cache_chunks", str(chunks), "--verify_buckets", "1", "--bucket_mb", bucket_mb])
     seed_everything(7, r)
     tr = Trainer(args, build_model(args, ctx.device), ctx, 10)
 
@@ -86,6 +88,8 @@ def main():
     from mil_nce_howto100m_amd.ops import tune_sync
     res["plan_hash"] = tune_sync.plan_hash()
     res["tune_decisions"] = tune_sync.decisions()
+    res["buckets"] = [list(b) for b in tr.bucketer.buckets]
+    res["bucket_plan"] = tr.comm_plan.as_dict() if tr.comm_plan is not None else None
     if W > 1:
         from mil_nce_howto100m_amd.parallel.comm_probe import probe
         res["comm"] = probe(tr.bucketer.flat.numel(), tr.bucketer.buckets, b_local * 3, 512, torch.float32,

@@ -52,7 +52,8 @@ def _run(out, world, chunks, production=False):
                     "MILNCE_BOX": "0"})
         if production:  # the bench's kernel set (box-tiled variants included)
             env.pop("MILNCE_BOX")
-        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, out, str(chunks)], env=env,
+        argv = [out, str(chunks)] + (["auto"] if production else [])  # production: the default bucket plan
+        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, *argv], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     for p in procs:
@@ -105,9 +106,10 @@ def test_two_ranks_on_gpu_match_single_process(chunks):
 
 
 def test_two_ranks_production_kernels_rank_consistent():
-    """Production defaults (box-tiled kernels in the tuner, as in bench.py): rank 0 tunes and every
-    rank launches its choices (ops/tune_sync), so both ranks hold the same plan and, after two real
-    train steps, bitwise identical parameters and losses."""
+    """Production defaults (box-tiled kernels in the tuner, the measured bucket plan, as in
+    bench.py): rank 0 tunes and every rank launches its choices (ops/tune_sync), so both ranks hold
+    the same plan and, after two real train steps, bitwise identical parameters and losses
+    (VERDICT r3 item 5)."""
     with tempfile.TemporaryDirectory() as out:
         _run(out, 2, 0, production=True)
         (r0, g0, p0), (r1, g1, p1) = _load(out, 2, 0), _load(out, 2, 1)
@@ -118,3 +120,6 @@ def test_two_ranks_production_kernels_rank_consistent():
     for k in ("train_loss1", "train_loss2"):
         assert r0[k] == r1[k]
     assert torch.equal(p0, p1)
+    # --bucket_mb auto: the plan measured on the process group at start-up, the same buckets on both
+    assert r0["bucket_plan"]["source"] == "measured" and r0["buckets"] == r1["buckets"]
+    assert r0["bucket_plan"]["bucket_bytes"] == r1["bucket_plan"]["bucket_bytes"]
