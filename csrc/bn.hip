@@ -163,10 +163,15 @@ __global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_group_kernel(FinG
 // channel sums can be reduced in LDS and committed with one atomic per channel per block.
 // WRITE = false (bn_relu_gsum_kernel): the SelfGating channel sums only, a read-only reduction
 // (the lazy gate inputs' z is applied by the gate_scale pass / the consumer instead).
-template <bool WRITE>
+// MSTAT (bn_relu_gsum_mstat_kernel, with WRITE = false): also the per-clip mask statistics of this
+// BN, mpart[split][b][2][C] = (sum mask, sum mask * xhat) (mask = y * scale + shift > 0, as the BN
+// backward's), which a gated pool's backward needs for its BN-backward partial sums
+// (gated_pool_bn_partials_kernel).
+template <bool WRITE, bool MSTAT = false>
 __device__ __forceinline__ void bn_relu_apply_body(
     const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
-    int C, int rows_per_b, int rows_per_block, float* __restrict__ part, float* __restrict__ gsum) {
+    int C, int rows_per_b, int rows_per_block, float* __restrict__ part, float* __restrict__ gsum,
+    float* __restrict__ mpart = nullptr) {
   __shared__ float red[256 * 8];
   const int cpr = C >> 3;
   const int rpi = 256 / cpr;  // rows per iteration
@@ -178,11 +183,18 @@ __device__ __forceinline__ void bn_relu_apply_body(
   const int r_end = min(rows_per_b, r_begin + rows_per_block);
   const int c0 = cc * 8;
   float sc[8], sh[8], acc[8];
+  float mu[MSTAT ? 8 : 1], is[MSTAT ? 8 : 1], m0[MSTAT ? 8 : 1], m1[MSTAT ? 8 : 1];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     sc[k] = active ? ss[2 * C + c0 + k] : 0.f;
     sh[k] = active ? ss[3 * C + c0 + k] : 0.f;
     acc[k] = 0.f;
+    if constexpr (MSTAT) {
+      mu[k] = active ? ss[c0 + k] : 0.f;
+      is[k] = active ? ss[C + c0 + k] : 0.f;
+      m0[k] = 0.f;
+      m1[k] = 0.f;
+    }
   }
   if (active && r_begin + rr < r_end) {
     const long long base = (long long)b * rows_per_b;
@@ -201,6 +213,11 @@ __device__ __forceinline__ void bn_relu_apply_body(
         unpack8(v[u], f);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
+          if constexpr (MSTAT) {
+            const bool m = f[k] * sc[k] + sh[k] > 0.f;
+            m0[k] += m ? 1.f : 0.f;
+            m1[k] += m ? (f[k] - mu[k]) * is[k] : 0.f;
+          }
           f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
           acc[k] += f[k];
         }
@@ -225,14 +242,34 @@ __device__ __forceinline__ void bn_relu_apply_body(
       else atomicAdd(gsum + (long long)b * C + c0 + k, s);
     }
   }
+  if constexpr (MSTAT) {  // the mask sums the same way, one [2][C] row per (split, clip)
+    float* __restrict__ mr = mpart + ((long long)blockIdx.x * gridDim.y + b) * 2 * C + c0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // red's previous readers are done
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[k * 256 + tid] = h == 0 ? m0[k] : m1[k];
+      __syncthreads();
+      if (rr == 0 && active) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          float v = h == 0 ? m0[k] : m1[k];
+          for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
+          mr[h * C + k] = v;
+        }
+      }
+    }
+  }
 }
 
-// gsum[i] += sum over s < nsplit of part[s * n + i], in split order (deterministic gating sums)
-__global__ void bn_gsum_sum_kernel(float* __restrict__ gsum, const float* __restrict__ part, int nsplit, long long n) {
+// gsum[i] (+)= sum over s < nsplit of part[s * n + i], in split order (deterministic gating sums);
+// add = 0: overwrite
+__global__ void bn_gsum_sum_kernel(float* __restrict__ gsum, const float* __restrict__ part, int nsplit, long long n,
+                                   int add = 1) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     float v = part[i];
     for (int sp = 1; sp < nsplit; ++sp) v += part[(long long)sp * n + i];
-    gsum[i] += v;
+    gsum[i] = add ? gsum[i] + v : v;
   }
 }
 
@@ -246,6 +283,90 @@ __global__ __launch_bounds__(256) void bn_relu_gsum_kernel(
     const bf16_t* __restrict__ y, int ldy, const float* __restrict__ ss, int C, int rows_per_b,
     int rows_per_block, float* __restrict__ part, float* __restrict__ gsum) {
   bn_relu_apply_body<false>(y, ldy, nullptr, 0, ss, C, rows_per_b, rows_per_block, part, gsum);
+}
+
+__global__ __launch_bounds__(256) void bn_relu_gsum_mstat_kernel(
+    const bf16_t* __restrict__ y, int ldy, const float* __restrict__ ss, int C, int rows_per_b,
+    int rows_per_block, float* __restrict__ part, float* __restrict__ gsum, float* __restrict__ mpart) {
+  bn_relu_apply_body<false, true>(y, ldy, nullptr, 0, ss, C, rows_per_b, rows_per_block, part, gsum, mpart);
+}
+
+// BN-backward partial sums of a SelfGating + TF-SAME max pool's input BN, taken over the POOLED
+// tensors (hip_ops _GatedPool): the BN layer's dz = dx * g + dmean / thw, with dx the pool-routed
+// gradient (nonzero only at arg-max cells), so
+//   sum_cells dz mask (1, xhat) = sum_o dout_o g mask(yr_o) (1, xhat(yr_o)) + dmean / thw (S0, S1)
+// where yr is the raw conv output at each output's arg-max (written by the pool forward) and S0 / S1
+// the per-clip sums of mask and mask * xhat over all cells (mstat, from the forward's gating-sum
+// pass) -- the full-resolution gather pass over dout, the arg-max codes and the raw conv output
+// is not needed. (The per-cell dz of the old pass was rounded to bf16 before the sums; these sum
+// its fp32 value.) Grid (splits, B): part[(split * B + b)][2][C]; split 0 adds the dmean term.
+__global__ __launch_bounds__(256) void gated_pool_bn_partials_kernel(
+    const bf16_t* __restrict__ dout, const bf16_t* __restrict__ yr, const float* __restrict__ g,
+    const float* __restrict__ dmean, const float* __restrict__ ss, const float* __restrict__ mstat, int C,
+    int rows_per_b, int rows_per_block, float inv_thw, float* __restrict__ part) {
+  __shared__ float red[256 * 8];
+  const int cpr = C >> 3, rpi = 256 / cpr;
+  const int tid = threadIdx.x, cc = tid % cpr, rr = tid / cpr;
+  const bool active = rr < rpi;
+  const int b = blockIdx.y, c0 = cc * 8;
+  const int r_begin = blockIdx.x * rows_per_block, r_end = min(rows_per_b, r_begin + rows_per_block);
+  float gg[8], mu[8], is[8], sc[8], sh[8], a1[8], a2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = active ? c0 + k : 0;
+    gg[k] = g[(long long)b * C + c];
+    mu[k] = ss[c];
+    is[k] = ss[C + c];
+    sc[k] = ss[2 * C + c];
+    sh[k] = ss[3 * C + c];
+    a1[k] = 0.f;
+    a2[k] = 0.f;
+  }
+  if (active && r_begin + rr < r_end) {
+    const long long base = (long long)b * rows_per_b;
+    for (int r0 = r_begin + rr; r0 < r_end; r0 += BN_U * rpi) {
+      uint4 dv[BN_U], yv[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long long row = base + min(r0 + u * rpi, r_end - 1);
+        dv[u] = *(const uint4*)(dout + row * C + c0);
+        yv[u] = *(const uint4*)(yr + row * C + c0);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        if (r0 + u * rpi >= r_end) break;
+        float d[8], v[8];
+        unpack8(dv[u], d);
+        unpack8(yv[u], v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float gm = (v[k] * sc[k] + sh[k] > 0.f) ? d[k] * gg[k] : 0.f;
+          a1[k] += gm;
+          a2[k] += gm * (v[k] - mu[k]) * is[k];
+        }
+      }
+    }
+  }
+  float* __restrict__ pr = part + ((long long)blockIdx.x * gridDim.y + b) * 2 * C + c0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[k * 256 + tid] = h == 0 ? a1[k] : a2[k];
+    __syncthreads();
+    if (rr == 0 && active) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = h == 0 ? a1[k] : a2[k];
+        for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
+        if (blockIdx.x == 0) {
+          const long long i = (long long)b * C + c0 + k;
+          v += dmean[i] * inv_thw * mstat[((long long)b * 2 + h) * C + c0 + k];
+        }
+        pr[h * C + k] = v;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -469,8 +590,44 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
   if (part != nullptr) {
     const long long g = (n + 255) / 256;
     hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, gsum, part,
-                       splits, n);
+                       splits, n, 1);
   }
+  return (int)hipGetLastError();
+}
+
+// milnce_bn_relu_apply's gating-sums-only pass (z not written) that also leaves the per-clip mask
+// statistics mstat [B][2][C] = (sum mask, sum mask * xhat) (overwritten); gsum [B][C] is added to.
+// Not inside a HIP graph capture (the deterministic partial rows need the stream scratch).
+MILNCE_API int milnce_bn_relu_gsum_mstat(const void* y, int ldy, const float* ss, int C, int B, int rows_per_b,
+                                         float* gsum, float* mstat, hipStream_t stream) {
+  if (C % 8 || C > 2048 || gsum == nullptr || mstat == nullptr) return (int)hipErrorInvalidValue;
+  const int splits = pick_splits(rows_per_b, 4 * BN_U * (256 / (C / 8)));
+  const int rpb = (rows_per_b + splits - 1) / splits;
+  const long long n = (long long)B * C;
+  float* part = stream_scratch((size_t)splits * n * 3, stream, SCRATCH_BN_GSUM);
+  if (part == nullptr) return (int)hipErrorInvalidValue;
+  float* mpart = part + (size_t)splits * n;
+  hipLaunchKernelGGL(bn_relu_gsum_mstat_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)y, ldy, ss, C,
+                     rows_per_b, rpb, part, gsum, mpart);
+  long long g = (n + 255) / 256;
+  hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, gsum, part, splits,
+                     n, 1);
+  g = (2 * n + 255) / 256;
+  hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, mstat, mpart,
+                     splits, 2 * n, 0);
+  return (int)hipGetLastError();
+}
+
+// BN-backward partials of a gated pool's input BN from the pooled side (gated_pool_bn_partials_kernel):
+// dout / yr [B][rows_per_b][C] (pooled), g / dmean [B][C], ss [4][C], mstat [B][2][C], thw the
+// full-resolution positions per clip; part [splits * B][2][C].
+MILNCE_API int milnce_gated_pool_bn_partials(const void* dout, const void* yr, const float* g, const float* dmean,
+                                             const float* ss, const float* mstat, int C, int B, int rows_per_b,
+                                             int thw, int splits, float* part, hipStream_t stream) {
+  if (C % 8 || C > 2048 || splits < 1 || rows_per_b < 1 || thw < 1) return (int)hipErrorInvalidValue;
+  const int rpb = (rows_per_b + splits - 1) / splits;
+  hipLaunchKernelGGL(gated_pool_bn_partials_kernel, dim3(splits, B), dim3(256), 0, stream, (const bf16_t*)dout,
+                     (const bf16_t*)yr, g, dmean, ss, mstat, C, rows_per_b, rpb, 1.f / thw, part);
   return (int)hipGetLastError();
 }
 

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
     for (int t = 0; t < KT * KH * KW; ++t) {
       float f[8], raw[8];
       unpack8(v[t], f);
-      if constexpr (BN && !GATE) {
+      if constexpr (BN) {
         // yr: the raw conv output at each arg-max (any real window cell when the maximum is a zero
         // pad candidate: every real cell's z is 0 then, so its BN mask is off like the pad's)
 #pragma unroll
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
         const bool gt = val > best[k];
         best[k] = gt ? val : best[k];
         bi[k] = gt ? (uint32_t)t : bi[k];
-        if constexpr (BN && !GATE) braw[k] = ((gt && in[t]) || (in[t] && !have_real)) ? raw[k] : braw[k];
+        if constexpr (BN) braw[k] = ((gt && in[t]) || (in[t] && !have_real)) ? raw[k] : braw[k];
       }
       have_real |= in[t];
     }
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_t(PoolParams p, PoolDivs d, c
     a.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | (bi[3] << 24);
     a.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | (bi[7] << 24);
     *(uint2*)(arg + o) = a;
-    if constexpr (BN && !GATE) {
+    if constexpr (BN) {
       if (yr != nullptr) *(uint4*)(yr + o) = pack8(braw);  // exact: bf16 values
     }
   }
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(256) void maxpool_fwd_pair(PoolParams p, PoolDivs d
                                                         const float* __restrict__ ss = nullptr,
                                                         const float* __restrict__ gate = nullptr,
                                                         bf16_t* __restrict__ yr = nullptr) {
-  constexpr bool YR = BN && !GATE;
+  constexpr bool YR = BN;  // the raw value at each arg-max (yr), when asked for
   const FastDiv fWq = d.fmw;  // Wq, set by the launcher
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < npair_chunks; i += gridDim.x * blockDim.x) {
     const uint32_t r = fdiv(i, d.fcpr);
@@ -1835,7 +1835,7 @@ static bool pool_fwd_special(const PoolParams& p, const void* x, void* y, void* 
     if (p.kt == a && p.kh == b && p.kw == c && p.st == e && p.sh == f && p.sw == h) {                            \
       if (gate != nullptr)                                                                                           \
         hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, true>), dim3(grid), dim3(256), 0, s, p, d,     \
-                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate);               \
+                           (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, gate, (bf16_t*)yr);  \
       else                                                                                                       \
         hipLaunchKernelGGL((maxpool_fwd_t<a, b, c, e, f, h, true, false>), dim3(grid), dim3(256), 0, s, p, d,    \
                            (const bf16_t*)x, (bf16_t*)y, (uint8_t*)arg, (uint32_t)n, bn_ss, nullptr,             \
@@ -2099,14 +2099,16 @@ MILNCE_API int milnce_maxpool_bwd_gate(const void* dy, const void* arg, void* dx
 // SelfGating of a lazy BN-ReLU input followed by a TF-SAME max pool, in one pass over the raw conv
 // output x: pools bf16(bf16(relu(x * scale + shift)) * gate[b, c]), the gate output the unfused ops
 // would store (specialised window shapes only).
+// yr (optional, pooled shape): the raw conv output x at each output's arg-max, so the BN-backward
+// partial sums of x's BN can be taken over the pooled tensors (milnce_gated_pool_bn_partials).
 MILNCE_API int milnce_bn_relu_gate_maxpool_fwd(const void* x, const float* ss, const float* gate, void* y, void* arg,
                                                int B, int T, int H, int W, int C, int To, int Ho, int Wo, int kt,
                                                int kh, int kw, int st, int sh, int sw, int pt0, int pt1, int ph0,
-                                               int ph1, int pw0, int pw1, int zero_pad, hipStream_t stream) {
+                                               int ph1, int pw0, int pw1, int zero_pad, void* yr, hipStream_t stream) {
   if (C % 8 || gate == nullptr) return (int)hipErrorInvalidValue;
   PoolParams p = make_pool(T, H, W, C, To, Ho, Wo, kt, kh, kw, st, sh, sw, pt0, pt1, ph0, ph1, pw0, pw1, zero_pad);
   const long long n = (long long)B * To * Ho * Wo * (C / 8);
-  if (!pool_fwd_special(p, x, y, arg, n, stream, ss, gate)) return (int)hipErrorInvalidValue;
+  if (!pool_fwd_special(p, x, y, arg, n, stream, ss, gate, yr)) return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
 

@@ -58,7 +58,9 @@ SIGNATURES: Dict[str, list] = {
     "milnce_stem_wgrad_pool": [P, P, P, P, P, P, I, P, L, P, I, I, I, I, I, P],
     "milnce_stem_fwd": [P, I, P, I, P, P, L, P, I, I, I, I, P],
     "milnce_maxpool_bwd_gate": [P, P, P] + [I] * 21 + [P, P, I, P],
-    "milnce_bn_relu_gate_maxpool_fwd": [P, P, P, P, P] + [I] * 21 + [P],
+    "milnce_bn_relu_gate_maxpool_fwd": [P, P, P, P, P] + [I] * 21 + [P, P],
+    "milnce_bn_relu_gsum_mstat": [P, I, P, I, I, I, P, P, P],
+    "milnce_gated_pool_bn_partials": [P, P, P, P, P, P, I, I, I, I, I, P, P],
     "milnce_maxpool_bwd_gated": [P, P, P] + [I] * 21 + [P, I, P, P, I, P, P, P],
     "milnce_maxpool_bwd_apply": [P, P, P] + [I] * 21 + [P, I, P, P, P, P, I, P],
     "milnce_gate_dot": [P, P, I, I, I, P, P],

@@ -918,6 +918,13 @@ _LAZY_POOL_DZ = os.environ.get("MILNCE_LAZY_POOL_DZ", "1") != "0"
 # the same sums over the full-resolution dz -- and the partials-only gather pass over the stem
 # output (dout, arg-max and the 2.6 GB stem output read) disappears. MILNCE_POOL_YR=0 disables.
 _POOL_YR = os.environ.get("MILNCE_POOL_YR", "1") != "0"
+# The same for the gated maxpool_3a (conv_2c -> SelfGating -> pool, _GatedPool): its input BN's
+# dz = dx * g + dmean / thw is nonzero at every cell, so its partial sums are the pooled-side sums
+# over (dout * g, yr) plus dmean / thw times the per-clip mask statistics (sum mask, sum mask *
+# xhat), which the forward's gating-sum pass takes from the same read of y
+# (milnce_bn_relu_gsum_mstat) -- one pass over the pooled tensors replaces the full-resolution
+# partials gather (dout, codes, 2 GB of y). MILNCE_GATED_POOL_STATS=0 disables.
+_GATED_POOL_STATS = os.environ.get("MILNCE_GATED_POOL_STATS", "1") != "0"
 
 
 def _lazy_z(shape, device, bn_info) -> torch.Tensor:
@@ -1836,6 +1843,13 @@ class _ConvBNReLU(torch.autograd.Function):
             z = _lazy_z(y.shape, y.device, (y, ss, C)) if lazy else torch.empty_like(y)
             if lazy and _defer_gsum(want_gsum):
                 gsum._milnce_gsum_deferred = True  # summed with the block's other branches (gate_concat)
+            elif (lazy and _GATED_POOL_STATS and training and C <= 2048
+                  and not torch.cuda.is_current_stream_capturing()):
+                # a single-branch SelfGating (conv_2c -> gated maxpool_3a): also the mask statistics
+                mstat = torch.empty((plan.B, 2, C), dtype=F32, device=x.device)
+                call("milnce_bn_relu_gsum_mstat", ptr(y), C, ptr(ss), C, plan.B, plan.To * plan.Ho * plan.Wo,
+                     ptr(gsum), ptr(mstat), stream())
+                gsum._milnce_mstat = mstat
             else:
                 call("milnce_bn_relu_apply", ptr(y), C, None if lazy else ptr(z), C, ptr(ss), C, plan.B,
                      plan.To * plan.Ho * plan.Wo, ptr(gsum), stream())
@@ -2547,15 +2561,20 @@ class _GatedPool(torch.autograd.Function):
         arg = torch.empty((B, To, Ho, Wo, C), dtype=torch.uint8, device=dev)
         geo = [B, T, H, W, C, To, Ho, Wo, *kernel, *stride, pads[0][0], pads[0][1], pads[1][0], pads[1][1],
                pads[2][0], pads[2][1], 1]
-        call("milnce_bn_relu_gate_maxpool_fwd", ptr(y), ptr(ss), ptr(g), ptr(out), ptr(arg), *geo, stream())
-        ctx.save_for_backward(y, ss, g, mean, w, out, arg)
+        # pooled-side BN-backward partials (_GATED_POOL_STATS): the raw y at each arg-max, and the
+        # mask statistics the gating-sum pass left on gsum
+        mstat = getattr(gsum, "_milnce_mstat", None)
+        yr = (torch.empty((B, To, Ho, Wo, C), dtype=BF16, device=dev)
+              if mstat is not None and ld == C and _LAZY_POOL_DZ and _FUSE_BN_BWD else None)
+        call("milnce_bn_relu_gate_maxpool_fwd", ptr(y), ptr(ss), ptr(g), ptr(out), ptr(arg), *geo, ptr(yr), stream())
+        ctx.save_for_backward(y, ss, g, mean, w, out, arg, yr, mstat if yr is not None else None)
         ctx.geo, ctx.ld = geo, ld
         ctx.bias = bias
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        y, ss, g, mean, w, out, arg = ctx.saved_tensors
+        y, ss, g, mean, w, out, arg, yr, mstat = ctx.saved_tensors
         geo = ctx.geo
         B, T, H, W, C, To, Ho, Wo = geo[:8]
         dout = dout.contiguous()
@@ -2563,8 +2582,18 @@ class _GatedPool(torch.autograd.Function):
         call("milnce_gate_dot", ptr(dout), ptr(out), B, To * Ho * Wo, C, ptr(gs), stream())
         dmean, (dw,), (db,) = gate_fc_backward(gs, g, mean, [w], [ctx.bias], [C])
         nparts = _pool_nparts(B * T * H * W * (C // 8))
-        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
         lazy = _LAZY_POOL_DZ and _FUSE_BN_BWD
+        if yr is not None and lazy:
+            # partials from the pooled side (see _GATED_POOL_STATS); the apply pass still gathers
+            rows = To * Ho * Wo
+            splits = max(1, _ceil(rows, 64 * (256 // (C // 8))))
+            part = torch.empty((splits * B * 2 * C,), dtype=F32, device=dout.device)
+            call("milnce_gated_pool_bn_partials", ptr(dout), ptr(yr), ptr(g), ptr(dmean), ptr(ss), ptr(mstat), C, B,
+                 rows, T * H * W, splits, ptr(part), stream())
+            dz = _lazy_dz((B, T, H, W, C), dout.device, ("pool", dout, arg, geo, g, dmean, nparts))
+            attach_bn_partials(dz, part, splits * B, C)
+            return dz, None, dw, db, None, None
+        part = torch.empty((nparts * 2 * C,), dtype=F32, device=dout.device)
         dz = None if lazy else torch.empty((B, T, H, W, C), dtype=BF16, device=dout.device)
         call("milnce_maxpool_bwd_gated", ptr(dout), ptr(arg), ptr(dz), *geo, ptr(y), ctx.ld, ptr(ss), ptr(part),
              nparts, ptr(g), ptr(dmean), stream())

@@ -1191,12 +1191,100 @@ def test_gated_pool_matches_unfused():
 
 def test_lazy_pool_dz_matches_stored():
     """Gated pool backward with the producer's BN backward applied inside a second gather pass
-    (dz never stored) vs the stored-dz path: the same values, so the same gradients."""
+    (dz never stored) vs the stored-dz path: the same values, so the same gradients (partial sums
+    from the full-resolution gather in both: _GATED_POOL_STATS off)."""
     h = hip()
-    lazy = _gated_pool_grads(h, "_LAZY_POOL_DZ", True)
-    stored = _gated_pool_grads(h, "_LAZY_POOL_DZ", False)
+    old = h._GATED_POOL_STATS
+    h._GATED_POOL_STATS = False
+    try:
+        lazy = _gated_pool_grads(h, "_LAZY_POOL_DZ", True)
+        stored = _gated_pool_grads(h, "_LAZY_POOL_DZ", False)
+    finally:
+        h._GATED_POOL_STATS = old
     for a, b in zip(lazy, stored):
         assert rel_err(a, b) < 1e-5
+
+
+def test_gated_pool_stats_partials_in_model_path():
+    """The gated pool's BN-backward partial sums from the pooled side (_GATED_POOL_STATS: mask
+    statistics from the forward's gating-sum pass, yr from the pool forward) vs the full-resolution
+    gather: same forward, gradients to bf16 rounding (the old pass summed bf16-rounded dz)."""
+    h = hip()
+    new = _gated_pool_grads(h, "_GATED_POOL_STATS", True)
+    old = _gated_pool_grads(h, "_GATED_POOL_STATS", False)
+    assert torch.equal(new[0], old[0])
+    for a, b in zip(new[1:], old[1:]):
+        assert rel_err(a, b) < 5e-3
+
+
+def test_gated_pool_partials_from_pooled_side():
+    """milnce_bn_relu_gsum_mstat (gating sums + per-clip mask statistics) and
+    milnce_gated_pool_bn_partials (BN-backward partials of the gated pool's input BN over the pooled
+    tensors) against fp64 PyTorch references: dz = dx * g + dmean / thw with dx the pooled gradient
+    routed to the kernel's arg-max cells; the full-resolution gather pass (milnce_maxpool_bwd_gated,
+    which sums bf16-rounded dz) is checked against the same reference, more loosely."""
+    from mil_nce_howto100m_amd.ops._lib import lib, ptr, stream
+    torch.manual_seed(5)
+    h = hip()
+    B, T, H, W, C = 2, 4, 26, 26, 64
+    y = torch.randn(B, T, H, W, C, device=DEV).to(torch.bfloat16)
+    yf = y.float()
+    mean = yf.mean(dim=(0, 1, 2, 3))
+    invstd = 1.0 / (yf.var(dim=(0, 1, 2, 3), unbiased=False) + 1e-3).sqrt()
+    scale = torch.rand(C, device=DEV) + 0.5
+    shift = torch.randn(C, device=DEV) * 0.2
+    ss = torch.stack([mean, invstd, scale, shift]).reshape(-1).contiguous()
+    g = torch.rand(B, C, device=DEV) + 0.2
+    dmean = torch.randn(B, C, device=DEV)
+    thw = T * H * W
+    gsum = torch.zeros(B, C, device=DEV)
+    mstat = torch.empty(B, 2, C, device=DEV)
+    assert lib().milnce_bn_relu_gsum_mstat(ptr(y), C, ptr(ss), C, B, thw, ptr(gsum), ptr(mstat), stream()) == 0
+    t = yf * scale + shift
+    m = (t > 0).double()
+    xhat = ((yf - mean) * invstd).double()
+    ref_gsum = t.clamp_min(0).double().sum(dim=(1, 2, 3))
+    assert rel_err(gsum, ref_gsum.float()) < 1e-4
+    ref_s0, ref_s1 = m.sum(dim=(1, 2, 3)), (m * xhat).sum(dim=(1, 2, 3))
+    assert (mstat[:, 0].double() - ref_s0).abs().max().item() <= 2.0
+    assert rel_err(mstat[:, 1], ref_s1.float()) < 1e-3
+    # pool forward: pooled gate output, arg-max codes and the raw y there
+    (ph0, ph1), (pw0, pw1) = aten.tf_same_pad((3, 3), (2, 2))
+    Ho, Wo = h._pool_out(H, 3, 2, ph0, ph1), h._pool_out(W, 3, 2, pw0, pw1)
+    geo = [B, T, H, W, C, T, Ho, Wo, 1, 3, 3, 1, 2, 2, 0, 0, ph0, ph1, pw0, pw1, 1]
+    out = torch.empty((B, T, Ho, Wo, C), dtype=torch.bfloat16, device=DEV)
+    arg = torch.empty(out.shape, dtype=torch.uint8, device=DEV)
+    yr = torch.empty_like(out)
+    assert lib().milnce_bn_relu_gate_maxpool_fwd(ptr(y), ptr(ss), ptr(g), ptr(out), ptr(arg), *geo, ptr(yr),
+                                                 stream()) == 0
+    dout = torch.randn(out.shape, device=DEV).to(torch.bfloat16)
+    rows = T * Ho * Wo
+    splits = 3
+    part = torch.empty(splits * B * 2 * C, device=DEV)
+    assert lib().milnce_gated_pool_bn_partials(ptr(dout), ptr(yr), ptr(g), ptr(dmean), ptr(ss), ptr(mstat), C, B,
+                                               rows, thw, splits, ptr(part), stream()) == 0
+    p_new = part.view(-1, 2, C).double().sum(0)
+    nparts = 64
+    part_old = torch.empty(nparts * 2 * C, device=DEV)
+    assert lib().milnce_maxpool_bwd_gated(ptr(dout), ptr(arg), None, *geo, ptr(y), C, ptr(ss), ptr(part_old), nparts,
+                                          ptr(g), ptr(dmean), stream()) == 0
+    p_old = part_old.view(-1, 2, C).double().sum(0)
+    # reference: route dout to the coded cells (tap = 3 dh + dw of the window at (2 ho, 2 wo))
+    code = arg.long()
+    ho = torch.arange(Ho, device=DEV).view(1, 1, Ho, 1, 1)
+    wo = torch.arange(Wo, device=DEV).view(1, 1, 1, Wo, 1)
+    hi, wi = 2 * ho + code // 3, 2 * wo + code % 3
+    assert int(hi.max()) < H and int(wi.max()) < W  # no trailing-pad winner (zeros never beat a real cell)
+    bi = torch.arange(B, device=DEV).view(B, 1, 1, 1, 1).expand_as(code)
+    ti = torch.arange(T, device=DEV).view(1, T, 1, 1, 1).expand_as(code)
+    ci = torch.arange(C, device=DEV).view(1, 1, 1, 1, C).expand_as(code)
+    flat = (((bi * T + ti) * H + hi) * W + wi) * C + ci
+    dx = torch.zeros(B * T * H * W * C, dtype=torch.float64, device=DEV)
+    dx.index_add_(0, flat.reshape(-1), dout.double().reshape(-1))
+    dz = dx.view(B, T, H, W, C) * g.double().view(B, 1, 1, 1, C) + (dmean.double() / thw).view(B, 1, 1, 1, C)
+    ref = torch.stack([(dz * m).sum(dim=(0, 1, 2, 3)), (dz * m * xhat).sum(dim=(0, 1, 2, 3))])
+    assert rel_err(p_new, ref) < 1e-4, rel_err(p_new, ref)
+    assert rel_err(p_old, ref) < 1e-2, rel_err(p_old, ref)
 
 def test_gate_fc_backward_kernel():
     """One-launch SelfGating fc backward (csrc/gate.hip gate_fc_bwd_kernel) vs fp32 PyTorch GEMMs,
@@ -1333,14 +1421,14 @@ def test_pool_pair_forward_bitwise(shape, mode):
                 rc = lib().milnce_bn_relu_maxpool_fwd(ptr(x), ptr(ss), ptr(y), ptr(arg), *geo, ptr(yr), stream())
             else:
                 rc = lib().milnce_bn_relu_gate_maxpool_fwd(ptr(x), ptr(ss), ptr(gate), ptr(y), ptr(arg), *geo,
-                                                           stream())
+                                                           ptr(yr), stream())
             assert rc == 0
             torch.cuda.synchronize()
             res[on] = (y, arg, yr)
         finally:
             lib().milnce_pool_set_quad(1)
     assert torch.equal(res[1][0], res[0][0]) and torch.equal(res[1][1], res[0][1])
-    if mode == "bn":
+    if mode != "plain":  # the raw input at the arg-max (yr), pair and per-output kernels alike
         assert torch.equal(res[1][2], res[0][2])
     if mode == "plain":
         assert torch.equal(res[1][0].float(), aten.maxpool_tf_same(x.float(), (1, 3, 3), (1, 2, 2)))
