@@ -58,6 +58,10 @@ def test_bench_self_launches_n_ranks(world):
     assert c["world_size"] == world and c["buckets"] >= 1 and c["grad_mib"] > 0
     assert c["allreduce_ms"] > 0 and c["bucketed_allreduce_ms"] > 0 and c["allgather_ms"] > 0
     assert c["allreduce_bf16_ms"] > 0
+    # the link-aware bucket plan measured at start-up (--bucket_mb auto, parallel/bucket_plan.py)
+    bp = c["bucket_plan"]
+    assert bp["source"] == "measured" and bp["world_size"] == world
+    assert 0 < bp["tail_bytes"] <= bp["bucket_bytes"]
     assert c["allgather_kib"] == world * 2 * (1 + 4) * 512 * 4 / 1024  # W * b(1+K) rows * 512 fp32
 
 
