@@ -87,12 +87,17 @@ struct TwParams {
   const float* xss;
 };
 
-// REG = false: LDS-DMA ring of TW_NSTG stages (two boxes in flight). REG = true: register-staged
+// MODE 0: LDS-DMA ring of TW_NSTG stages (two boxes in flight). MODE 1 (REG): register-staged
 // boxes (NSUB + 2 16-B chunks per thread and box) in a 3-box register ring written into 2 LDS
 // slots: three boxes (~100 KiB per CU) in flight instead of two, for ~1.5x the latency cover at
-// the same LDS footprint of the DMA ring's two stages.
-template <int BN, bool REG>
+// the same LDS footprint of the DMA ring's two stages. MODE 2: the register ring with 3 LDS slots,
+// software-pipelined across boxes: the next box's first k-step fragments are read from LDS under
+// the current box's second k-step MFMAs (its slot was written a step earlier), so a step starts
+// its MFMAs right after the barrier instead of waiting for the fragment reads of all 8 waves
+// (counter passes, profiles/r6_twgrad_pmc.txt: 18 % of wave time waiting on LDS in MODE 1).
+template <int BN, int MODE>
 __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
+  constexpr bool REG = MODE >= 1;
   using G = TwGeom<BN>;
   constexpr int NBLK = BN / 16, CBLK = TW_CC / 16;  // 16-row n blocks, 16-channel c blocks
   constexpr int WK = CBLK, WN = TW_NW / WK;         // waves: 4 channel blocks x 2 n halves
@@ -211,6 +216,7 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
     mma(af1, bf1);
     __builtin_amdgcn_s_setprio(0);
   };
+  auto dimg_of = [&](int slot_i) -> const lds_char* { return lds + slot_i * G::STAGE_BYTES; };
 
   if constexpr (REG) {
     constexpr int NR = G::NSUB + 3;  // NSUB dY chunks, 2 halo chunks, the halo chunks' validity (.x)
@@ -282,30 +288,74 @@ __global__ __launch_bounds__(TW_NT, 1) void twgrad_kernel(TwParams p) {
         *(uint4*)(sx + r * 128 + tw_chunk(r, rch) * 16) = xv;
       }
     };
-    uint4 R0[NR], R1[NR], R2[NR];
-    rload(box_begin, R0);
-    rload(box_begin + 1, R1);
-    rload(box_begin + 2, R2);
-    rstore(R0, 0);
-    rload(box_begin + 3, R0);
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    // box j lives in register set j % 3 and LDS slot (j - box_begin) % 2. Every step issues its NR
-    // loads, also past box_end (out of range: no traffic): the compiler's vmcnt before a set's LDS
-    // write counts the loads issued after that set on every path into it, and a path that skipped
-    // the later steps' loads made it wait for the set loaded one step earlier instead of three
-    auto step = [&](int box, uint4 (&Rn)[NR]) {
-      const int i = box - box_begin;
-      if (box < box_end) {
-        compute(i & 1);
-        if (box + 1 < box_end) rstore(Rn, (i + 1) & 1);  // slot of box - 1: every wave finished it
-      }
-      rload(box + 4, Rn);
+    if constexpr (MODE == 1) {
+      uint4 R0[NR], R1[NR], R2[NR];
+      rload(box_begin, R0);
+      rload(box_begin + 1, R1);
+      rload(box_begin + 2, R2);
+      rstore(R0, 0);
+      rload(box_begin + 3, R0);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    };
-    for (int box = box_begin; box < box_end; box += 3) {
-      step(box, R1);
-      step(box + 1, R2);
-      step(box + 2, R0);
+      // box j lives in register set j % 3 and LDS slot (j - box_begin) % 2. Every step issues its NR
+      // loads, also past box_end (out of range: no traffic): the compiler's vmcnt before a set's LDS
+      // write counts the loads issued after that set on every path into it, and a path that skipped
+      // the later steps' loads made it wait for the set loaded one step earlier instead of three
+      auto step = [&](int box, uint4 (&Rn)[NR]) {
+        const int i = box - box_begin;
+        if (box < box_end) {
+          compute(i & 1);
+          if (box + 1 < box_end) rstore(Rn, (i + 1) & 1);  // slot of box - 1: every wave finished it
+        }
+        rload(box + 4, Rn);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      };
+      for (int box = box_begin; box < box_end; box += 3) {
+        step(box, R1);
+        step(box + 1, R2);
+        step(box + 2, R0);
+      }
+    } else {
+      // MODE 2: box j in LDS slot (j - box_begin) % 3, stored two steps before its compute, and in
+      // register set (j - box_begin) % 2 (loaded two steps before its store): two register sets
+      // instead of three, the third set's registers hold the next box's fragments.
+      uint4 RA[NR], RB[NR];
+      rload(box_begin, RA);
+      rload(box_begin + 1, RB);
+      rstore(RA, 0);
+      rload(box_begin + 2, RA);
+      rstore(RB, 1);
+      rload(box_begin + 3, RB);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      bf16x8 af0[NBW], bf0[KBW], af1[NBW], bf1[KBW];
+      load(dimg_of(0), dimg_of(0) + G::D_BYTES, 0, af0, bf0);
+      // step(box): k-step 1 of box from its slot si, the k-step-0 MFMAs, k-step 0 of box + 1 (its
+      // slot was written a step ago) read under the k-step-1 MFMAs, then box + 2 (in Rs) into the
+      // slot box - 1 used (every wave finished it before the last barrier) and box + 4 into Rs
+      // (issued on every path: uniform vmcnt counts, as in MODE 1)
+      auto pstep = [&](int box, int si, uint4(&Rs)[NR]) {
+        const int s1 = si == 2 ? 0 : si + 1, s2 = si == 0 ? 2 : si - 1;
+        if (box < box_end) {
+          load(dimg_of(si), dimg_of(si) + G::D_BYTES, 1, af1, bf1);
+          __builtin_amdgcn_s_setprio(1);
+          mma(af0, bf0);
+          __builtin_amdgcn_s_setprio(0);
+          if (box + 1 < box_end) load(dimg_of(s1), dimg_of(s1) + G::D_BYTES, 0, af0, bf0);
+          __builtin_amdgcn_s_setprio(1);
+          mma(af1, bf1);
+          __builtin_amdgcn_s_setprio(0);
+          if (box + 2 < box_end) rstore(Rs, s2);
+        }
+        rload(box + 4, Rs);
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      };
+      for (int box = box_begin; box < box_end; box += 6) {
+        pstep(box, 0, RA);
+        pstep(box + 1, 1, RB);
+        pstep(box + 2, 2, RA);
+        pstep(box + 3, 0, RB);
+        pstep(box + 4, 1, RA);
+        pstep(box + 5, 2, RB);
+      }
     }
   } else {
   // prologue: boxes 0 .. NSTG-2 in flight
@@ -360,18 +410,18 @@ bool tw_box(int T, int HW, int& bt, int& lbs) {
   return ok;
 }
 
-template <int BN, bool REG>
+template <int BN, int MODE>
 int launch_tw(TwParams& p, hipStream_t stream) {
   using G = TwGeom<BN>;
-  const int lds = REG ? 2 * G::STAGE_BYTES : G::LDS;
+  const int lds = MODE == 1 ? 2 * G::STAGE_BYTES : MODE == 2 ? 3 * G::STAGE_BYTES : G::LDS;
   static bool attr_set = false;
   if (!attr_set) {
-    HIP_RET(hipFuncSetAttribute((const void*)twgrad_kernel<BN, REG>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    HIP_RET(hipFuncSetAttribute((const void*)twgrad_kernel<BN, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 lds));
     attr_set = true;
   }
-  hipLaunchKernelGGL((twgrad_kernel<BN, REG>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT),
-                     lds_floor(twgrad_kernel<BN, REG>, lds), stream,
+  hipLaunchKernelGGL((twgrad_kernel<BN, MODE>), dim3(p.n_slices * p.c_chunks * p.splits), dim3(TW_NT),
+                     lds_floor(twgrad_kernel<BN, MODE>, lds), stream,
                      p);
   return (int)hipGetLastError();
 }
@@ -400,13 +450,14 @@ MILNCE_API int milnce_twgrad_plan(int B, int T, int H, int W, int Cin, int Cout,
 
 // dW of a (3,1,1) / stride 1 / padding (1,0,0) conv: the split slab is written to `slab`; with dw
 // != null it is also reduced (accumulated when accumulate != 0) into dw [Cout][Cin_param][3][1][1].
-// reg != 0: the register-staged variant (REG = true).
+// reg: 0 the LDS-DMA ring, 1 the register-staged boxes, 2 the same software-pipelined (MODE).
 // xss (register-staged kernel only, else null): x is a BN layer's raw conv output and the operand
 // its relu(x * scale + shift), xss = [mean, invstd, scale, shift][Cin] (see TwParams::xss)
 MILNCE_API int milnce_twgrad(const void* dy, int ldd, const void* x, float* slab, float* dw, int accumulate, int B,
                              int T, int H, int W, int Cin, int Cin_param, int Cout, int bn, int splits, int reg,
                              const float* xss, hipStream_t stream) {
-  if (!(bn == 64 || bn == 128 || bn == 192) || (xss != nullptr && !reg)) return (int)hipErrorInvalidValue;
+  if (!(bn == 64 || bn == 128 || bn == 192) || (xss != nullptr && !reg) || reg < 0 || reg > 2)
+    return (int)hipErrorInvalidValue;
   TwParams p;
   p.dy = (const bf16_t*)dy;
   p.x = (const bf16_t*)x;
@@ -431,14 +482,18 @@ MILNCE_API int milnce_twgrad(const void* dy, int ldd, const void* x, float* slab
   // per-clip byte offsets are 32-bit buffer offsets
   if ((long long)T * p.HW * (ldd > Cin ? ldd : Cin) * 2 > 0x7FFFFFF0LL) return (int)hipErrorInvalidValue;
   int rc;
-  if (reg) {
-    if (bn == 64) rc = launch_tw<64, true>(p, stream);
-    else if (bn == 128) rc = launch_tw<128, true>(p, stream);
-    else rc = launch_tw<192, true>(p, stream);
+  if (reg == 2) {
+    if (bn == 64) rc = launch_tw<64, 2>(p, stream);
+    else if (bn == 128) rc = launch_tw<128, 2>(p, stream);
+    else rc = launch_tw<192, 2>(p, stream);
+  } else if (reg) {
+    if (bn == 64) rc = launch_tw<64, 1>(p, stream);
+    else if (bn == 128) rc = launch_tw<128, 1>(p, stream);
+    else rc = launch_tw<192, 1>(p, stream);
   } else {
-    if (bn == 64) rc = launch_tw<64, false>(p, stream);
-    else if (bn == 128) rc = launch_tw<128, false>(p, stream);
-    else rc = launch_tw<192, false>(p, stream);
+    if (bn == 64) rc = launch_tw<64, 0>(p, stream);
+    else if (bn == 128) rc = launch_tw<128, 0>(p, stream);
+    else rc = launch_tw<192, 0>(p, stream);
   }
   if (rc) return rc;
   if (dw == nullptr) return 0;

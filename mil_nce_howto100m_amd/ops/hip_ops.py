@@ -1529,8 +1529,9 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
     def launch_with(tn, impl, occ, tk, target, accumulate):
         """Runs the wgrad into ``target``; with ``target`` None only the split slab is filled and
         (slab, splits, Npad, Kpad) returned for the caller's reduction."""
-        if impl >= 1000:  # temporal box wgrad: N tile impl % 1000, register-staged from 2000
-            return _twgrad(dy, x, plan, impl % 1000, target, accumulate, occ, int(impl >= 2000),
+        if impl >= 1000:  # temporal box wgrad: N tile impl % 1000, register-staged from 2000,
+            # software-pipelined across boxes from 3000
+            return _twgrad(dy, x, plan, impl % 1000, target, accumulate, occ, impl // 1000 - 1,
                            xss if impl >= 2000 else None)
         if impl >= 100:  # box-tiled halo wgrad, channel chunk impl - 100
             return _halo_wgrad(dy, x, plan, impl - 100, target, accumulate, occ)
@@ -1558,7 +1559,7 @@ def conv_wgrad(dy: torch.Tensor, x: torch.Tensor, plan: ConvPlan, out: Optional[
                 if plan.k == (3, 1, 1) and plan.Cin % 128 == 0:  # temporal boxes also take 128-channel chunks
                     cands += [(64, 228, occ, 0) for occ in _HALO_OCCS]
             if _twgrad_ok(plan, x):
-                cands += [(bn, base + bn, occ, 0) for base in (1000, 2000) for bn in _tw_tiles(plan.Cout)
+                cands += [(bn, base + bn, occ, 0) for base in (1000, 2000, 3000) for bn in _tw_tiles(plan.Cout)
                           for occ in _TW_OCCS]
             code = {c: i + 1 for i, c in enumerate(cands)}
             inv = {v: k for k, v in code.items()}

@@ -1509,7 +1509,7 @@ def test_step_group_prepack_matches_concat_pack(widths, cin):
 @pytest.mark.parametrize("B,T,HW,cin,cout", [(4, 8, 50, 192, 192), (4, 8, 25, 128, 128), (4, 4, 13, 96, 208),
                                              (8, 2, 7, 384, 384), (3, 5, 9, 24, 40), (2, 16, 10, 64, 64)])
 @pytest.mark.parametrize("bn", [64, 128, 192])
-@pytest.mark.parametrize("reg", [0, 1])
+@pytest.mark.parametrize("reg", [0, 1, 2])
 def test_temporal_box_wgrad(B, T, HW, cin, cout, bn, reg):
     """csrc/conv_twgrad.hip (3,1,1) weight gradient (boxes of frames x flattened positions with a
     3-frame halo, 64/128/192-wide output tiles, partial boxes / channel chunks / output tiles) vs the
@@ -1526,11 +1526,17 @@ def test_temporal_box_wgrad(B, T, HW, cin, cout, bn, reg):
     assert rel_err(out, ref) < 1e-4, rel_err(out, ref)
     h._twgrad(dy, x, plan, bn, out, 1, occ=2, reg=reg)  # accumulate, another split count
     assert rel_err(out, 2 * ref) < 1e-4
+    if reg == 2:  # the software-pipelined ring sums in MODE 1's order: bitwise the same
+        one, two = torch.zeros_like(out), torch.zeros_like(out)
+        h._twgrad(dy, x, plan, bn, one, 0, reg=1)
+        h._twgrad(dy, x, plan, bn, two, 0, reg=2)
+        assert torch.equal(one, two)
 
 
 @pytest.mark.parametrize("B,T,HW,cin,cout", [(4, 8, 13, 192, 192), (3, 5, 9, 24, 40)])
 @pytest.mark.parametrize("bn", [64, 192])
-def test_temporal_box_wgrad_bn_relu_operand(B, T, HW, cin, cout, bn):
+@pytest.mark.parametrize("reg", [1, 2])
+def test_temporal_box_wgrad_bn_relu_operand(B, T, HW, cin, cout, bn, reg):
     """The register-staged temporal wgrad applying its input's BN-ReLU itself (xss: the producer's
     [mean, invstd, scale, shift], padding rows kept zero) is bitwise the same kernel on the
     materialised z = relu(y * scale + shift) (bn_relu_apply)."""
@@ -1546,8 +1552,8 @@ def test_temporal_box_wgrad_bn_relu_operand(B, T, HW, cin, cout, bn):
     plan = h.conv_plan(y.shape, (cout, cin, 3, 1, 1), (1, 1, 1), (1, 0, 0))
     a = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
     b = torch.zeros((cout, cin, 3, 1, 1), device=DEV)
-    h._twgrad(dy, z, plan, bn, a, 0, reg=1)
-    h._twgrad(dy, y, plan, bn, b, 0, reg=1, xss=ss)
+    h._twgrad(dy, z, plan, bn, a, 0, reg=reg)
+    h._twgrad(dy, y, plan, bn, b, 0, reg=reg, xss=ss)
     assert torch.equal(a, b)
 
 
