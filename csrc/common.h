@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define MILNCE_API extern "C" __attribute__((visibility("default")))
 
@@ -136,6 +137,21 @@ __device__ __forceinline__ int xcd_remap(int id, int nblocks) {
 // s_barrier, with a compiler memory clobber. Unlike __syncthreads() it does not drain
 // outstanding global loads (vmcnt), so register prefetches stay in flight across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Host: split count of a persistent kernel whose ntiles x splits workgroups share a box range
+// equally: at most `target` workgroups (floor), so no last round of a few workgroups that each run a
+// full share while the rest of the chip idles (the ceil overshoot by up to ntiles - 1 workgroups
+// doubled or added a third round to the temporal / halo wgrads at their one-workgroup-per-CU
+// residency). MILNCE_SPLIT_CEIL=1 restores the rounded-up count (A/B).
+static inline long long fill_splits(long long target, long long ntiles) {
+  static int ceil_mode = -1;
+  if (ceil_mode < 0) {
+    const char* e = getenv("MILNCE_SPLIT_CEIL");
+    ceil_mode = (e != nullptr && e[0] == '1') ? 1 : 0;
+  }
+  const long long s = ceil_mode ? (target + ntiles - 1) / ntiles : target / ntiles;
+  return s < 1 ? 1 : s;
+}
 
 // Host: device scratch (floats) for kernels that stage partial results between launches of ONE
 // API call -- one growing buffer per (purpose slot, stream, device), so reuse is ordered by the

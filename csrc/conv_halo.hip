@@ -362,7 +362,7 @@ MILNCE_API int milnce_halo_wgrad_plan(int B, int T, int H, int W, int Cin, int C
   const int nboxes = B * ((T + bx.bt - 1) / bx.bt) * ((H + bx.bh - 1) / bx.bh) * ((W + bx.bw - 1) / bx.bw);
   const int ntiles = ((Cout + bn - 1) / bn) * ((Cin + cc - 1) / cc);
   const int target = blocks_target > 0 ? blocks_target : 512;
-  int splits = (target + ntiles - 1) / ntiles;
+  int splits = (int)fill_splits(target, ntiles);
   if (splits > nboxes) splits = nboxes;
   if (splits < 1) splits = 1;
   *splits_out = splits;

@@ -440,7 +440,7 @@ MILNCE_API int milnce_twgrad_plan(int B, int T, int H, int W, int Cin, int Cout,
   if (!tw_box(T, H * W, bt, lbs)) return (int)hipErrorInvalidValue;
   const long long nboxes = (long long)B * ((T + bt - 1) / bt) * ((H * W + (1 << lbs) - 1) >> lbs);
   const int ntiles = ((Cout + bn - 1) / bn) * ((Cin + TW_CC - 1) / TW_CC);
-  long long splits = ((blocks_target > 0 ? blocks_target : 256) + ntiles - 1) / ntiles;
+  long long splits = fill_splits(blocks_target > 0 ? blocks_target : 256, ntiles);
   if (splits > nboxes) splits = nboxes;
   if (splits < 1) splits = 1;
   *splits_out = (int)splits;

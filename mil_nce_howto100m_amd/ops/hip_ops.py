@@ -223,8 +223,20 @@ _WIDE_IMPLS = {96: (3, 4), 160: (3, 4), 192: (3, 4, 5)}
 _FWD_WGS_TUNE = tuple(int(v) for v in os.environ.get("MILNCE_FWD_WGS_TUNE", "2,3").split(","))
 
 
+# Persistent grids split their work statically over the workgroups, so a count just above the
+# resident capacity (wgs per CU x CUs, rounded UP to a multiple of the N tiles) leaves a last round
+# of a few workgroups that each run a full share while the chip idles. Round down instead
+# (csrc/common.h fill_splits, the same rule for the halo / temporal wgrad split counts);
+# MILNCE_SPLIT_CEIL=1 restores the rounded-up counts (A/B).
+_SPLIT_CEIL = os.environ.get("MILNCE_SPLIT_CEIL", "0") == "1"
+
+
+def _fill(target: int, ntiles: int) -> int:
+    return max(1, _ceil(target, ntiles) if _SPLIT_CEIL else target // ntiles)
+
+
 def _grid_for(M: int, npad: int, bn: int, wgs: int) -> int:
-    return max(1, min(_ceil(M, 128), _ceil(wgs * _NUM_CU, npad // bn)))
+    return max(1, min(_ceil(M, 128), _fill(wgs * _NUM_CU, npad // bn)))
 
 
 def _stats_rows(M: int, npad: int, bn: int) -> int:
@@ -396,7 +408,7 @@ def _fwd_tiles(M: int, N: int, K: int) -> Tuple[int, int, int, int, int]:
     kpad = _ceil(K, bk) * bk
     m_tiles = _ceil(M, 128)
     n_tiles = npad // bn
-    grid_m = max(1, min(m_tiles, _ceil(_FWD_WGS_PER_CU * _NUM_CU, n_tiles)))
+    grid_m = max(1, min(m_tiles, _fill(_FWD_WGS_PER_CU * _NUM_CU, n_tiles)))
     return bn, bk, npad, kpad, grid_m
 
 
@@ -1122,7 +1134,7 @@ def _wgrad_geom(Cout: int, Ktot: int, M: int, tn: int, tk: int, occ: int = 4) ->
     npad = _ceil(Cout, tn) * tn
     kpad = _ceil(Ktot, tk) * tk
     tiles = (npad // tn) * (kpad // tk)
-    splits = max(1, min(_ceil(occ * _GRID_CU[0], tiles), _ceil(M, 32 * 8)))
+    splits = max(1, min(_fill(occ * _GRID_CU[0], tiles), _ceil(M, 32 * 8)))
     return npad, kpad, splits
 
 

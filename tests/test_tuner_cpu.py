@@ -42,11 +42,19 @@ def test_wgrad_split_geometry():
         npad, kpad, splits = h._wgrad_geom(192, 576, 5_120_000, 96, 192, occ)
         assert npad == 192 and kpad == 576
         tiles = (npad // 96) * (kpad // 192)
-        # enough workgroups for `occ` per CU, never more splits than 256-row chunks
-        assert splits * tiles >= min(occ * h._NUM_CU, tiles * (5_120_000 // 256))
+        # as many workgroups as `occ` per CU hold without a partial last round (rounded down to
+        # whole splits), never more splits than 256-row chunks
+        assert occ * h._NUM_CU - tiles < splits * tiles <= occ * h._NUM_CU
         assert splits <= h._ceil(5_120_000, 256)
     # tiny reduction: one split
     assert h._wgrad_geom(64, 64, 100, 64, 64, 4)[2] == 1
+
+
+def test_persistent_grids_round_down():
+    """Persistent grids and split counts fill the resident capacity without overshooting it
+    (hip_ops._fill, csrc/common.h fill_splits): 512 target workgroups over 3 N tiles -> 170 each."""
+    assert h._fill(512, 3) == 170 and h._fill(512, 1) == 512 and h._fill(2, 3) == 1
+    assert h._grid_for(5_120_000, 192, 64, 2) * 3 <= 2 * h._NUM_CU
 
 
 def test_grad_sink_deferral_bookkeeping():
