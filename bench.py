@@ -99,12 +99,11 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
-    # A/B knob: the whole step on a high-priority stream (the side stream's weight-gradient
-    # workgroups then lose the dispatch arbitration to the main chain's)
-    prio_ctx = None
-    if cuda and os.environ.get("MILNCE_MAIN_PRIO", "0") == "1":
-        prio_ctx = torch.cuda.stream(torch.cuda.Stream(device=ctx.device, priority=-1))
-        prio_ctx.__enter__()
+    # the steps run on a high-priority stream, as in the trainer's loop (utils/streams.py
+    # MainStream; MILNCE_MAIN_PRIO=0 keeps the default stream)
+    from mil_nce_howto100m_amd.utils import MainStream
+    main_stream = MainStream(ctx.device)
+    main_stream.__enter__()
 
     step = 0
     if opts.warmup == 0 and cuda:
@@ -214,7 +213,9 @@ def main():
                 out["comm"]["bucket_plan"] = trainer.comm_plan.as_dict()
         if cuda:
             out["kernel_lib"] = _native_lib()
+            out["main_stream_priority"] = main_stream.priority
         print(json.dumps(out), flush=True)
+    main_stream.__exit__(None, None, None)
     pdist.destroy()
     return 0
 

@@ -29,7 +29,7 @@ from ..models import S3D
 from ..parallel import bucket_plan
 from ..parallel import dist as pdist
 from ..parallel.ddp import BufferBroadcaster, GradBucketer, broadcast_parameters
-from ..utils import StepTimer, Watchdog
+from ..utils import MainStream, StepTimer, Watchdog
 from . import checkpoint as ckpt
 from .logging import MetricsLogger, log, train_line
 from .optim import FlatAdam, FlatSGD, cosine_schedule_with_warmup
@@ -314,10 +314,21 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
             log("=> no checkpoint found at '{}'".format(cdir), args, ctx.rank)
     total_bs = local_bs * ctx.world_size  # clips per step over all ranks
     log("Starting training loop for rank: {}, total batch size: {}".format(ctx.rank, total_bs), args, ctx.rank)
-    last = {}
     watchdog = Watchdog(getattr(args, "watchdog_s", 0.0), ctx.rank,
                         dump_dir=getattr(args, "log_root", "log") or "log").start()
     eval_every = max(1, total_bs // 512)  # main_distributed.py:188
+    try:
+        with MainStream(ctx.device):  # the steps on a high-priority stream (utils/streams.py)
+            return _epochs(args, ctx, trainer, feed, metrics, cdir, watchdog, start_epoch, start_step,
+                           steps_per_epoch, total_bs, eval_every)
+    finally:
+        watchdog.stop()
+
+
+def _epochs(args, ctx, trainer, feed, metrics, cdir, watchdog, start_epoch, start_step, steps_per_epoch, total_bs,
+            eval_every) -> Dict[str, float]:
+    """The epoch loop of run_training (main_distributed.py:185-200)."""
+    last = {}
     for epoch in range(start_epoch, args.epochs):
         if args.evaluate and epoch % eval_every == 0 and not (epoch == start_epoch and start_step):
             from .evaluation import evaluate_hmdb_during_training
@@ -355,5 +366,4 @@ def run_training(args, ctx: Optional[pdist.DistContext] = None) -> Dict[str, flo
         pdist.barrier()
         if getattr(args, "stop_epoch", 0) and epoch + 1 >= args.stop_epoch:
             break
-    watchdog.stop()
     return last
