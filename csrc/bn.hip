@@ -164,9 +164,9 @@ __global__ __launch_bounds__(FIN_CH * FIN_RG) void bn_finalize_group_kernel(FinG
 // WRITE = false (bn_relu_gsum_kernel): the SelfGating channel sums only, a read-only reduction
 // (the lazy gate inputs' z is applied by the gate_scale pass / the consumer instead).
 // MSTAT (bn_relu_gsum_mstat_kernel, with WRITE = false): also the per-clip mask statistics of this
-// BN, mpart[split][b][2][C] = (sum mask, sum mask * xhat) (mask = y * scale + shift > 0, as the BN
-// backward's), which a gated pool's backward needs for its BN-backward partial sums
-// (gated_pool_bn_partials_kernel).
+// BN, mpart[split][b][2][C] = (sum mask, sum mask * y) (mask = y * scale + shift > 0, as the BN
+// backward's; bn_mstat_sum_kernel turns the second into sum mask * xhat), which a gated pool's
+// backward needs for its BN-backward partial sums (gated_pool_bn_partials_kernel).
 template <bool WRITE, bool MSTAT = false>
 __device__ __forceinline__ void bn_relu_apply_body(
     const bf16_t* __restrict__ y, int ldy, bf16_t* __restrict__ z, int ldz, const float* __restrict__ ss,
@@ -183,15 +183,13 @@ __device__ __forceinline__ void bn_relu_apply_body(
   const int r_end = min(rows_per_b, r_begin + rows_per_block);
   const int c0 = cc * 8;
   float sc[8], sh[8], acc[8];
-  float mu[MSTAT ? 8 : 1], is[MSTAT ? 8 : 1], m0[MSTAT ? 8 : 1], m1[MSTAT ? 8 : 1];
+  float m0[MSTAT ? 8 : 1], m1[MSTAT ? 8 : 1];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     sc[k] = active ? ss[2 * C + c0 + k] : 0.f;
     sh[k] = active ? ss[3 * C + c0 + k] : 0.f;
     acc[k] = 0.f;
     if constexpr (MSTAT) {
-      mu[k] = active ? ss[c0 + k] : 0.f;
-      is[k] = active ? ss[C + c0 + k] : 0.f;
       m0[k] = 0.f;
       m1[k] = 0.f;
     }
@@ -213,10 +211,10 @@ __device__ __forceinline__ void bn_relu_apply_body(
         unpack8(v[u], f);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          if constexpr (MSTAT) {
+          if constexpr (MSTAT) {  // sum mask and sum mask * y; xhat's affine map applied once at the end
             const bool m = f[k] * sc[k] + sh[k] > 0.f;
             m0[k] += m ? 1.f : 0.f;
-            m1[k] += m ? (f[k] - mu[k]) * is[k] : 0.f;
+            m1[k] += m ? f[k] : 0.f;
           }
           f[k] = fmaxf(f[k] * sc[k] + sh[k], 0.f);
           acc[k] += f[k];
@@ -255,7 +253,7 @@ __device__ __forceinline__ void bn_relu_apply_body(
         for (int k = 0; k < 8; ++k) {
           float v = h == 0 ? m0[k] : m1[k];
           for (int j = 1; j < rpi; ++j) v += red[k * 256 + j * cpr + cc];
-          mr[h * C + k] = v;
+          mr[h * C + k] = v;  // h = 1: sum mask * y (this row's part of sum mask * xhat, see below)
         }
       }
     }
@@ -595,6 +593,24 @@ MILNCE_API int milnce_bn_relu_apply(const void* y, int ldy, void* z, int ldz, co
   return (int)hipGetLastError();
 }
 
+// mstat[b][0][c] = sum over splits of mpart's sum mask, mstat[b][1][c] = invstd * (sum mask * y -
+// mean * sum mask) = sum mask * xhat (in split order)
+__global__ void bn_mstat_sum_kernel(float* __restrict__ mstat, const float* __restrict__ mpart, int nsplit, int B,
+                                    int C, const float* __restrict__ ss) {
+  const long long n = (long long)B * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / C, c = i - b * C;
+    float s0 = 0.f, s1 = 0.f;
+    for (int sp = 0; sp < nsplit; ++sp) {
+      const float* r = mpart + (((long long)sp * B + b) * 2) * C + c;
+      s0 += r[0];
+      s1 += r[C];
+    }
+    mstat[(b * 2) * C + c] = s0;
+    mstat[(b * 2 + 1) * C + c] = ss[C + c] * (s1 - ss[c] * s0);
+  }
+}
+
 // milnce_bn_relu_apply's gating-sums-only pass (z not written) that also leaves the per-clip mask
 // statistics mstat [B][2][C] = (sum mask, sum mask * xhat) (overwritten); gsum [B][C] is added to.
 // Not inside a HIP graph capture (the deterministic partial rows need the stream scratch).
@@ -612,9 +628,8 @@ MILNCE_API int milnce_bn_relu_gsum_mstat(const void* y, int ldy, const float* ss
   long long g = (n + 255) / 256;
   hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, gsum, part, splits,
                      n, 1);
-  g = (2 * n + 255) / 256;
-  hipLaunchKernelGGL(bn_gsum_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, mstat, mpart,
-                     splits, 2 * n, 0);
+  hipLaunchKernelGGL(bn_mstat_sum_kernel, dim3((int)(g < 4096 ? g : 4096)), dim3(256), 0, stream, mstat, mpart,
+                     splits, B, C, ss);
   return (int)hipGetLastError();
 }
 
