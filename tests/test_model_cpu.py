@@ -100,3 +100,10 @@ def test_space_to_depth_forward_matches_ncdhw_oracle():
         f = m(v, None, mode="video", mixed5c=True)
         ref = ref_s3d.s3d_video(sd, v, training=training, mixed5c=True)
         assert torch.allclose(f, ref, rtol=1e-8, atol=1e-9), (training, (f - ref).abs().max())
+
+
+def test_main_stream_on_cpu_is_a_no_op():
+    """utils/streams.py MainStream does nothing for a CPU device (the gloo / CPU runs)."""
+    from mil_nce_howto100m_amd.utils import MainStream
+    with MainStream(torch.device("cpu")) as ms:
+        assert not ms.enabled and ms.priority == 0
